@@ -1,0 +1,117 @@
+"""ctypes bindings of the two in-tree native libraries (include/ggp.h, include/ggp_host.h).
+
+The device engine is the product path: there is no Python or CPU fallback.  If
+lib/libggp.so is missing or cannot be loaded, ``engine()`` raises -- loudly -- rather
+than silently computing something else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_PKG, "lib")
+
+GGP_OK, GGP_EINVAL, GGP_ENAN, GGP_EDEV, GGP_ENOMEM = 0, 1, 2, 3, 4
+N_PARAMS = 11
+STATE = 20
+KERNELS = {"auto": 0, "lane": 1, "group": 2}
+
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+
+
+class ForestDesc(ctypes.Structure):
+    """ggp_forest_desc (include/ggp.h)."""
+    _fields_ = [
+        ("n_cells", ctypes.c_int64), ("n_rows", ctypes.c_int64),
+        ("row_offset", c_int64_p), ("parent", c_int32_p), ("daughter1", c_int32_p),
+        ("daughter2", c_int32_p), ("segment", c_int32_p),
+        ("time", c_double_p), ("log_length", c_double_p), ("fp", c_double_p),
+        ("root_mean_xg", ctypes.c_double * 2), ("root_var_xg", ctypes.c_double * 2),
+        ("leaf_mean_xg", ctypes.c_double * 2), ("leaf_var_xg", ctypes.c_double * 2),
+        ("noise_scaled", ctypes.c_int32), ("division_binomial", ctypes.c_int32),
+        ("fp_auto", ctypes.c_double), ("device", ctypes.c_int32), ("kernel", ctypes.c_int32),
+    ]
+
+
+class ParamSetC(ctypes.Structure):
+    """ggp_param_set (include/ggp_host.h)."""
+    _fields_ = [
+        ("name", (ctypes.c_char * 16) * N_PARAMS),
+        ("kind", ctypes.c_int32 * N_PARAMS), ("set", ctypes.c_int32 * N_PARAMS),
+        ("init", ctypes.c_double * N_PARAMS), ("step", ctypes.c_double * N_PARAMS),
+        ("lower", ctypes.c_double * N_PARAMS), ("upper", ctypes.c_double * N_PARAMS),
+    ]
+
+
+# every symbol each header declares (tests check the exports against this list)
+ENGINE_SYMBOLS = {
+    "ggp_forest_create": (ctypes.c_int, [ctypes.POINTER(ForestDesc), ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_forest_destroy": (None, [ctypes.c_void_p]),
+    "ggp_total_loglik": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p, c_int64_p, c_int64_p]),
+    "ggp_total_loglik_async": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "ggp_loglik_result": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_int64_p, c_int64_p]),
+    "ggp_predict": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, c_double_p,
+                                   c_double_p, c_double_p]),
+    "ggp_reset_state": (ctypes.c_int, [ctypes.c_void_p]),
+    "ggp_get_state": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "ggp_last_launch_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                               c_int64_p, ctypes.c_int32, c_int32_p]),
+    "ggp_forest_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int32_p]),
+    "ggp_device_count": (ctypes.c_int, [c_int32_p]),
+    "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "ggp_version": (ctypes.c_char_p, []),
+}
+
+HOST_SYMBOLS = {
+    "ggp_host_last_error": (ctypes.c_char_p, []),
+    "ggp_csv_config_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_csv_config_free": (None, [ctypes.c_void_p]),
+    "ggp_csv_config_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "ggp_param_file_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.POINTER(ParamSetC)]),
+    "ggp_dataset_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_dataset_free": (None, [ctypes.c_void_p]),
+    "ggp_dataset_n_cells": (ctypes.c_int64, [ctypes.c_void_p]),
+    "ggp_dataset_n_rows": (ctypes.c_int64, [ctypes.c_void_p]),
+    "ggp_dataset_segments": (ctypes.c_int, [ctypes.c_void_p, c_int32_p, ctypes.c_int32, c_int32_p]),
+    "ggp_forest_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_host_forest_free": (None, [ctypes.c_void_p]),
+    "ggp_host_forest_desc": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ForestDesc)]),
+    "ggp_host_forest_cell_id": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_int64]),
+    "ggp_host_forest_parent_id": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_int64]),
+    "ggp_host_forest_n_roots": (ctypes.c_int64, [ctypes.c_void_p]),
+    "ggp_synthetic_forest": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+}
+
+_cache: dict = {}
+
+
+def _load(name: str, table: dict):
+    if name in _cache:
+        return _cache[name]
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -m gfp_gaussian_process_amd.build_ext` "
+            "(there is no CPU fallback for the likelihood engine)")
+    lib = ctypes.CDLL(path)
+    for sym, (res, args) in table.items():
+        fn = getattr(lib, sym)
+        fn.restype = res
+        fn.argtypes = args
+    _cache[name] = lib
+    return lib
+
+
+def engine():
+    """libggp.so (HIP, gfx950)."""
+    return _load("libggp.so", ENGINE_SYMBOLS)
+
+
+def host():
+    """libggp_host.so (host ingest)."""
+    return _load("libggp_host.so", HOST_SYMBOLS)

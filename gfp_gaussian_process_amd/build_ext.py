@@ -1,0 +1,86 @@
+"""Compile the native libraries in-tree (no JIT cache, no pip install).
+
+  lib/libggp.so       HIP engine for gfx950 (hipcc --offload-arch=gfx950)   include/ggp.h
+  lib/libggp_host.so  host ingest, plain C++17 (g++)                        include/ggp_host.h
+  lib/ggp             C++ CLI mirroring the reference's main.cpp modes
+
+``python -m gfp_gaussian_process_amd.build_ext`` or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+INC = os.path.join(ROOT, "include")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = "gfx950"
+
+# -ffp-contract=off: evaluate the reference's expressions without FMA contraction (the
+# reference is built for plain x86-64, src/Makefile:2); DESIGN.md "Parity".
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
+             "-Wall", "-Wno-unused-function"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall"]
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"build step failed: {' '.join(cmd[:3])} ...")
+
+
+def _newer(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return False
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> dict:
+    os.makedirs(LIB, exist_ok=True)
+    out = {}
+    # --- device engine ---
+    eng_src = os.path.join(CSRC, "ggp_engine.hip")
+    eng_deps = [eng_src, os.path.join(CSRC, "ggp_device.h"), os.path.join(CSRC, "dawson_table.inc"),
+                os.path.join(INC, "ggp.h")]
+    for extra in ("ggp_group.h", "ggp_predict.h"):
+        p = os.path.join(CSRC, extra)
+        if os.path.exists(p):
+            eng_deps.append(p)
+    eng = os.path.join(LIB, "libggp.so")
+    if force or not _newer(eng, eng_deps):
+        _run([HIPCC, *HIP_FLAGS, "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src], verbose)
+    out["libggp"] = eng
+    # --- host ingest ---
+    host_src = os.path.join(CSRC, "host", "ggp_host.cpp")
+    host = os.path.join(LIB, "libggp_host.so")
+    if force or not _newer(host, [host_src, os.path.join(INC, "ggp_host.h"), os.path.join(INC, "ggp.h")]):
+        cxx = shutil.which("g++") or "g++"
+        _run([cxx, *CXX_FLAGS, "-shared", f"-I{INC}", "-o", host, host_src, "-lpthread"], verbose)
+    out["libggp_host"] = host
+    # --- CLI ---
+    cli_src = os.path.join(CSRC, "host", "ggp_cli.cpp")
+    if os.path.exists(cli_src):
+        cli = os.path.join(LIB, "ggp")
+        deps = [cli_src, host_src, os.path.join(INC, "ggp.h"), os.path.join(INC, "ggp_host.h")]
+        nm = os.path.join(CSRC, "host", "ggp_nelder_mead.h")
+        if os.path.exists(nm):
+            deps.append(nm)
+        if force or not _newer(cli, deps + [eng]):
+            _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", "-o", cli, cli_src, host_src,
+                  f"-L{LIB}", "-lggp", "-Wl,-rpath,$ORIGIN", "-lpthread"], verbose)
+        out["cli"] = cli
+    return out
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

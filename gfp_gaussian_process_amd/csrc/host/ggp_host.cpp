@@ -1,0 +1,689 @@
+// ggp_host.cpp -- host-side forest ingest with the reference's data-model semantics.
+// See include/ggp_host.h for the function <-> reference mapping.
+#include "ggp_host.h"
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+// ---- string helpers with the reference's exact semantics (utils.h:143-225) -------------
+std::vector<std::string> split_at(std::string s, const std::string &delim)
+{   // split_string_at (utils.h:206-215)
+    std::vector<std::string> out;
+    size_t pos;
+    while ((pos = s.find(delim)) != std::string::npos) {
+        out.push_back(s.substr(0, pos));
+        s.erase(0, pos + delim.length());
+    }
+    out.push_back(s);
+    return out;
+}
+
+std::string trim_ref(const std::string &str, char c = ' ')
+{   // trim (utils.h:217-225): strips leading `c`, trailing ' ' only
+    size_t first = str.find_first_not_of(c);
+    if (first == std::string::npos) return str;
+    size_t last = str.find_last_not_of(' ');
+    return str.substr(first, last - first + 1);
+}
+
+double stod_ref(const std::string &s)
+{   // std::stod semantics (leading whitespace, trailing junk ignored, ERANGE throws)
+    const char *p = s.c_str();
+    char *end = nullptr;
+    errno = 0;
+    double d = std::strtod(p, &end);
+    if (end == p) throw std::invalid_argument("stod");
+    if (errno == ERANGE) throw std::out_of_range("stod");
+    return d;
+}
+
+double stod_reject_nan(const std::string &s)
+{   // utils.h:143-149
+    double d = stod_ref(s);
+    if (std::isnan(d)) throw std::invalid_argument("String is Nan");
+    return d;
+}
+
+int stoi_ref(const std::string &s)
+{   // std::stoi semantics
+    const char *p = s.c_str();
+    char *end = nullptr;
+    errno = 0;
+    long v = std::strtol(p, &end, 10);
+    if (end == p) throw std::invalid_argument("stoi");
+    if (errno == ERANGE || v < INT32_MIN || v > INT32_MAX) throw std::out_of_range("stoi");
+    return (int)v;
+}
+
+bool string2bool(const std::string &s)
+{   // utils.h:151-160
+    if (s == "True" || s == "true" || s == "TRUE" || s == "1") return true;
+    if (s == "False" || s == "false" || s == "FALSE" || s == "0") return false;
+    throw std::invalid_argument("no valid bool conversion of " + s);
+}
+
+std::string remove_last_decimal(const std::string &str)
+{   // moma_input.h:320-338
+    for (char ch : str)
+        if (!isdigit((unsigned char)ch) && ch != '.') return str;
+    std::vector<std::string> parts = split_at(str, ".");
+    const std::string &last = parts.back();
+    for (char ch : last)
+        if (ch != '0') return str;
+    return std::to_string(stoi_ref(str));
+}
+
+}  // namespace
+
+// ---- CSVconfig (CSVconfig.h:6-98) ------------------------------------------------------
+struct ggp_csv_config {
+    std::string time_col = "time";
+    double rescale_time = 1.;
+    std::string length_col = "length";
+    bool length_islog = false;
+    std::string fp_col = "gfp";
+    double fp_auto = 0;
+    std::string delm = ",";
+    std::string segment_col = "";
+    std::string filter_col = "";
+    std::vector<std::string> cell_tags{"cell_id"};
+    std::vector<std::string> parent_tags{"parent_id"};
+};
+
+// ---- dataset: read_data output, cells in input order -----------------------------------
+namespace {
+struct Cell {
+    std::string id, parent_id;
+    std::vector<double> time, log_length, fp;
+    std::vector<int32_t> segment;
+};
+}  // namespace
+
+struct ggp_dataset {
+    std::vector<Cell> cells;
+    double fp_auto = 0;
+};
+
+struct ggp_host_forest {
+    std::vector<std::string> ids, parent_ids;
+    std::vector<int64_t> row_off;
+    std::vector<int32_t> parent, d1, d2, segment;
+    std::vector<double> time, log_length, fp;
+    double root_mean[2] = {0, 0}, root_var[2] = {0, 0}, leaf_mean[2] = {0, 0}, leaf_var[2] = {0, 0};
+    int32_t noise_scaled = 1, division_binomial = 1;
+    double fp_auto = 0;
+    int64_t n_roots = 0;
+};
+
+extern "C" const char *ggp_host_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ggp_csv_config_load(const char *path, ggp_csv_config **out)
+{
+    if (!out) return fail(GGP_EINVAL, "null out");
+    auto *c = new ggp_csv_config();
+    if (path && *path) {
+        std::ifstream fin(path);
+        std::string line;
+        try {
+            while (std::getline(fin, line)) {
+                if (line.empty() || line[0] == '#') continue;
+                std::vector<std::string> parts = split_at(line, "=");
+                if (parts.size() < 2) throw std::invalid_argument("missing '=' in: " + line);
+                parts[0] = trim_ref(parts[0]);
+                parts[1] = trim_ref(parts[1]);
+                const std::string &k = parts[0], &v = parts[1];
+                if (k == "time_col") c->time_col = v;
+                else if (k == "rescale_time") c->rescale_time = stod_ref(v);
+                else if (k == "length_col") c->length_col = v;
+                else if (k == "length_islog") c->length_islog = string2bool(v);
+                else if (k == "fp_col") c->fp_col = v;
+                else if (k == "fp_auto") c->fp_auto = stod_ref(v);
+                else if (k == "delm") c->delm = v;
+                else if (k == "cell_tags" || k == "parent_tags") {
+                    std::vector<std::string> &tags = (k == "cell_tags") ? c->cell_tags : c->parent_tags;
+                    tags.clear();
+                    for (auto &s : split_at(v, ",")) tags.push_back(trim_ref(s));
+                } else if (k == "segment_col") c->segment_col = v;
+                else if (k == "filter_col") c->filter_col = v;
+            }
+        } catch (std::exception &e) {
+            delete c;
+            return fail(GGP_EINVAL, std::string("(CSVconfig) ERROR: ") + e.what());
+        }
+    }
+    *out = c;
+    return GGP_OK;
+}
+
+extern "C" void ggp_csv_config_free(ggp_csv_config *c) { delete c; }
+
+extern "C" int ggp_csv_config_get(const ggp_csv_config *c, const char *key, char *buf, size_t buflen)
+{
+    if (!c || !key || !buf || !buflen) return GGP_EINVAL;
+    std::string v;
+    std::string k(key);
+    auto join = [](const std::vector<std::string> &t) {
+        std::string s;
+        for (size_t i = 0; i < t.size(); ++i) s += (i ? "," : "") + t[i];
+        return s;
+    };
+    char tmp[64];
+    if (k == "time_col") v = c->time_col;
+    else if (k == "length_col") v = c->length_col;
+    else if (k == "fp_col") v = c->fp_col;
+    else if (k == "delm") v = c->delm;
+    else if (k == "segment_col") v = c->segment_col;
+    else if (k == "filter_col") v = c->filter_col;
+    else if (k == "rescale_time") { snprintf(tmp, sizeof tmp, "%.17g", c->rescale_time); v = tmp; }
+    else if (k == "fp_auto") { snprintf(tmp, sizeof tmp, "%.17g", c->fp_auto); v = tmp; }
+    else if (k == "length_islog") v = c->length_islog ? "1" : "0";
+    else if (k == "cell_tags") v = join(c->cell_tags);
+    else if (k == "parent_tags") v = join(c->parent_tags);
+    else return GGP_EINVAL;
+    snprintf(buf, buflen, "%s", v.c_str());
+    return GGP_OK;
+}
+
+// ---- Parameter_set (Parameters.h:50-201) ----------------------------------------------
+static const char *k_param_names[GGP_N_PARAMS] = {
+    "mean_lambda", "gamma_lambda", "var_lambda", "mean_q", "gamma_q", "var_q",
+    "beta", "var_x", "var_g", "var_dx", "var_dg"};
+
+extern "C" int ggp_param_file_load(const char *path, int32_t check_complete, ggp_param_set *out)
+{
+    if (!out) return fail(GGP_EINVAL, "null out");
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < GGP_N_PARAMS; ++i) {
+        std::snprintf(out->name[i], sizeof out->name[i], "%s", k_param_names[i]);
+        out->kind[i] = 1;
+        out->lower[i] = 0.;          // Parameter("..", 0.) (Parameters.h:114-128)
+        out->upper[i] = HUGE_VAL;
+    }
+    std::ifstream fin(path ? path : "");
+    std::string line;
+    while (std::getline(fin, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        std::vector<std::string> parts = split_at(line, "=");
+        parts[0] = trim_ref(parts[0]);
+        int idx = -1;
+        for (int i = 0; i < GGP_N_PARAMS; ++i)
+            if (parts[0] == k_param_names[i]) idx = i;
+        if (idx < 0) continue;
+        if (parts.size() < 2) return fail(GGP_EINVAL, "(set_paramter) ERROR: Parameter settings of '" + parts[0] + "' cannot be processed (missing '=')");
+        std::vector<std::string> vals = split_at(parts[1], ",");
+        for (auto &v : vals) v = trim_ref(v);
+        try {
+            if (vals.size() == 4) {
+                out->init[idx] = stod_reject_nan(vals[0]);
+                out->step[idx] = stod_reject_nan(vals[1]);
+                out->lower[idx] = stod_reject_nan(vals[2]);
+                out->upper[idx] = stod_reject_nan(vals[3]);
+                out->kind[idx] = 2;
+            } else if (vals.size() == 1) {
+                out->init[idx] = stod_reject_nan(vals[0]);
+                out->kind[idx] = 0;
+            } else if (vals.size() == 2) {
+                out->init[idx] = stod_reject_nan(vals[0]);
+                out->step[idx] = stod_reject_nan(vals[1]);
+                out->kind[idx] = 1;
+            } else {
+                throw std::invalid_argument("Invalide number of arguments");
+            }
+            out->set[idx] = 1;
+        } catch (std::exception &e) {
+            return fail(GGP_EINVAL, "(set_paramter) ERROR: Parameter settings of '" + parts[0] +
+                                        "' cannot be processed (" + e.what() + ")");
+        }
+    }
+    if (check_complete) {
+        for (int i = 0; i < GGP_N_PARAMS; ++i)
+            if (!out->set[i])
+                return fail(GGP_EINVAL, std::string("(check_if_complete) ERROR: Parameter ") +
+                                            k_param_names[i] + " not found in parameter file");
+    }
+    return GGP_OK;
+}
+
+// ---- read_data (moma_input.h:401-527) ---------------------------------------------------
+extern "C" int ggp_dataset_read(const char *infile, const ggp_csv_config *cfg_in, ggp_dataset **out)
+{
+    if (!infile || !out) return fail(GGP_EINVAL, "null argument");
+    ggp_csv_config defaults;
+    const ggp_csv_config &cfg = cfg_in ? *cfg_in : defaults;
+    std::ifstream file(infile);
+    if (!file) return fail(GGP_EINVAL, std::string("cannot open ") + infile);
+    std::string line;
+    std::getline(file, line);
+    std::vector<std::string> hdr = split_at(line, cfg.delm);
+    std::map<std::string, int> H;   // get_header_indices: first occurrence wins (map::insert)
+    for (size_t i = 0; i < hdr.size(); ++i) {
+        std::string s = trim_ref(hdr[i], ' ');
+        for (char ch : {'\t', '\n', '\v', '\f', '\r'}) s = trim_ref(s, ch);
+        H.insert({s, (int)i});
+    }
+    auto need = [&](const std::string &col, const char *what) {
+        if (!H.count(col))
+            throw std::invalid_argument(std::string("(read_data) ERROR: (") + what +
+                                        ") is not an column in input file: " + col);
+    };
+    auto *ds = new ggp_dataset();
+    ds->fp_auto = cfg.fp_auto;
+    long line_count = 1;
+    try {
+        need(cfg.time_col, "time_col");
+        need(cfg.length_col, "length_col");
+        need(cfg.fp_col, "fp_col");
+        if (!cfg.segment_col.empty()) need(cfg.segment_col, "segment_col");
+        if (!cfg.filter_col.empty()) need(cfg.filter_col, "filter_col");
+        for (auto &t : cfg.cell_tags) need(t, "cell_tags");
+        for (auto &t : cfg.parent_tags) need(t, "parent_tags");
+        const int it = H[cfg.time_col], il = H[cfg.length_col], ig = H[cfg.fp_col];
+        const int is = cfg.segment_col.empty() ? -1 : H[cfg.segment_col];
+        const int iflt = cfg.filter_col.empty() ? -1 : H[cfg.filter_col];
+        std::vector<int> ic, ip;
+        for (auto &t : cfg.cell_tags) ic.push_back(H[t]);
+        for (auto &t : cfg.parent_tags) ip.push_back(H[t]);
+        std::string last_cell;
+        while (std::getline(file, line)) {
+            ++line_count;
+            std::vector<std::string> f = split_at(line, cfg.delm);
+            auto field = [&](int i) -> const std::string & {
+                if (i < 0 || (size_t)i >= f.size())
+                    throw std::out_of_range("row has fewer fields than the header");
+                return f[i];
+            };
+            try {
+                if (iflt >= 0 && !string2bool(field(iflt))) continue;
+                auto compose = [&](const std::vector<int> &idx) {
+                    std::string id;
+                    for (size_t k = 0; k < idx.size(); ++k) {
+                        if (k) id += ".";
+                        id += remove_last_decimal(field(idx[k]));
+                    }
+                    return id;
+                };
+                std::string cur = compose(ic);
+                if (ds->cells.empty() || cur != last_cell) {
+                    Cell c;
+                    c.id = cur;
+                    c.parent_id = compose(ip);
+                    ds->cells.push_back(std::move(c));
+                }
+                Cell &c = ds->cells.back();
+                c.time.push_back(stod_reject_nan(field(it)) / cfg.rescale_time);
+                double len = stod_reject_nan(field(il));
+                c.log_length.push_back(cfg.length_islog ? len : std::log(len));
+                c.fp.push_back(stod_reject_nan(field(ig)));
+                c.segment.push_back(is < 0 ? 0 : stoi_ref(field(is)));
+                last_cell = cur;
+            } catch (std::exception &e) {
+                throw std::runtime_error("(read_data) ERROR: Line no." + std::to_string(line_count) +
+                                         " cannnot be processed (" + e.what() + ")");
+            }
+        }
+    } catch (std::exception &e) {
+        delete ds;
+        return fail(GGP_EINVAL, e.what());
+    }
+    *out = ds;
+    return GGP_OK;
+}
+
+extern "C" void ggp_dataset_free(ggp_dataset *d) { delete d; }
+extern "C" int64_t ggp_dataset_n_cells(const ggp_dataset *d) { return d ? (int64_t)d->cells.size() : 0; }
+extern "C" int64_t ggp_dataset_n_rows(const ggp_dataset *d)
+{
+    int64_t n = 0;
+    if (d)
+        for (auto &c : d->cells) n += (int64_t)c.time.size();
+    return n;
+}
+
+extern "C" int ggp_dataset_segments(const ggp_dataset *d, int32_t *out, int32_t cap, int32_t *n)
+{   // get_segment_indices (moma_input.h:538-570)
+    if (!d || !n) return fail(GGP_EINVAL, "null argument");
+    std::vector<int32_t> segs;
+    for (auto &c : d->cells)
+        for (int32_t s : c.segment)
+            if (std::find(segs.begin(), segs.end(), s) == segs.end()) segs.push_back(s);
+    *n = (int32_t)segs.size();
+    for (int32_t i = 0; i < cap && i < (int32_t)segs.size(); ++i) out[i] = segs[i];
+    if (segs.empty()) return GGP_OK;
+    int32_t mn = *std::min_element(segs.begin(), segs.end());
+    int32_t mx = *std::max_element(segs.begin(), segs.end());
+    if (mn != 0) return fail(GGP_EINVAL, "(get_segment_indices) ERROR: The segment indices do not start at 0");
+    if ((int32_t)segs.size() - 1 != mx)
+        return fail(GGP_EINVAL, "(get_segment_indices) ERROR: The segment indices are not consecutive");
+    return GGP_OK;
+}
+
+namespace {
+// vec_mean / vec_var (moma_input.h:663-672): accumulate order, E[v^2] - E[v]^2
+void mean_var(const std::vector<double> &v, double &m, double &var)
+{
+    double s = 0.0;
+    for (double x : v) s = s + x;
+    m = s / (double)v.size();
+    double sq = 0.0;
+    for (double x : v) sq = sq + x * x;
+    double mm = s / (double)v.size();
+    var = sq / (double)v.size() - mm * mm;
+}
+
+void finish_forest(ggp_host_forest *f)
+{
+    const int64_t n = (int64_t)f->ids.size();
+    // build_cell_genealogy (moma_input.h:125-151) with a hash map of id -> cells in order
+    std::unordered_map<std::string, std::vector<int32_t>> by_id;
+    by_id.reserve((size_t)n * 2);
+    for (int64_t j = 0; j < n; ++j) by_id[f->ids[j]].push_back((int32_t)j);
+    f->parent.assign(n, -1);
+    f->d1.assign(n, -1);
+    f->d2.assign(n, -1);
+    for (int64_t k = 0; k < n; ++k) {
+        auto it = by_id.find(f->parent_ids[k]);
+        if (it == by_id.end()) continue;
+        for (int32_t j : it->second) {
+            f->parent[k] = j;
+            if (f->d1[j] == -1) f->d1[j] = (int32_t)k;
+            else if (f->d2[j] == -1) f->d2[j] = (int32_t)k;
+            else
+                throw std::invalid_argument("(build_cell_genealogy) ERROR: Both daughter pointers are set, cell_id: " +
+                                            f->ids[j]);
+        }
+    }
+    f->n_roots = 0;
+    for (int64_t k = 0; k < n; ++k) f->n_roots += (f->parent[k] == -1);
+    // init_cells_f / init_cells_r (moma_input.h:675-735): cells with > 1 row
+    std::vector<double> x0, g0, x1, g1;
+    for (int64_t k = 0; k < n; ++k) {
+        int64_t a = f->row_off[k], b = f->row_off[k + 1];
+        if (b - a > 1) {
+            x0.push_back(f->log_length[a]);
+            g0.push_back(f->fp[a]);
+            x1.push_back(f->log_length[b - 1]);
+            g1.push_back(f->fp[b - 1]);
+        }
+    }
+    mean_var(x0, f->root_mean[0], f->root_var[0]);
+    mean_var(g0, f->root_mean[1], f->root_var[1]);
+    mean_var(x1, f->leaf_mean[0], f->leaf_var[0]);
+    mean_var(g1, f->leaf_mean[1], f->leaf_var[1]);
+}
+}  // namespace
+
+extern "C" int ggp_forest_build(const ggp_dataset *d, int32_t segment, int32_t noise_scaled,
+                                int32_t division_binomial, ggp_host_forest **out)
+{
+    if (!d || !out) return fail(GGP_EINVAL, "null argument");
+    auto *f = new ggp_host_forest();
+    f->noise_scaled = noise_scaled;
+    f->division_binomial = division_binomial;
+    f->fp_auto = d->fp_auto;
+    f->row_off.push_back(0);
+    for (const Cell &c : d->cells) {
+        size_t kept = 0;
+        for (size_t t = 0; t < c.time.size(); ++t) {
+            if (segment >= 0 && c.segment[t] != segment) continue;   // get_segment (:580-620)
+            f->time.push_back(c.time[t]);
+            f->log_length.push_back(c.log_length[t]);
+            f->fp.push_back(c.fp[t]);
+            f->segment.push_back(c.segment[t]);
+            ++kept;
+        }
+        if (kept == 0) continue;   // "only keep the cell if it has any data points"
+        f->ids.push_back(c.id);
+        f->parent_ids.push_back(c.parent_id);
+        f->row_off.push_back((int64_t)f->time.size());
+    }
+    try {
+        finish_forest(f);
+    } catch (std::exception &e) {
+        delete f;
+        return fail(GGP_EINVAL, e.what());
+    }
+    *out = f;
+    return GGP_OK;
+}
+
+extern "C" void ggp_host_forest_free(ggp_host_forest *f) { delete f; }
+
+extern "C" int ggp_host_forest_desc(const ggp_host_forest *f, ggp_forest_desc *d)
+{
+    if (!f || !d) return fail(GGP_EINVAL, "null argument");
+    std::memset(d, 0, sizeof *d);
+    d->n_cells = (int64_t)f->ids.size();
+    d->n_rows = (int64_t)f->time.size();
+    d->row_offset = f->row_off.data();
+    d->parent = f->parent.data();
+    d->daughter1 = f->d1.data();
+    d->daughter2 = f->d2.data();
+    d->segment = f->segment.data();
+    d->time = f->time.data();
+    d->log_length = f->log_length.data();
+    d->fp = f->fp.data();
+    for (int i = 0; i < 2; ++i) {
+        d->root_mean_xg[i] = f->root_mean[i];
+        d->root_var_xg[i] = f->root_var[i];
+        d->leaf_mean_xg[i] = f->leaf_mean[i];
+        d->leaf_var_xg[i] = f->leaf_var[i];
+    }
+    d->noise_scaled = f->noise_scaled;
+    d->division_binomial = f->division_binomial;
+    d->fp_auto = f->fp_auto;
+    return GGP_OK;
+}
+
+extern "C" const char *ggp_host_forest_cell_id(const ggp_host_forest *f, int64_t i)
+{
+    return (f && i >= 0 && i < (int64_t)f->ids.size()) ? f->ids[i].c_str() : nullptr;
+}
+extern "C" const char *ggp_host_forest_parent_id(const ggp_host_forest *f, int64_t i)
+{
+    return (f && i >= 0 && i < (int64_t)f->parent_ids.size()) ? f->parent_ids[i].c_str() : nullptr;
+}
+extern "C" int64_t ggp_host_forest_n_roots(const ggp_host_forest *f) { return f ? f->n_roots : 0; }
+
+// ---- synthetic forests ------------------------------------------------------------------
+namespace {
+// Philox4x32-10 (Salmon et al., SC'11)
+struct Philox {
+    uint32_t key[2];
+    uint32_t ctr[4];
+    uint32_t buf[4];
+    int avail = 0;
+    Philox(uint64_t seed, uint64_t stream)
+    {
+        key[0] = (uint32_t)seed;
+        key[1] = (uint32_t)(seed >> 32);
+        ctr[0] = 0; ctr[1] = 0;
+        ctr[2] = (uint32_t)stream;
+        ctr[3] = (uint32_t)(stream >> 32);
+    }
+    void block()
+    {
+        uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+        uint32_t k0 = key[0], k1 = key[1];
+        for (int r = 0; r < 10; ++r) {
+            uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+            uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+            uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+            uint32_t n1 = (uint32_t)p1;
+            uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+            uint32_t n3 = (uint32_t)p0;
+            c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        for (int i = 0; i < 4; ++i) buf[i] = c[i];
+        avail = 4;
+        if (++ctr[0] == 0) ++ctr[1];
+    }
+    double uniform()   // (0, 1)
+    {
+        if (avail < 2) block();
+        uint64_t hi = buf[--avail], lo = buf[--avail];
+        uint64_t v = ((hi << 32) | lo) >> 11;
+        return ((double)v + 0.5) * (1.0 / 9007199254740992.0);
+    }
+    double normal()
+    {
+        double u1 = uniform(), u2 = uniform();
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    }
+};
+
+struct SimState { double x, g, l, q; };
+
+// example parameters (example_data_set/parameter_file.txt:2-16)
+const double kML = 2.31e-03, kGL = 4.36e-02, kSL2 = 9.75e-08, kMQ = 9.03e+01, kGQ = 1.60e-02,
+             kSQ2 = 1.94e+01, kBETA = 4.95e-04, kVX = 3.35e-04, kVG = 8.26e-01, kVDX = 1.63e-04,
+             kVDG = 7.48e-01;
+
+// one minute of the model SDE (calculations_notes/prior_calculation.nb:275-333):
+// dx = l dt, dl = -gl (l - ml) dt + sqrt(sl2) dW, dq = -gq (q - mq) dt + sqrt(sq2) dW,
+// dg = (q e^x - beta g) dt; 8 Euler-Maruyama substeps.
+void sim_step(SimState &s, Philox &rng)
+{
+    const int sub = 8;
+    const double h = 1.0 / sub, sh = std::sqrt(h);
+    for (int i = 0; i < sub; ++i) {
+        double dl = -kGL * (s.l - kML) * h + std::sqrt(kSL2) * sh * rng.normal();
+        double dq = -kGQ * (s.q - kMQ) * h + std::sqrt(kSQ2) * sh * rng.normal();
+        double dg = (s.q * std::exp(s.x) - kBETA * s.g) * h;
+        s.x += s.l * h;
+        s.g += dg;
+        s.l += dl;
+        s.q += dq;
+    }
+}
+
+void sim_cell(SimState s, int64_t rows, Philox &rng, double t0, std::vector<double> &T,
+              std::vector<double> &X, std::vector<double> &G, SimState &end)
+{
+    for (int64_t r = 0; r < rows; ++r) {
+        if (r) sim_step(s, rng);
+        T.push_back(t0 + (double)r);
+        X.push_back(s.x + std::sqrt(kVX) * rng.normal());
+        double gv = kVG * std::max(s.g, 1.0);
+        G.push_back(s.g + std::sqrt(gv) * rng.normal());
+    }
+    end = s;
+}
+
+SimState divide(const SimState &p, Philox &rng)
+{
+    SimState d = p;
+    d.x = p.x - std::log(2.0) + std::sqrt(kVDX) * rng.normal();
+    d.g = p.g / 2.0 + std::sqrt(kVDG * std::max(p.g, 1.0) / 4.0) * rng.normal();
+    return d;
+}
+}  // namespace
+
+extern "C" int ggp_synthetic_forest(int64_t n_trees, int64_t P, uint64_t seed, int64_t first_tree,
+                                    int32_t noise_scaled, int32_t division_binomial,
+                                    ggp_host_forest **out)
+{
+    if (!out || n_trees < 0 || P < 4) return fail(GGP_EINVAL, "bad synthetic forest shape");
+    const int64_t n_root = P / 2, n_d = P / 4;
+    const int64_t rows_tree = n_root + 2 * n_d;
+    auto *f = new ggp_host_forest();
+    f->noise_scaled = noise_scaled;
+    f->division_binomial = division_binomial;
+    f->fp_auto = 0;
+    const int64_t ncell = 3 * n_trees, nrow = rows_tree * n_trees;
+    f->ids.resize(ncell);
+    f->parent_ids.resize(ncell);
+    f->row_off.resize(ncell + 1);
+    f->time.resize(nrow);
+    f->log_length.resize(nrow);
+    f->fp.resize(nrow);
+    f->segment.assign(nrow, 0);
+    unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n_trees < 64) nth = 1;
+    auto work = [&](int64_t lo, int64_t hi) {
+        std::vector<double> T, X, G;
+        for (int64_t k = lo; k < hi; ++k) {
+            const int64_t tree = first_tree + k;
+            Philox rng(seed, (uint64_t)tree);
+            T.clear(); X.clear(); G.clear();
+            SimState s{std::log(2.1) + 0.05 * rng.normal(), 3e4 + 3e3 * rng.normal(), kML, kMQ};
+            SimState end, e1, e2;
+            sim_cell(s, n_root, rng, 0.0, T, X, G, end);
+            sim_step(end, rng);
+            SimState a = divide(end, rng), b = divide(end, rng);
+            sim_cell(a, n_d, rng, (double)n_root, T, X, G, e1);
+            sim_cell(b, n_d, rng, (double)n_root, T, X, G, e2);
+            const int64_t r0 = k * rows_tree;
+            std::memcpy(&f->time[r0], T.data(), rows_tree * sizeof(double));
+            std::memcpy(&f->log_length[r0], X.data(), rows_tree * sizeof(double));
+            std::memcpy(&f->fp[r0], G.data(), rows_tree * sizeof(double));
+            const std::string base = "t" + std::to_string(tree);
+            f->ids[3 * k] = base + ".0";
+            f->ids[3 * k + 1] = base + ".1";
+            f->ids[3 * k + 2] = base + ".2";
+            f->parent_ids[3 * k] = base + ".p";
+            f->parent_ids[3 * k + 1] = base + ".0";
+            f->parent_ids[3 * k + 2] = base + ".0";
+            f->row_off[3 * k] = r0;
+            f->row_off[3 * k + 1] = r0 + n_root;
+            f->row_off[3 * k + 2] = r0 + n_root + n_d;
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < nth; ++i) {
+        int64_t lo = n_trees * i / nth, hi = n_trees * (i + 1) / nth;
+        th.emplace_back(work, lo, hi);
+    }
+    for (auto &t : th) t.join();
+    f->row_off[ncell] = nrow;
+    // genealogy is known by construction (root, d1, d2 per tree); init stats as init_cells
+    f->parent.assign(ncell, -1);
+    f->d1.assign(ncell, -1);
+    f->d2.assign(ncell, -1);
+    for (int64_t k = 0; k < n_trees; ++k) {
+        f->d1[3 * k] = (int32_t)(3 * k + 1);
+        f->d2[3 * k] = (int32_t)(3 * k + 2);
+        f->parent[3 * k + 1] = f->parent[3 * k + 2] = (int32_t)(3 * k);
+    }
+    f->n_roots = n_trees;
+    std::vector<double> x0, g0, x1, g1;
+    x0.reserve(ncell); g0.reserve(ncell); x1.reserve(ncell); g1.reserve(ncell);
+    for (int64_t c = 0; c < ncell; ++c) {
+        int64_t a = f->row_off[c], b = f->row_off[c + 1];
+        if (b - a > 1) {
+            x0.push_back(f->log_length[a]); g0.push_back(f->fp[a]);
+            x1.push_back(f->log_length[b - 1]); g1.push_back(f->fp[b - 1]);
+        }
+    }
+    if (!x0.empty()) {
+        mean_var(x0, f->root_mean[0], f->root_var[0]);
+        mean_var(g0, f->root_mean[1], f->root_var[1]);
+        mean_var(x1, f->leaf_mean[0], f->leaf_var[0]);
+        mean_var(g1, f->leaf_mean[1], f->leaf_var[1]);
+    }
+    *out = f;
+    return GGP_OK;
+}

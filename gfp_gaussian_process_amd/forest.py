@@ -1,0 +1,387 @@
+"""Host-side mirror of the reference's data model and objective entry points.
+
+Reference interface (C++), and what mirrors it here:
+
+  CSVconfig(filename)                      CSVConfig.load             CSVconfig.h:26-98
+  Parameter_set(filename)                  ParameterSet.load          Parameters.h:133-176
+  read_data(file, config, noise, div)      Dataset.read               moma_input.h:401-527
+  get_segment_indices(cells)               Dataset.segment_indices    moma_input.h:538-570
+  get_segment + build_cell_genealogy       HostForest.build           moma_input.h:580-620,125-151
+    + init_cells                                                      moma_input.h:738-741
+  std::vector<MOMAdata> (on the device)    Forest                     moma_input.h:22-80
+  total_likelihood(params, cells) -> +ll   total_likelihood           likelihood.h:170-174
+  total_likelihood(x, grad, data) -> -ll   total_likelihood_nlopt     likelihood.h:125-159
+  total_likelihood_log_params              total_likelihood_log_params likelihood.h:161-167
+
+Every likelihood evaluation runs in the HIP engine (lib/libggp.so).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+
+NOISE_MODELS = {"scaled": 1, "const": 0}
+DIVISION_MODELS = {"binomial": 1, "gauss": 0}
+PARAM_NAMES = ["mean_lambda", "gamma_lambda", "var_lambda", "mean_q", "gamma_q", "var_q",
+               "beta", "var_x", "var_g", "var_dx", "var_dg"]
+
+
+class GGPError(RuntimeError):
+    pass
+
+
+class LikelihoodIsNan(GGPError):
+    """std::domain_error("Likelihood is Nan") of likelihood.h:71-93."""
+
+    def __init__(self, cell: int, row: int, cell_id: str | None = None):
+        self.cell, self.row, self.cell_id = cell, row, cell_id
+        super().__init__(f"Likelihood is Nan (cell {cell_id or cell}, row {row})")
+
+
+def _host_err() -> str:
+    return (N.host().ggp_host_last_error() or b"").decode()
+
+
+# ------------------------------------------------------------------------------------------
+class CSVConfig:
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load(cls, path: str | None = None) -> "CSVConfig":
+        h = ctypes.c_void_p()
+        rc = N.host().ggp_csv_config_load(path.encode() if path else None, ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls(h)
+
+    def get(self, key: str) -> str:
+        buf = ctypes.create_string_buffer(4096)
+        if N.host().ggp_csv_config_get(self._h, key.encode(), buf, 4096) != N.GGP_OK:
+            raise KeyError(key)
+        return buf.value.decode()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            N.host().ggp_csv_config_free(self._h)
+            self._h = None
+
+
+@dataclass
+class ParameterSet:
+    names: list = field(default_factory=lambda: list(PARAM_NAMES))
+    kind: list = field(default_factory=list)      # "fixed" | "free" | "bound"
+    init: np.ndarray = None
+    step: np.ndarray = None
+    lower: np.ndarray = None
+    upper: np.ndarray = None
+
+    @classmethod
+    def load(cls, path: str, check_complete: bool = True) -> "ParameterSet":
+        ps = N.ParamSetC()
+        rc = N.host().ggp_param_file_load(path.encode(), 1 if check_complete else 0, ctypes.byref(ps))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        kinds = {0: "fixed", 1: "free", 2: "bound"}
+        return cls(kind=[kinds[ps.kind[i]] for i in range(N.N_PARAMS)],
+                   init=np.array(ps.init[:]), step=np.array(ps.step[:]),
+                   lower=np.array(ps.lower[:]), upper=np.array(ps.upper[:]))
+
+    def get_init(self) -> np.ndarray:
+        return self.init.copy()
+
+    def non_fixed(self) -> list:
+        return [i for i, k in enumerate(self.kind) if k != "fixed"]
+
+    def bound(self) -> list:
+        return [i for i, k in enumerate(self.kind) if k == "bound"]
+
+
+class Dataset:
+    """read_data output: cells in input order (moma_input.h:401-527)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def read(cls, infile: str, config: CSVConfig | None = None) -> "Dataset":
+        h = ctypes.c_void_p()
+        rc = N.host().ggp_dataset_read(infile.encode(), config._h if config else None, ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls(h)
+
+    @property
+    def n_cells(self) -> int:
+        return int(N.host().ggp_dataset_n_cells(self._h))
+
+    @property
+    def n_rows(self) -> int:
+        return int(N.host().ggp_dataset_n_rows(self._h))
+
+    def segment_indices(self) -> list:
+        buf = (ctypes.c_int32 * 4096)()
+        n = ctypes.c_int32()
+        rc = N.host().ggp_dataset_segments(self._h, buf, 4096, ctypes.byref(n))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return list(buf[: n.value])
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            N.host().ggp_dataset_free(self._h)
+            self._h = None
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+class HostForest:
+    """A flattened forest: the reference's std::vector<MOMAdata> after genealogy + init_cells,
+    as structure-of-arrays (cells in input order, rows cell-major)."""
+
+    def __init__(self, arrays: dict, ids=None, parent_ids=None):
+        self.a = arrays
+        self.ids = ids
+        self.parent_ids = parent_ids
+
+    # -- constructors --
+    @classmethod
+    def _from_handle(cls, h, with_ids=True) -> "HostForest":
+        H = N.host()
+        d = N.ForestDesc()
+        H.ggp_host_forest_desc(h, ctypes.byref(d))
+        nc, nr = int(d.n_cells), int(d.n_rows)
+        a = dict(
+            row_offset=_arr(d.row_offset, nc + 1, np.int64), parent=_arr(d.parent, nc, np.int32),
+            daughter1=_arr(d.daughter1, nc, np.int32), daughter2=_arr(d.daughter2, nc, np.int32),
+            segment=_arr(d.segment, nr, np.int32), time=_arr(d.time, nr, np.float64),
+            log_length=_arr(d.log_length, nr, np.float64), fp=_arr(d.fp, nr, np.float64),
+            root_mean_xg=np.array(d.root_mean_xg[:]), root_var_xg=np.array(d.root_var_xg[:]),
+            leaf_mean_xg=np.array(d.leaf_mean_xg[:]), leaf_var_xg=np.array(d.leaf_var_xg[:]),
+            noise_scaled=int(d.noise_scaled), division_binomial=int(d.division_binomial),
+            fp_auto=float(d.fp_auto))
+        ids = pids = None
+        if with_ids:
+            ids = [H.ggp_host_forest_cell_id(h, i).decode() for i in range(nc)]
+            pids = [H.ggp_host_forest_parent_id(h, i).decode() for i in range(nc)]
+        H.ggp_host_forest_free(h)
+        return cls(a, ids, pids)
+
+    @classmethod
+    def build(cls, dataset: Dataset, segment: int = -1, noise_model: str = "scaled",
+              cell_division_model: str = "binomial") -> "HostForest":
+        h = ctypes.c_void_p()
+        rc = N.host().ggp_forest_build(dataset._h, segment, NOISE_MODELS[noise_model],
+                                       DIVISION_MODELS[cell_division_model], ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls._from_handle(h)
+
+    @classmethod
+    def from_csv(cls, infile: str, csv_config: str | None = None, segment: int = -1,
+                 noise_model: str = "scaled", cell_division_model: str = "binomial") -> "HostForest":
+        ds = Dataset.read(infile, CSVConfig.load(csv_config))
+        return cls.build(ds, segment, noise_model, cell_division_model)
+
+    @classmethod
+    def synthetic(cls, n_trees: int, rows_per_tree: int = 200, seed: int = 20261015, first_tree: int = 0,
+                  noise_model: str = "scaled", cell_division_model: str = "binomial",
+                  with_ids: bool = False) -> "HostForest":
+        h = ctypes.c_void_p()
+        rc = N.host().ggp_synthetic_forest(n_trees, rows_per_tree, seed, first_tree,
+                                           NOISE_MODELS[noise_model], DIVISION_MODELS[cell_division_model],
+                                           ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls._from_handle(h, with_ids=with_ids)
+
+    # -- properties --
+    @property
+    def n_cells(self) -> int:
+        return len(self.a["parent"])
+
+    @property
+    def n_rows(self) -> int:
+        return len(self.a["time"])
+
+    @property
+    def roots(self) -> np.ndarray:
+        return np.nonzero(self.a["parent"] == -1)[0]
+
+    def tree_of_cell(self) -> np.ndarray:
+        """root index of every cell"""
+        p = self.a["parent"]
+        tree = np.full(self.n_cells, -1, np.int64)
+        for c in range(self.n_cells):
+            r = c
+            while p[r] != -1:
+                r = p[r]
+            tree[c] = r
+        return tree
+
+    def subset_trees(self, roots) -> "HostForest":
+        """The sub-forest made of whole trees `roots` (cells keep input order); root/leaf
+        statistics stay those of the full forest, as one MOMAdata vector would have them."""
+        tree = self.tree_of_cell()
+        keep = np.isin(tree, np.asarray(roots))
+        idx = np.nonzero(keep)[0]
+        remap = np.full(self.n_cells, -1, np.int64)
+        remap[idx] = np.arange(len(idx))
+        ro = self.a["row_offset"]
+        rows = np.concatenate([np.arange(ro[c], ro[c + 1]) for c in idx]) if len(idx) else np.zeros(0, np.int64)
+        lens = (ro[idx + 1] - ro[idx]).astype(np.int64)
+        a = dict(self.a)
+        a["row_offset"] = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+
+        def rm(v):
+            v = v[idx]
+            return np.where(v >= 0, remap[np.maximum(v, 0)], -1).astype(np.int32)
+        a["parent"], a["daughter1"], a["daughter2"] = rm(self.a["parent"]), rm(self.a["daughter1"]), rm(self.a["daughter2"])
+        for k in ("segment", "time", "log_length", "fp"):
+            a[k] = self.a[k][rows]
+        ids = [self.ids[i] for i in idx] if self.ids else None
+        pids = [self.parent_ids[i] for i in idx] if self.parent_ids else None
+        return HostForest(a, ids, pids)
+
+    def desc(self, device: int = 0, kernel: str = "auto") -> N.ForestDesc:
+        a = self.a
+        d = N.ForestDesc()
+        d.n_cells, d.n_rows = self.n_cells, self.n_rows
+
+        def ptr(name, ctype):
+            arr = np.ascontiguousarray(a[name])
+            a[name] = arr
+            return arr.ctypes.data_as(ctypes.POINTER(ctype))
+        d.row_offset = ptr("row_offset", ctypes.c_int64)
+        d.parent = ptr("parent", ctypes.c_int32)
+        d.daughter1 = ptr("daughter1", ctypes.c_int32)
+        d.daughter2 = ptr("daughter2", ctypes.c_int32)
+        d.segment = ptr("segment", ctypes.c_int32)
+        d.time = ptr("time", ctypes.c_double)
+        d.log_length = ptr("log_length", ctypes.c_double)
+        d.fp = ptr("fp", ctypes.c_double)
+        d.root_mean_xg[:] = list(a["root_mean_xg"])
+        d.root_var_xg[:] = list(a["root_var_xg"])
+        d.leaf_mean_xg[:] = list(a["leaf_mean_xg"])
+        d.leaf_var_xg[:] = list(a["leaf_var_xg"])
+        d.noise_scaled = a["noise_scaled"]
+        d.division_binomial = a["division_binomial"]
+        d.fp_auto = a["fp_auto"]
+        d.device = device
+        d.kernel = N.KERNELS[kernel]
+        return d
+
+
+# ------------------------------------------------------------------------------------------
+class Forest:
+    """Device-resident forest + carried state (one HIP device).  Owns a ggp_forest handle."""
+
+    def __init__(self, host_forest: HostForest, device: int = 0, kernel: str = "auto"):
+        self.host = host_forest
+        self._lib = N.engine()
+        d = host_forest.desc(device, kernel)
+        h = ctypes.c_void_p()
+        rc = self._lib.ggp_forest_create(ctypes.byref(d), ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(self._lib.ggp_strerror(rc).decode())
+        self._h = h
+        self.n_rows = host_forest.n_rows
+        self.n_cells = host_forest.n_cells
+
+    def _check(self, rc):
+        if rc != N.GGP_OK:
+            raise GGPError(self._lib.ggp_strerror(rc).decode())
+
+    def total_likelihood(self, params) -> float:
+        p = np.ascontiguousarray(params, np.float64)
+        if p.shape != (N.N_PARAMS,):
+            raise ValueError("params must hold 11 values (Parameters.h:175 order)")
+        ll = ctypes.c_double()
+        nc, nr = ctypes.c_int64(), ctypes.c_int64()
+        rc = self._lib.ggp_total_loglik(self._h, p.ctypes.data_as(N.c_double_p), ctypes.byref(ll),
+                                        ctypes.byref(nc), ctypes.byref(nr))
+        if rc == N.GGP_ENAN:
+            cid = self.host.ids[nc.value] if (self.host.ids and nc.value >= 0) else None
+            raise LikelihoodIsNan(nc.value, nr.value, cid)
+        self._check(rc)
+        return ll.value
+
+    def submit(self, params) -> None:
+        """enqueue one evaluation (ggp_total_loglik_async)"""
+        self._pending = np.ascontiguousarray(params, np.float64)
+        self._check(self._lib.ggp_total_loglik_async(self._h, self._pending.ctypes.data_as(N.c_double_p)))
+
+    def result(self) -> float:
+        ll = ctypes.c_double()
+        nc, nr = ctypes.c_int64(), ctypes.c_int64()
+        rc = self._lib.ggp_loglik_result(self._h, ctypes.byref(ll), ctypes.byref(nc), ctypes.byref(nr))
+        if rc == N.GGP_ENAN:
+            raise LikelihoodIsNan(nc.value, nr.value)
+        self._check(rc)
+        return ll.value
+
+    def reset_state(self) -> None:
+        self._check(self._lib.ggp_reset_state(self._h))
+
+    def state(self) -> np.ndarray:
+        out = np.zeros((self.n_cells, N.STATE))
+        self._check(self._lib.ggp_get_state(self._h, out.ctypes.data_as(N.c_double_p)))
+        return out
+
+    def predict(self, params_per_segment):
+        p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
+        out = [np.zeros((self.n_rows, N.STATE)) for _ in range(3)]
+        self._check(self._lib.ggp_predict(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0],
+                                          *(o.ctypes.data_as(N.c_double_p) for o in out)))
+        return tuple(out)
+
+    def enable_profile(self) -> None:
+        n = ctypes.c_int32()
+        self._check(self._lib.ggp_last_launch_profile(self._h, None, None, 0, ctypes.byref(n)))
+
+    def launch_profile(self):
+        cap = 4096
+        ms = (ctypes.c_float * cap)()
+        rows = (ctypes.c_int64 * cap)()
+        n = ctypes.c_int32()
+        self._check(self._lib.ggp_last_launch_profile(self._h, ms, rows, cap, ctypes.byref(n)))
+        return list(ms[: n.value]), list(rows[: n.value])
+
+    def info(self) -> dict:
+        nl, mx = ctypes.c_int64(), ctypes.c_int64()
+        k = ctypes.c_int32()
+        self._check(self._lib.ggp_forest_info(self._h, ctypes.byref(nl), ctypes.byref(mx), ctypes.byref(k)))
+        return {"levels": nl.value, "max_level_cells": mx.value, "kernel": k.value}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.ggp_forest_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+# ---- reference-named entry points ---------------------------------------------------------
+def total_likelihood(params_vec, forest: Forest) -> float:
+    """+ll (likelihood.h:170-174).  Mutates the forest's carried root state."""
+    return forest.total_likelihood(params_vec)
+
+
+def total_likelihood_nlopt(params_vec, grad, forest: Forest) -> float:
+    """-ll, the NLopt objective signature (likelihood.h:125-159); grad is ignored."""
+    return -forest.total_likelihood(params_vec)
+
+
+def total_likelihood_log_params(log_params_vec, grad, forest: Forest) -> float:
+    """exp() of the parameters first (likelihood.h:161-167)."""
+    return total_likelihood_nlopt([math.exp(v) for v in log_params_vec], grad, forest)

@@ -1,0 +1,117 @@
+/*
+ * ggp.h -- C-ABI of the MI355X lineage-tree likelihood engine (libggp.so).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference is one C++
+ * translation unit with no plugin/FFI layer; the seam it replaces is the
+ * C++ call boundary below the optimiser / scan / Hessian / smoother drivers:
+ *
+ *   ggp_total_loglik  replaces  total_likelihood(params, cells)      likelihood.h:170-174
+ *                               (and the NLopt vfunc form            likelihood.h:125-159,
+ *                                total_likelihood_log_params         likelihood.h:161-167:
+ *                                the caller negates / exponentiates)
+ *                               incl. likelihood_recr / sc_likelihood likelihood.h:36-122
+ *   ggp_predict       replaces  prediction_forward                   predictions.h:166-173
+ *                               prediction_backward                  predictions.h:438-444
+ *                               combine_predictions                  predictions.h:466-499
+ *   ggp_forest_create replaces  the in-memory std::vector<MOMAdata> after
+ *                               build_cell_genealogy + init_cells    moma_input.h:125-151,738-741
+ *
+ * Plain pointers and sizes only; no HIP or torch types.  The library copies its inputs.
+ *
+ * Carried state: the reference's objective is stateful -- a root cell's covariance
+ * off-diagonals survive from one total_likelihood call to the next (predictions.h:63-78
+ * resets only the mean and the diagonal).  A ggp_forest keeps that state on the device
+ * and carries it across ggp_total_loglik calls exactly like the MOMAdata vector does;
+ * ggp_reset_state() restores the "fresh cells" (all zero) state of read_data().
+ * ggp_predict always starts from fresh cells, as main.cpp:434-438 does.
+ *
+ * Errors: return codes instead of C++ exceptions.  GGP_ENAN corresponds to the
+ * std::domain_error("Likelihood is Nan") of likelihood.h:71-93; the first NaN in
+ * reference order (roots in input order, DFS pre-order, row) is reported.
+ * Not re-entrant: one host thread per handle.
+ */
+#ifndef GGP_H
+#define GGP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGP_OK 0
+#define GGP_EINVAL 1   /* bad descriptor / argument                              */
+#define GGP_ENAN 2     /* log-likelihood is NaN (likelihood.h:71-93)             */
+#define GGP_EDEV 3     /* HIP runtime / device error                             */
+#define GGP_ENOMEM 4   /* device allocation failed                               */
+
+#define GGP_N_PARAMS 11      /* Parameters.h:175 order                           */
+#define GGP_STATE_DOUBLES 20 /* per cell/row: mean[4] then cov[16] row-major     */
+
+typedef struct ggp_forest ggp_forest;
+
+typedef struct {
+    int64_t n_cells;             /* cells in input order (read_data order)           */
+    int64_t n_rows;              /* data points (count_data_points)                  */
+    const int64_t *row_offset;   /* [n_cells+1]                                      */
+    const int32_t *parent;       /* [n_cells] -1 = root   (MOMAdata::parent)         */
+    const int32_t *daughter1;    /* [n_cells] -1 = none   (MOMAdata::daughter1)      */
+    const int32_t *daughter2;    /* [n_cells] -1 = none   (MOMAdata::daughter2)      */
+    const int32_t *segment;      /* [n_rows] segment index per row, or NULL (all 0)  */
+    const double *time;          /* [n_rows] time / rescale_time                     */
+    const double *log_length;    /* [n_rows]                                         */
+    const double *fp;            /* [n_rows]                                         */
+    double root_mean_xg[2];      /* init_cells_f: mean of first x, g                 */
+    double root_var_xg[2];       /*               population variance                */
+    double leaf_mean_xg[2];      /* init_cells_r: mean of last x, g                  */
+    double leaf_var_xg[2];
+    int32_t noise_scaled;        /* 1 = "scaled" (default), 0 = "const"              */
+    int32_t division_binomial;   /* 1 = "binomial" (default), 0 = "gauss"            */
+    double fp_auto;              /* CSVconfig::fp_auto                               */
+    int32_t device;              /* HIP device ordinal                               */
+    int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (results identical) */
+} ggp_forest_desc;
+
+#define GGP_KERNEL_AUTO 0     /* pick by occupancy                                   */
+#define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
+#define GGP_KERNEL_GROUP 2    /* one workgroup per cell (latency)                    */
+
+int ggp_forest_create(const ggp_forest_desc *desc, ggp_forest **out);
+void ggp_forest_destroy(ggp_forest *f);
+
+/* +ll of the whole forest (total_likelihood 2-arg form).  params: 11 doubles.
+ * nan_cell / nan_row (may be NULL) receive the first NaN (cell index in input order,
+ * row within the cell) or -1.  Returns GGP_OK, GGP_ENAN, GGP_EDEV. */
+int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *nan_cell,
+                     int64_t *nan_row);
+
+/* Asynchronous form for drivers that pipeline: enqueue one evaluation on the handle's
+ * stream; ggp_loglik_result() waits and returns what ggp_total_loglik would have. */
+int ggp_total_loglik_async(ggp_forest *f, const double *params);
+int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row);
+
+/* -p smoother.  params: n_seg*11 doubles (one Parameter_set per segment).
+ * out_fwd/out_bwd/out_comb: [n_rows*20] each (NULL = not requested).  out_bwd is in
+ * normal (un-reversed) coordinates as stored in MOMAdata::mean_backward. */
+int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd,
+                double *out_bwd, double *out_comb);
+
+/* carried state: zero it (fresh cells), or read it back ([n_cells*20]) */
+int ggp_reset_state(ggp_forest *f);
+int ggp_get_state(ggp_forest *f, double *out);
+
+/* measurement hooks (bench.py): HIP-event timings of the launches of the last
+ * ggp_total_loglik on the handle's stream.  ms[i], rows[i] for i < *n (cap entries). */
+int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t cap, int32_t *n);
+int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
+                    int32_t *kernel_used);
+
+int ggp_device_count(int32_t *n);
+const char *ggp_strerror(int code);
+const char *ggp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GGP_H */

@@ -1,0 +1,87 @@
+/*
+ * ggp_host.h -- C-ABI of the host-side forest ingest (libggp_host.so, plain C++17).
+ *
+ * Host half of the drop-in: it re-implements the reference's data-model layer with the
+ * same semantics so that a forest handed to libggp is index-for-index the reference's
+ * std::vector<MOMAdata>:
+ *
+ *   ggp_csv_config_load    CSVconfig::CSVconfig          CSVconfig.h:26-98
+ *   ggp_param_file_load    Parameter_set::Parameter_set  Parameters.h:133-176 (+ :50-85)
+ *   ggp_dataset_read       read_data                     moma_input.h:401-527
+ *                          get_cell_id / remove_last_decimal            :320-355
+ *   ggp_dataset_segments   get_segment_indices           moma_input.h:538-570
+ *   ggp_forest_build       get_segment + build_cell_genealogy + init_cells
+ *                                                        moma_input.h:580-620, 125-151, 675-741
+ *
+ * build_cell_genealogy is O(N^2) string compares in the reference; here it is a hash map
+ * with identical outcomes (parent = LAST cell in vector order with a matching id, every
+ * matching cell gets the child as daughter1 then daughter2, a third child is an error).
+ */
+#ifndef GGP_HOST_H
+#define GGP_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ggp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ggp_csv_config ggp_csv_config;
+typedef struct ggp_dataset ggp_dataset;
+typedef struct ggp_host_forest ggp_host_forest;
+
+/* Parameter file (Parameters.h).  kind: 0 fixed, 1 free, 2 bound (Parameter::fixed/free/bound) */
+typedef struct {
+    char name[GGP_N_PARAMS][16];
+    int32_t kind[GGP_N_PARAMS];
+    int32_t set[GGP_N_PARAMS];
+    double init[GGP_N_PARAMS], step[GGP_N_PARAMS], lower[GGP_N_PARAMS], upper[GGP_N_PARAMS];
+} ggp_param_set;
+
+/* error text of the last failing call on this thread */
+const char *ggp_host_last_error(void);
+
+int ggp_csv_config_load(const char *path /* NULL or "" = defaults */, ggp_csv_config **out);
+void ggp_csv_config_free(ggp_csv_config *c);
+/* accessors used by tests: key in {time_col, length_col, fp_col, delm, segment_col,
+ * filter_col, rescale_time, fp_auto, length_islog, cell_tags, parent_tags} */
+int ggp_csv_config_get(const ggp_csv_config *c, const char *key, char *buf, size_t buflen);
+
+/* returns GGP_OK; GGP_EINVAL (message via ggp_host_last_error) on a malformed file or an
+ * incomplete one when check_complete != 0 (Parameter_set::check_if_complete) */
+int ggp_param_file_load(const char *path, int32_t check_complete, ggp_param_set *out);
+
+int ggp_dataset_read(const char *infile, const ggp_csv_config *cfg, ggp_dataset **out);
+void ggp_dataset_free(ggp_dataset *d);
+int64_t ggp_dataset_n_cells(const ggp_dataset *d);
+int64_t ggp_dataset_n_rows(const ggp_dataset *d);
+/* segment indices in order of first occurrence; *n receives the count (<= cap copied) */
+int ggp_dataset_segments(const ggp_dataset *d, int32_t *out, int32_t cap, int32_t *n);
+
+/* segment < 0: the whole dataset (-p / -j path, main.cpp:434-443)
+ * segment >= 0: get_segment copy (-m / -s path, main.cpp:402-432) */
+int ggp_forest_build(const ggp_dataset *d, int32_t segment, int32_t noise_scaled,
+                     int32_t division_binomial, ggp_host_forest **out);
+void ggp_host_forest_free(ggp_host_forest *f);
+/* fills every field of desc except device/kernel; pointers stay owned by f */
+int ggp_host_forest_desc(const ggp_host_forest *f, ggp_forest_desc *desc);
+const char *ggp_host_forest_cell_id(const ggp_host_forest *f, int64_t i);
+const char *ggp_host_forest_parent_id(const ggp_host_forest *f, int64_t i);
+int64_t ggp_host_forest_n_roots(const ggp_host_forest *f);
+
+/* Synthetic forests (BASELINE.md / SURVEY.md §8d): n_trees trees of P rows each, a root
+ * of P/2 rows and two daughters of P/4 rows (P=200: 100+50+50), dt = 1, data simulated
+ * from the model SDE with the example parameters, Philox4x32 keyed by (seed, tree).
+ * Deterministic and independent of how trees are split: tree k of a forest built with
+ * first_tree = k0 is tree k0+k of the full forest. */
+int ggp_synthetic_forest(int64_t n_trees, int64_t rows_per_tree, uint64_t seed,
+                         int64_t first_tree, int32_t noise_scaled, int32_t division_binomial,
+                         ggp_host_forest **out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,821 @@
+/*
+ * ggp_oracle.c -- CPU restatement (checker) of the reference lineage-tree likelihood,
+ * propagator and smoother.  TEST INFRASTRUCTURE ONLY (see ggp_oracle.h header).
+ *
+ * Every floating-point expression is written in the reference's evaluation order
+ * (left-to-right, same grouping, pow(v,2) == v*v as gcc -O3 folds it, no FMA contraction:
+ * the reference is built `g++ -std=c++17 -O3` for plain x86-64, src/Makefile:2), so that
+ * this file reproduces the reference's rounding wherever libm does.
+ */
+#include "ggp_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define GGP_DAWSON_TABLE_QUALIFIER static const
+#include "../gfp_gaussian_process_amd/csrc/dawson_table.inc"
+
+#ifdef ORA_EXPERIMENT
+double (*ora_exp_hook)(double) = exp;
+double (*ora_dawson_hook)(double) = 0;
+#define EXP(v) (ora_exp_hook(v))
+#else
+#define EXP(v) exp(v)
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* Dawson: Faddeeva.cc:1458-1888 (w_im_y100, w_im), :467-471 (Dawson)                  */
+/* ------------------------------------------------------------------------------------ */
+static double w_im_y100(double y100, double x)
+{
+    if (!(y100 >= 0)) return NAN;   /* NaN input: no switch case matches (Faddeeva.cc:1860) */
+    int k = (int)y100;
+    if (k < GGP_DAWSON_NINT) {
+        const double *c = ggp_dawson_coef + GGP_DAWSON_NCOEF * k;
+        double t = 2 * y100 - (double)(2 * k + 1);
+        return c[0] + (c[1] + (c[2] + (c[3] + (c[4] + (c[5] + (c[6] + (c[7] + c[8] * t) * t) * t) * t) * t) * t) * t) * t;
+    }
+    if (k <= 100) {
+        const double *c = ggp_dawson_taylor;
+        double x2 = x * x;
+        return x * (c[0] - x2 * (c[1] - x2 * (c[2] - x2 * (c[3] - x2 * c[4]))));
+    }
+    return NAN;
+}
+
+static double w_im(double x)
+{
+    if (x >= 0) {
+        if (x > 45) {
+            if (x > 5e7) return GGP_ISPI / x;
+            return GGP_ISPI * ((x * x) * (x * x - 4.5) + 2) / (x * ((x * x) * (x * x - 5) + 3.75));
+        }
+        return w_im_y100(100 / (1 + x), x);
+    }
+    if (x < -45) {
+        if (x < -5e7) return GGP_ISPI / x;
+        return GGP_ISPI * ((x * x) * (x * x - 4.5) + 2) / (x * ((x * x) * (x * x - 5) + 3.75));
+    }
+    return -w_im_y100(100 / (1 - x), -x);
+}
+
+double ora_dawson(double x)
+{
+#ifdef ORA_EXPERIMENT
+    if (ora_dawson_hook) return ora_dawson_hook(x);
+#endif
+    return GGP_SPI2 * w_im(x);
+}
+#define DAW(v) ora_dawson(v)
+
+/* ------------------------------------------------------------------------------------ */
+/* tauint integrals: mean_cov_model.h:9-67.  I_k = int_{t0}^{t1} s^k exp(a s^2 + b s + c) */
+/* ------------------------------------------------------------------------------------ */
+static double tau0(double a, double b, double c, double t1, double t0)
+{   /* mean_cov_model.h:9-21 */
+    double z0 = (b + 2. * a * t0) / (2. * sqrt(a));
+    double z1 = (b + 2. * a * t1) / (2. * sqrt(a));
+    double x = 2. * (-EXP(a * (t0 * t0) + b * t0 + c) * DAW(z0)
+                     + EXP(a * (t1 * t1) + b * t1 + c) * (DAW(z1)));
+    return x / (2. * sqrt(a));
+}
+
+static double tau1(double a, double b, double c, double t1, double t0)
+{   /* mean_cov_model.h:23-34 */
+    double z0 = (b + 2. * a * t0) / (2. * sqrt(a));
+    double z1 = (b + 2. * a * t1) / (2. * sqrt(a));
+    double x = (-2. * sqrt(a) * EXP(c) * (EXP(t0 * (b + a * t0)) - EXP(t1 * (b + a * t1)))
+                + b * 2. * (EXP(-(b * b) / (4. * a) + c + z0 * z0) * DAW(z0)
+                            - EXP(-(b * b) / (4. * a) + c + z1 * z1) * DAW(z1)));
+    return x / (4. * pow(a, 1.5));
+}
+
+static double tau2(double a, double b, double c, double t_1, double t_0)
+{   /* mean_cov_model.h:36-49 */
+    double z0 = (b + 2. * a * t_0) / (2. * sqrt(a));
+    double z1 = (b + 2. * a * t_1) / (2. * sqrt(a));
+    double x = (2. * sqrt(a) * EXP(c) * (EXP(t_0 * (a * t_0 + b)) * (b - 2. * a * t_0)
+                                         - EXP(t_1 * (a * t_1 + b)) * (b - 2. * a * t_1))
+                + (EXP(-(b * b) / (4. * a) + c + z0 * z0) * (2. * a - b * b) * 2. * DAW(z0)
+                   + EXP(-(b * b) / (4. * a) + c + z1 * z1) * (-2. * a + b * b) * 2. * DAW(z1)));
+    return x / (8. * pow(a, 2.5));
+}
+
+static double tau3(double a, double b, double c, double t_1, double t_0)
+{   /* mean_cov_model.h:51-67 */
+    double z0 = (b + 2. * a * t_0) / (2. * sqrt(a));
+    double z1 = (b + 2. * a * t_1) / (2. * sqrt(a));
+    double e0 = EXP(t_0 * (b + a * t_0)), e1 = EXP(t_1 * (b + a * t_1));
+    double x = (-2. * sqrt(a) * EXP(c)
+                * ((b * b) * (e0 - e1) - 2. * a * e0 * (2. + b * t_0) + 2 * a * e1 * (2 + b * t_1)
+                   + 4 * (a * a) * (e0 * (t_0 * t_0) - e1 * (t_1 * t_1))))
+             + EXP(-(b * b) / (4. * a) + c + z0 * z0) * b * (-6. * a + b * b) * 2. * DAW(z0)
+             - EXP(-(b * b) / (4. * a) + c + z1 * z1) * b * (-6 * a + b * b) * 2. * DAW(z1);
+    return x / (16. * pow(a, 3.5));
+}
+
+double ora_tauint(int k, double a, double b, double c, double t1, double t0)
+{
+    switch (k) {
+    case 0: return tau0(a, b, c, t1, t0);
+    case 1: return tau1(a, b, c, t1, t0);
+    case 2: return tau2(a, b, c, t1, t0);
+    default: return tau3(a, b, c, t1, t0);
+    }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* mean_cov_model: mean_cov_model.h:73-274                                              */
+/* ------------------------------------------------------------------------------------ */
+/* All 22 scalars of the reference mean_x..cov_qq signatures, named as there. */
+typedef struct {
+    double t, bx, bg, bl, bq, Cxx, Cxg, Cxl, Cxq, Cgg, Cgl, Cgq, Cll, Clq, Cqq;
+    double ml, gl, sl2, mq, gq, sq2, b;
+} prop_in;
+
+#define I0(B, C, T1, T0) tau0(a, (B), (C), (T1), (T0))
+#define I1(B, C, T1, T0) tau1(a, (B), (C), (T1), (T0))
+#define I2(B, C, T1, T0) tau2(a, (B), (C), (T1), (T0))
+#define I3(B, C, T1, T0) tau3(a, (B), (C), (T1), (T0))
+#define UNPACK                                                                          \
+    const double t = s->t, bx = s->bx, bg = s->bg, bl = s->bl, bq = s->bq;              \
+    const double Cxx = s->Cxx, Cxg = s->Cxg, Cxl = s->Cxl, Cxq = s->Cxq, Cgg = s->Cgg;  \
+    const double Cgl = s->Cgl, Cgq = s->Cgq, Cll = s->Cll, Clq = s->Clq, Cqq = s->Cqq;  \
+    const double ml = s->ml, gl = s->gl, sl2 = s->sl2, mq = s->mq, gq = s->gq;         \
+    const double sq2 = s->sq2, b = s->b;                                                \
+    const double a = Cll / 2.;                                                          \
+    (void)t; (void)bx; (void)bg; (void)bl; (void)bq; (void)Cxx; (void)Cxg; (void)Cxl;   \
+    (void)Cxq; (void)Cgg; (void)Cgl; (void)Cgq; (void)Cll; (void)Clq; (void)Cqq;        \
+    (void)ml; (void)gl; (void)sl2; (void)mq; (void)gq; (void)sq2; (void)b; (void)a
+
+static double m_x(const prop_in *s)
+{   UNPACK; return bx + ml * t + (bl - ml) * (1 - EXP(-gl * t)) / gl; }           /* :73-75 */
+
+static double m_g(const prop_in *s)
+{   UNPACK;                                                                          /* :77-80 */
+    return bg / EXP(b * t) + Clq * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+           + mq * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+           + (bq + Cxq - mq) * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0);
+}
+
+static double m_l(const prop_in *s) { UNPACK; return ml + (bl - ml) * EXP(-gl * t); } /* :82-84 */
+static double m_q(const prop_in *s) { UNPACK; return mq + (bq - mq) * EXP(-gq * t); } /* :85-87 */
+
+static double c_xx(const prop_in *s)
+{   UNPACK;                                                                          /* :93-95 */
+    return Cll * ((1 - EXP(-gl * t)) * (1 - EXP(-gl * t))) / (gl * gl)
+           + 2 * Cxl * (1 - EXP(-gl * t)) / gl + Cxx
+           + sl2 / (2 * pow(gl, 3)) * (2 * gl * t - 3 + 4 * EXP(-gl * t) - (EXP(-gl * t) * EXP(-gl * t)));
+}
+
+static double c_xg(const prop_in *s, const double *nm)
+{   UNPACK;                                                                          /* :97-115 */
+    return (bg * bx) / EXP(b * t) + Cxg / EXP(b * t) + (bg * bl) / (EXP(b * t) * gl)
+        + Cgl / (EXP(b * t) * gl) - (bg * bl) / (EXP((b + gl) * t) * gl)
+        - Cgl / (EXP((b + gl) * t) * gl) - (bg * ml) / (EXP(b * t) * gl)
+        + (bg * ml) / (EXP((b + gl) * t) * gl) + (bg * ml * t) / EXP(b * t)
+        + (Cxl * mq + (Cll * mq) / gl) * I1(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        - (Cll * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t - gl * t, t, 0)) / gl
+        + (bx * Clq + bq * Cxl + Cxl * Cxq + Clq * Cxx + (bq * Cll) / gl + (bl * Clq) / gl
+           + (Clq * Cxl) / gl + (Cll * Cxq) / gl - (Clq * ml) / gl - Cxl * mq - (Cll * mq) / gl
+           + Clq * ml * t) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (-((bq * Cll) / gl) - (bl * Clq) / gl - (Clq * Cxl) / gl - (Cll * Cxq) / gl
+           + (Clq * ml) / gl + (Cll * mq) / gl) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + (Clq * Cxl + (Cll * Clq) / gl) * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        - (Cll * Clq * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)) / gl
+        + (bx * mq + Cxx * mq + (bl * mq) / gl + (Cxl * mq) / gl - (ml * mq) / gl + ml * mq * t)
+          * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (-((bl * mq) / gl) - (Cxl * mq) / gl + (ml * mq) / gl)
+          * I0(b + bl + Cxl, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + (bq * bx + Cxq + bx * Cxq + bq * Cxx + Cxq * Cxx + (bl * bq) / gl + Clq / gl
+           + (bq * Cxl) / gl + (bl * Cxq) / gl + (Cxl * Cxq) / gl - (bq * ml) / gl
+           - (Cxq * ml) / gl - bx * mq - Cxx * mq - (bl * mq) / gl - (Cxl * mq) / gl
+           + (ml * mq) / gl + bq * ml * t + Cxq * ml * t - ml * mq * t)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (-((bl * bq) / gl) - Clq / gl - (bq * Cxl) / gl - (bl * Cxq) / gl - (Cxl * Cxq) / gl
+           + (bq * ml) / gl + (Cxq * ml) / gl + (bl * mq) / gl + (Cxl * mq) / gl - (ml * mq) / gl)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        - nm[1] * nm[0];
+}
+
+static double c_xl(const prop_in *s)
+{   UNPACK;                                                                          /* :117-119 */
+    return sl2 / (2 * (gl * gl)) * ((1 - EXP(-gl * t)) * (1 - EXP(-gl * t)))
+           + Cll * EXP(-gl * t) * (1 - EXP(-gl * t)) / gl + Cxl * EXP(-gl * t);
+}
+
+static double c_xq(const prop_in *s)
+{   UNPACK; return Clq * (1 - EXP(-gl * t)) * EXP(-gq * t) / gl + Cxq * EXP(-gq * t); } /* :121-123 */
+
+static double c_gg(const prop_in *s, const double *nm)
+{   UNPACK;                                                                          /* :125-170 */
+    return ((bg * bg) + Cgg) / EXP(2 * b * t)
+        + 2 * Cgl * mq * I1(b + bl + Cxl, bx + Cxx / 2. - 2 * b * t, t, 0)
+        + (mq * (2 * Clq + gq * mq) * I1(b + bl + 2 * Cxl, 2 * (bx + Cxx - b * t), t, 0)) / gq
+        + 2 * (bq * Cgl + bg * Clq + Clq * Cxg + Cgl * Cxq - Cgl * mq)
+          * I1(b + bl + Cxl - gq, bx + Cxx / 2. - 2 * b * t, t, 0)
+        + (((bq * bq) * gq + Cqq * gq + 4 * bq * Cxq * gq + 4 * (Cxq * Cxq) * gq - 2 * Clq * mq
+            - 2 * bq * gq * mq - 4 * Cxq * gq * mq + gq * (mq * mq))
+           * I1(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), t, 0)) / gq
+        - (mq * mq) * I1(b + bl + 2 * Cxl, 2 * (bx + Cxx - b * t), 2 * t, t)
+        - (2 * Clq * mq * I1(b + bl + 2 * Cxl, 2 * bx + 2 * Cxx - (2 * b + gq) * t, 2 * t, t)) / gq
+        - (sq2 * I1(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t, t, 0)) / (2. * gq)
+        + (sq2 * I1(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t, 2 * t, t)) / (2. * gq)
+        + (-(bq * bq) - Cqq - 4 * bq * Cxq - 4 * (Cxq * Cxq) + 2 * bq * mq + 4 * Cxq * mq
+           - (mq * mq) + 4 * bq * Clq * t + 8 * Clq * Cxq * t - 4 * Clq * mq * t)
+          * I1(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), 2 * t, t)
+        + (2 * Clq * mq * I1(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t + gq * t, 2 * t, t)) / gq
+        + (Clq * Clq) * I3(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), t, 0)
+        - (Clq * Clq) * I3(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), 2 * t, t)
+        + 2 * Cgl * Clq * I2(b + bl + Cxl - gq, bx + Cxx / 2. - 2 * b * t, t, 0)
+        + (2 * bq * Clq + 4 * Clq * Cxq - 2 * Clq * mq)
+          * I2(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), t, 0)
+        + (-2 * bq * Clq - 4 * Clq * Cxq + 2 * Clq * mq + 2 * (Clq * Clq) * t)
+          * I2(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), 2 * t, t)
+        + (2 * bg * mq + 2 * Cxg * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - 2 * b * t, t, 0)
+        + ((2 * bq * mq) / gq + (4 * Cxq * mq) / gq - (2 * (mq * mq)) / gq)
+          * I0(b + bl + 2 * Cxl, 2 * (bx + Cxx - b * t), t, 0)
+        + (2 * bg * bq + 2 * Cgq + 2 * bq * Cxg + 2 * bg * Cxq + 2 * Cxg * Cxq - 2 * bg * mq
+           - 2 * Cxg * mq) * I0(b + bl + Cxl - gq, bx + Cxx / 2. - 2 * b * t, t, 0)
+        + ((-2 * bq * mq) / gq - (4 * Cxq * mq) / gq + (2 * (mq * mq)) / gq)
+          * I0(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), t, 0)
+        + (sq2 * I0(b + bl + 2 * Cxl, 2 * bx + 2 * Cxx - 2 * b * t, t, 0)) / (2. * (gq * gq))
+        + (sq2 * I0(b + bl + 2 * Cxl, 2 * bx + 2 * Cxx - 2 * b * t, 2 * t, t)) / (2. * (gq * gq))
+        + 2 * (mq * mq) * t * I0(b + bl + 2 * Cxl, 2 * (bx + Cxx - b * t), 2 * t, t)
+        + ((-2 * bq * mq) / gq - (4 * Cxq * mq) / gq + (2 * (mq * mq)) / gq)
+          * I0(b + bl + 2 * Cxl, 2 * bx + 2 * Cxx - (2 * b + gq) * t, 2 * t, t)
+        - (sq2 * I0(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t, t, 0)) / (2. * (gq * gq))
+        - (sq2 * t * I0(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t, 2 * t, t)) / gq
+        + (2 * (bq * bq) * t + 2 * Cqq * t + 8 * bq * Cxq * t + 8 * (Cxq * Cxq) * t
+           - 4 * bq * mq * t - 8 * Cxq * mq * t + 2 * (mq * mq) * t)
+          * I0(b + bl + 2 * Cxl - gq, 2 * (bx + Cxx - b * t), 2 * t, t)
+        + ((2 * bq * mq) / gq + (4 * Cxq * mq) / gq - (2 * (mq * mq)) / gq)
+          * I0(b + bl + 2 * Cxl - gq, 2 * bx + 2 * Cxx - 2 * b * t + gq * t, 2 * t, t)
+        - (sq2 * I0(b + bl + 2 * Cxl + gq, 2 * bx + 2 * Cxx - 2 * b * t - 2 * gq * t, 2 * t, t))
+          / (2. * (gq * gq))
+        - (nm[1] * nm[1]);
+}
+
+static double c_gl(const prop_in *s, const double *nm)
+{   UNPACK;                                                                          /* :172-181 */
+    return (bg * bl) / EXP((b + gl) * t) + Cgl / EXP((b + gl) * t) + (bg * ml) / EXP(b * t)
+        - (bg * ml) / EXP((b + gl) * t)
+        + Cll * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + Clq * ml * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * Cll + bl * Clq + Clq * Cxl + Cll * Cxq - Clq * ml - Cll * mq)
+          * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + Cll * Clq * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + ml * mq * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bl * mq + Cxl * mq - ml * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        + (bq * ml + Cxq * ml - ml * mq) * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bl * bq + Clq + bq * Cxl + bl * Cxq + Cxl * Cxq - bq * ml - Cxq * ml - bl * mq
+           - Cxl * mq + ml * mq) * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gl * t, t, 0)
+        - nm[1] * nm[2];
+}
+
+static double c_gq(const prop_in *s, const double *nm)
+{   UNPACK;                                                                          /* :183-196 */
+    return (bg * bq) / EXP((b + gq) * t) + Cgq / EXP((b + gq) * t) + (bg * mq) / EXP(b * t)
+        - (bg * mq) / EXP((b + gq) * t)
+        + Clq * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t - gq * t, t, 0)
+        + Clq * mq * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (2 * bq * Clq + 2 * Clq * Cxq - 2 * Clq * mq)
+          * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gq * t, t, 0)
+        + (Clq * Clq) * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gq * t, t, 0)
+        + (mq * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * mq + Cxq * mq - (mq * mq)) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t - gq * t, t, 0)
+        + (bq * mq + Cxq * mq - (mq * mq)) * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        - (sq2 * I0(b + bl + Cxl - gq, -b * t + bx + Cxx / 2. - gq * t, t, 0)) / (2. * gq)
+        + ((bq * bq) + Cqq + 2 * bq * Cxq + (Cxq * Cxq) - 2 * bq * mq - 2 * Cxq * mq + (mq * mq))
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t - gq * t, t, 0)
+        + (sq2 * I0(b + bl + Cxl + gq, -b * t + bx + Cxx / 2. - gq * t, t, 0)) / (2. * gq)
+        - nm[1] * nm[3];
+}
+
+static double c_ll(const prop_in *s)
+{   UNPACK; return Cll * (EXP(-gl * t) * EXP(-gl * t)) + sl2 / (2 * gl) * (1 - (EXP(-gl * t) * EXP(-gl * t))); }
+static double c_lq(const prop_in *s) { UNPACK; return Clq * EXP(-gl * t) * EXP(-gq * t); }
+static double c_qq(const prop_in *s)
+{   UNPACK; return sq2 / (2 * gq) * (1 - (EXP(-gq * t) * EXP(-gq * t))) + Cqq * (EXP(-gq * t) * EXP(-gq * t)); }
+
+static void load_prop(prop_in *s, const double *m, const double *C, double t, const double *p)
+{   /* mean_cov_model.h:221-235: reads the mean and the UPPER triangle + diagonal only */
+    s->t = t;
+    s->bx = m[0]; s->bg = m[1]; s->bl = m[2]; s->bq = m[3];
+    s->Cxx = C[0]; s->Cxg = C[1]; s->Cxl = C[2]; s->Cxq = C[3];
+    s->Cgg = C[5]; s->Cgl = C[6]; s->Cgq = C[7];
+    s->Cll = C[10]; s->Clq = C[11]; s->Cqq = C[15];
+    s->ml = p[0]; s->gl = p[1]; s->sl2 = p[2]; s->mq = p[3]; s->gq = p[4]; s->sq2 = p[5];
+    s->b = p[6];
+}
+
+void ora_mean_cov_model(double *m, double *C, double t, const double *p)
+{   /* mean_cov_model.h:211-274 */
+    prop_in s;
+    double nm[4], nC[16];
+    load_prop(&s, m, C, t, p);
+    nm[0] = m_x(&s);
+    nm[1] = m_g(&s);
+    nm[2] = m_l(&s);
+    nm[3] = m_q(&s);
+    nC[1] = nC[4] = c_xg(&s, nm);
+    nC[2] = nC[8] = c_xl(&s);
+    nC[3] = nC[12] = c_xq(&s);
+    nC[6] = nC[9] = c_gl(&s, nm);
+    nC[7] = nC[13] = c_gq(&s, nm);
+    nC[11] = nC[14] = c_lq(&s);
+    nC[0] = c_xx(&s);
+    nC[5] = c_gg(&s, nm);
+    nC[10] = c_ll(&s);
+    nC[15] = c_qq(&s);
+    memcpy(m, nm, sizeof nm);
+    memcpy(C, nC, sizeof nC);
+}
+
+/* cross-covariance elements: mean_cov_model.h:282-377 */
+void ora_cross_cov_model(const double *m, const double *C, double dt, const double *p, double *out)
+{
+    prop_in sv;
+    const prop_in *s = &sv;
+    load_prop(&sv, m, C, dt, p);
+    UNPACK;
+    double nm1 = m_g(s);
+    /* row x */
+    out[0] = Cxx + Cxl * (1 - EXP(-gl * t)) / gl;
+    out[1] = Cxg + Cgl * (1 - EXP(-gl * t)) / gl;
+    out[2] = Cxl + Cll * (1 - EXP(-gl * t)) / gl;
+    out[3] = Cxq + Clq * (1 - EXP(-gl * t)) / gl;
+    /* row g */
+    out[4] = (bg * bx) / EXP(b * t) + Cxg / EXP(b * t)
+        + Cxl * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bx * Clq + bq * Cxl + Cxl * Cxq + Clq * Cxx - Cxl * mq) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + Clq * Cxl * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bx * mq + Cxx * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * bx + Cxq + bx * Cxq + bq * Cxx + Cxq * Cxx - bx * mq - Cxx * mq)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0) - nm1 * bx;
+    out[5] = (bg * bg) / EXP(b * t) + Cgg / EXP(b * t)
+        + Cgl * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * Cgl + bg * Clq + Clq * Cxg + Cgl * Cxq - Cgl * mq) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + Cgl * Clq * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bg * mq + Cxg * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bg * bq + Cgq + bq * Cxg + bg * Cxq + Cxg * Cxq - bg * mq - Cxg * mq)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0) - nm1 * bg;
+    out[6] = (bg * bl) / EXP(b * t) + Cgl / EXP(b * t)
+        + Cll * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * Cll + bl * Clq + Clq * Cxl + Cll * Cxq - Cll * mq) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + Cll * Clq * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bl * mq + Cxl * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (bl * bq + Clq + bq * Cxl + bl * Cxq + Cxl * Cxq - bl * mq - Cxl * mq)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0) - nm1 * bl;
+    out[7] = (bg * bq) / EXP(b * t) + Cgq / EXP(b * t)
+        + Clq * mq * I1(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + (2 * bq * Clq + 2 * Clq * Cxq - Clq * mq) * I1(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (Clq * Clq) * I2(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0)
+        + (bq * mq + Cxq * mq) * I0(b + bl + Cxl, bx + Cxx / 2. - b * t, t, 0)
+        + ((bq * bq) + Cqq + 2 * bq * Cxq + (Cxq * Cxq) - bq * mq - Cxq * mq)
+          * I0(b + bl + Cxl - gq, bx + Cxx / 2. - b * t, t, 0) - nm1 * bq;
+    /* rows l, q */
+    out[8] = Cxl * EXP(-gl * t);  out[9] = Cgl * EXP(-gl * t);
+    out[10] = Cll * EXP(-gl * t); out[11] = Clq * EXP(-gl * t);
+    out[12] = Cxq * EXP(-gq * t); out[13] = Cgq * EXP(-gq * t);
+    out[14] = Clq * EXP(-gq * t); out[15] = Cqq * EXP(-gq * t);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Kalman pieces                                                                        */
+/* ------------------------------------------------------------------------------------ */
+/* log(2*M_PI) as folded by the compiler at -O3 (constant expression) */
+#define ORA_TWO_LOG_2PI (2 * log(2 * M_PI))
+
+/* S.determinant() on a DYNAMIC 2x2 (likelihood.h:31 takes Eigen::MatrixXd): Eigen 3.3
+ * PartialPivLU, unblocked: pivot on the first max |a(i,0)|, l = a10/a00, u11 = a11-l*a01,
+ * det = sign * (u00*u11). */
+static double det2_pplu(double s00, double s01, double s10, double s11)
+{
+    double sign = 1.0;
+    if (fabs(s10) > fabs(s00)) {
+        double t0 = s00, t1 = s01;
+        s00 = s10; s01 = s11; s10 = t0; s11 = t1;
+        sign = -1.0;
+    }
+    if (s00 != 0.0) {
+        s10 = s10 / s00;
+        s11 = s11 - s10 * s01;
+    }
+    return sign * (s00 * s11);
+}
+
+typedef struct { double si00, si01, si10, si11, S00, S01, S10, S11; } ora_innov;
+
+/* S = cov.block(0,0,2,2) + D ; Si = S.inverse() (fixed 2x2: cofactor * (1/det)),
+ * likelihood.h:59-67 / predictions.h:127-135 */
+static void innovation(const double *m, const double *C, const double *p, int scaled,
+                       double fp_auto, ora_innov *v)
+{
+    double d11 = scaled ? p[8] * (m[1] + fp_auto) : p[8];
+    v->S00 = C[0] + p[7];
+    v->S01 = C[1] + 0;
+    v->S10 = C[4] + 0;
+    v->S11 = C[5] + d11;
+    double det = v->S00 * v->S11 - v->S10 * v->S01;
+    double invdet = 1.0 / det;
+    v->si00 = v->S11 * invdet;
+    v->si10 = -v->S10 * invdet;
+    v->si01 = -v->S01 * invdet;
+    v->si11 = v->S00 * invdet;
+}
+
+/* log_likelihood (likelihood.h:26-32) */
+static double ll_term(double x0, double x1, const ora_innov *v)
+{
+    double h0 = -0.5 * x0, h1 = -0.5 * x1;
+    double r0 = h0 * v->si00 + h1 * v->si10;
+    double r1 = h0 * v->si01 + h1 * v->si11;
+    double q = r0 * x0 + r1 * x1;
+    return q - 0.5 * log(det2_pplu(v->S00, v->S01, v->S10, v->S11)) - ORA_TWO_LOG_2PI;
+}
+
+/* posterior (predictions.h:84-89): K = cov rows 0..1; mean += K^T Si xg; cov -= K^T Si K */
+static void posterior(double *m, double *C, double x0, double x1, const ora_innov *v)
+{
+    double K[8];
+    memcpy(K, C, sizeof K);
+    double KS[8]; /* (K^T Si)(i,j) at KS[2i+j] */
+    for (int i = 0; i < 4; ++i) {
+        KS[2 * i + 0] = K[i] * v->si00 + K[4 + i] * v->si10;
+        KS[2 * i + 1] = K[i] * v->si01 + K[4 + i] * v->si11;
+    }
+    for (int i = 0; i < 4; ++i)
+        m[i] = m[i] + (KS[2 * i] * x0 + KS[2 * i + 1] * x1);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            C[4 * i + j] = C[4 * i + j] - (KS[2 * i] * K[j] + KS[2 * i + 1] * K[4 + j]);
+}
+
+/* mean_cov_after_division (predictions.h:18-61) */
+static void after_division(double *m, double *C, const double *pm, const double *pC,
+                           double dt, const double *p, int binomial)
+{
+    memcpy(m, pm, 4 * sizeof(double));
+    memcpy(C, pC, 16 * sizeof(double));
+    ora_mean_cov_model(m, C, dt, p);
+    double var_dx = p[9], var_dg = p[10];
+    if (binomial) {
+        C[0] += var_dx;
+        C[1] = C[4] = m[1] / 2. * var_dx + C[1];
+        C[5] = var_dx * (m[1] * m[1] + C[5]) / 2. + var_dg * m[1] / 4. * (1 - var_dx) + C[5] / 4.;
+        C[9] /= 2; C[6] /= 2;
+        C[13] /= 2; C[7] /= 2;
+    } else {
+        for (int j = 0; j < 4; ++j) { C[4 + j] *= 0.5; C[4 * j + 1] *= 0.5; }
+        C[0] = var_dx + C[0];
+        C[5] = var_dg + C[5];
+    }
+    m[0] = m[0] + -log(2.);
+    m[1] = 0.5 * m[1];
+}
+
+/* init_sc_distribution root branch (predictions.h:63-78): diag + mean only; the six
+ * off-diagonal pairs keep the cell's previous state (carried state). */
+static void root_init(const ora_forest *f, double *m, double *C, const double *p)
+{
+    m[0] = f->root_mean_xg[0];
+    m[1] = f->root_mean_xg[1];
+    C[0] = f->root_var_xg[0];
+    C[5] = f->root_var_xg[1];
+    m[2] = p[0];
+    m[3] = p[3];
+    C[10] = p[2] / (2. * p[1]);
+    C[15] = p[5] / (2. * p[4]);
+}
+
+static int64_t *dfs_preorder(const ora_forest *f, int64_t *count)
+{
+    int64_t n = f->n_cells, k = 0, sp = 0;
+    int64_t *order = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    int64_t *stack = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    for (int64_t r = 0; r < n; ++r) {
+        if (f->parent[r] != -1) continue;
+        stack[sp++] = r;
+        while (sp) {
+            int64_t c = stack[--sp];
+            order[k++] = c;
+            if (f->d2[c] >= 0) stack[sp++] = f->d2[c];
+            if (f->d1[c] >= 0) stack[sp++] = f->d1[c];
+        }
+    }
+    free(stack);
+    *count = k;
+    return order;
+}
+
+double ora_total_loglik(const ora_forest *f, const double *p, double *state,
+                        int64_t *nan_cell, int64_t *nan_row, double *cell_ll)
+{   /* total_likelihood (likelihood.h:125-159), likelihood_recr (:110-122),
+     * sc_likelihood (:36-103) */
+    int64_t n_order = 0;
+    int64_t *order = dfs_preorder(f, &n_order);
+    double tl = 0;
+    if (nan_cell) *nan_cell = -1;
+    if (nan_row) *nan_row = -1;
+    for (int64_t oi = 0; oi < n_order; ++oi) {
+        int64_t c = order[oi];
+        double *m = state + ORA_STATE * c, *C = m + 4;
+        int64_t r0 = f->row_off[c], r1 = f->row_off[c + 1];
+        if (f->parent[c] == -1) {
+            root_init(f, m, C, p);
+        } else {
+            int64_t pc = f->parent[c];
+            const double *pm = state + ORA_STATE * pc;
+            double dt = f->time[r0] - f->time[f->row_off[pc + 1] - 1];
+            after_division(m, C, pm, pm + 4, dt, p, f->div_binomial);
+        }
+        double cl = 0;
+        for (int64_t r = r0; r < r1; ++r) {
+            double x0 = f->log_length[r] - m[0];
+            double x1 = f->fp[r] - m[1];
+            ora_innov v;
+            innovation(m, C, p, f->noise_scaled, f->fp_auto, &v);
+            double term = ll_term(x0, x1, &v);
+            tl += term;
+            cl += term;
+            if (isnan(tl)) {
+                if (nan_cell) *nan_cell = c;
+                if (nan_row) *nan_row = r - r0;
+                free(order);
+                return tl;
+            }
+            posterior(m, C, x0, x1, &v);
+            if (r < r1 - 1) ora_mean_cov_model(m, C, f->time[r + 1] - f->time[r], p);
+        }
+        if (cell_ll) cell_ll[c] = cl;
+    }
+    free(order);
+    return tl;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* -p smoother (predictions.h:93-499)                                                    */
+/* ------------------------------------------------------------------------------------ */
+/* Dense 4x4 inverse by partial-pivot LU (Eigen PartialPivLU semantics for the pivoting:
+ * first max |a|, unit-lower L), solved column by column against the identity. */
+static void inv4(const double *A, double *R)
+{
+    double lu[16];
+    int perm[4] = {0, 1, 2, 3};
+    memcpy(lu, A, sizeof lu);
+    for (int k = 0; k < 4; ++k) {
+        int piv = k;
+        double big = fabs(lu[4 * k + k]);
+        for (int i = k + 1; i < 4; ++i)
+            if (fabs(lu[4 * i + k]) > big) { big = fabs(lu[4 * i + k]); piv = i; }
+        if (piv != k) {
+            for (int j = 0; j < 4; ++j) {
+                double t = lu[4 * k + j]; lu[4 * k + j] = lu[4 * piv + j]; lu[4 * piv + j] = t;
+            }
+            int t = perm[k]; perm[k] = perm[piv]; perm[piv] = t;
+        }
+        if (big != 0.0) {
+            for (int i = k + 1; i < 4; ++i) lu[4 * i + k] /= lu[4 * k + k];
+            for (int i = k + 1; i < 4; ++i)
+                for (int j = k + 1; j < 4; ++j) lu[4 * i + j] -= lu[4 * i + k] * lu[4 * k + j];
+        }
+    }
+    for (int col = 0; col < 4; ++col) {
+        double y[4];
+        for (int i = 0; i < 4; ++i) y[i] = (perm[i] == col) ? 1.0 : 0.0;
+        for (int i = 1; i < 4; ++i)
+            for (int j = 0; j < i; ++j) y[i] -= lu[4 * i + j] * y[j];
+        for (int i = 3; i >= 0; --i) {
+            for (int j = i + 1; j < 4; ++j) y[i] -= lu[4 * i + j] * y[j];
+            y[i] /= lu[4 * i + i];
+        }
+        for (int i = 0; i < 4; ++i) R[4 * i + col] = y[i];
+    }
+}
+
+static void mm4(const double *A, const double *B, double *R)
+{
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = A[4 * i] * B[j];
+            for (int k = 1; k < 4; ++k) s = s + A[4 * i + k] * B[4 * k + j];
+            R[4 * i + j] = s;
+        }
+}
+
+static void mv4(const double *A, const double *v, double *r)
+{
+    for (int i = 0; i < 4; ++i) {
+        double s = A[4 * i] * v[0];
+        for (int k = 1; k < 4; ++k) s = s + A[4 * i + k] * v[k];
+        r[i] = s;
+    }
+}
+
+/* multiply_gaussian (predictions.h:183-188) */
+static void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
+{
+    double i1[16], i2[16], sum[16], nc[16], t1[16], t2[16], v1[4], v2[4];
+    inv4(c1, i1);
+    inv4(c2, i2);
+    for (int k = 0; k < 16; ++k) sum[k] = i1[k] + i2[k];
+    inv4(sum, nc);
+    mm4(nc, i1, t1);
+    mm4(nc, i2, t2);
+    mv4(t1, m1, v1);
+    mv4(t2, m2, v2);
+    for (int k = 0; k < 4; ++k) m1[k] = v1[k] + v2[k];
+    memcpy(c1, nc, sizeof nc);
+}
+
+/* divide_by_prior (predictions.h:446-463) */
+static void divide_prior(double *m, double *c, const double *p)
+{
+    double mp[4] = {0, 0, p[0], p[3]};
+    double ip[16] = {0};
+    ip[10] = (2. * p[1]) / p[2];
+    ip[15] = (2. * p[4]) / p[5];
+    double ic[16], d[16], nc[16], a[4], bvec[4], r[4];
+    inv4(c, ic);
+    for (int k = 0; k < 16; ++k) d[k] = ic[k] - ip[k];
+    inv4(d, nc);
+    mv4(ic, m, a);
+    mv4(ip, mp, bvec);
+    for (int k = 0; k < 4; ++k) r[k] = a[k] - bvec[k];
+    mv4(nc, r, m);
+    memcpy(c, nc, sizeof nc);
+}
+
+static void reverse_state(double *m, double *C)
+{   /* reverse_mean / reverse_cov (predictions.h:278-301) */
+    m[2] = -m[2]; m[3] = -m[3];
+    C[2] = -C[2]; C[8] = -C[8]; C[3] = -C[3]; C[12] = -C[12];
+    C[6] = -C[6]; C[9] = -C[9]; C[7] = -C[7]; C[13] = -C[13];
+}
+
+static void div_r_transform(double *m, double *C, const double *p, int binomial)
+{   /* the per-daughter map of mean_cov_after_division_r (predictions.h:214-237) */
+    double var_dx = p[9], var_dg = p[10];
+    if (binomial) {
+        C[0] += var_dx;
+        C[5] = 8. * var_dx * (m[1] * m[1] + C[5]) + 2. * var_dg * m[1] + 8. * C[5];
+        C[1] = C[4] = 2. * m[1] * var_dx + 4. * C[1];
+        C[9] *= 2; C[6] *= 2; C[13] *= 2; C[7] *= 2;
+        m[0] += log(2.);
+        m[1] *= 2;
+    } else {
+        for (int j = 0; j < 4; ++j) { C[4 + j] *= 2.0; C[4 * j + 1] *= 2.0; }
+        C[0] = var_dx + C[0];
+        C[5] = var_dg + C[5];
+        m[0] = m[0] + log(2.);
+        m[1] = 2.0 * m[1];
+    }
+}
+
+static const double *seg_params(const double *params, int n_seg, const int32_t *seg, int64_t r)
+{
+    int s = seg ? seg[r] : 0;
+    if (s < 0 || s >= n_seg) s = 0;
+    return params + 11 * s;
+}
+
+static void neg_ou(const double *p, double *q)
+{   /* mean_cov_model_r (predictions.h:191-198): ml, mq, beta negated */
+    for (int k = 0; k < 11; ++k) q[k] = p[k];
+    q[0] = -p[0]; q[3] = -p[3]; q[6] = -p[6];
+}
+
+int ora_predict(const ora_forest *f, const double *params, int n_seg, double *state,
+                double *fwd, double *bwd, double *comb)
+{
+    int64_t n_order = 0;
+    int64_t *order = dfs_preorder(f, &n_order);
+    const int32_t *seg = f->segment;
+    double *F = fwd ? fwd : (double *)malloc((size_t)f->n_rows * ORA_STATE * sizeof(double));
+    double *B = bwd ? bwd : (double *)malloc((size_t)f->n_rows * ORA_STATE * sizeof(double));
+
+    /* forward: prediction_forward (predictions.h:93-173), pre-order */
+    for (int64_t oi = 0; oi < n_order; ++oi) {
+        int64_t c = order[oi];
+        double *m = state + ORA_STATE * c, *C = m + 4;
+        int64_t r0 = f->row_off[c], r1 = f->row_off[c + 1];
+        if (f->parent[c] == -1) {
+            root_init(f, m, C, seg_params(params, n_seg, seg, r0));
+        } else {
+            int64_t pc = f->parent[c];
+            int64_t plast = f->row_off[pc + 1] - 1;
+            const double *pm = state + ORA_STATE * pc;
+            after_division(m, C, pm, pm + 4, f->time[r0] - f->time[plast],
+                           seg_params(params, n_seg, seg, plast), f->div_binomial);
+        }
+        for (int64_t r = r0; r < r1; ++r) {
+            const double *p = seg_params(params, n_seg, seg, r);
+            double x0 = f->log_length[r] - m[0];
+            double x1 = f->fp[r] - m[1];
+            ora_innov v;
+            innovation(m, C, p, f->noise_scaled, f->fp_auto, &v);
+            posterior(m, C, x0, x1, &v);
+            memcpy(F + ORA_STATE * r, m, ORA_STATE * sizeof(double));
+            if (r < r1 - 1) ora_mean_cov_model(m, C, f->time[r + 1] - f->time[r], p);
+        }
+    }
+
+    /* backward: prediction_backward (predictions.h:368-444), post-order = reverse of a
+     * pre-order that visits d2 before d1 */
+    {
+        int64_t n = f->n_cells, k = 0, sp = 0;
+        int64_t *post = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+        int64_t *stack = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+        for (int64_t r = 0; r < n; ++r) {
+            if (f->parent[r] != -1) continue;
+            int64_t base = k;
+            stack[sp++] = r;
+            while (sp) {
+                int64_t c = stack[--sp];
+                post[k++] = c;
+                if (f->d1[c] >= 0) stack[sp++] = f->d1[c];
+                if (f->d2[c] >= 0) stack[sp++] = f->d2[c];
+            }
+            for (int64_t i = base, j = k - 1; i < j; ++i, --j) {
+                int64_t t = post[i]; post[i] = post[j]; post[j] = t;
+            }
+        }
+        for (int64_t oi = 0; oi < k; ++oi) {
+            int64_t c = post[oi];
+            double *m = state + ORA_STATE * c, *C = m + 4;
+            int64_t r0 = f->row_off[c], r1 = f->row_off[c + 1];
+            const double *pinit = seg_params(params, n_seg, seg, r1 - 1);
+            if (f->d1[c] == -1 && f->d2[c] == -1) {
+                /* init_sc_distribution_r leaf branch (predictions.h:317-332) */
+                m[0] = f->leaf_mean_xg[0];
+                m[1] = f->leaf_mean_xg[1];
+                C[0] = f->leaf_var_xg[0];
+                C[5] = f->leaf_var_xg[1];
+                m[2] = -pinit[0];
+                m[3] = -pinit[3];
+                C[10] = pinit[2] / (2. * pinit[1]);
+                C[15] = pinit[5] / (2. * pinit[4]);
+            } else {
+                /* mean_cov_after_division_r (predictions.h:201-275) */
+                int64_t a1 = f->d1[c];
+                const double *dm = state + ORA_STATE * a1;
+                memcpy(m, dm, ORA_STATE * sizeof(double));
+                div_r_transform(m, C, pinit, f->div_binomial);
+                if (f->d2[c] >= 0) {
+                    double m2[ORA_STATE];
+                    memcpy(m2, state + ORA_STATE * f->d2[c], sizeof m2);
+                    div_r_transform(m2, m2 + 4, pinit, f->div_binomial);
+                    mult_gauss(m, C, m2, m2 + 4);
+                }
+                double q[11];
+                neg_ou(pinit, q);
+                ora_mean_cov_model(m, C, f->time[f->row_off[a1]] - f->time[r1 - 1], q);
+            }
+            for (int64_t r = r1 - 1; r >= r0; --r) {
+                double *dst = B + ORA_STATE * r;
+                memcpy(dst, m, ORA_STATE * sizeof(double));
+                reverse_state(dst, dst + 4);
+                const double *p = seg_params(params, n_seg, seg, r);
+                double x0 = f->log_length[r] - m[0];
+                double x1 = f->fp[r] - m[1];
+                ora_innov v;
+                innovation(m, C, p, f->noise_scaled, f->fp_auto, &v);
+                posterior(m, C, x0, x1, &v);
+                if (r > r0) {
+                    double q[11];
+                    neg_ou(seg_params(params, n_seg, seg, r - 1), q);
+                    ora_mean_cov_model(m, C, f->time[r] - f->time[r - 1], q);
+                }
+            }
+        }
+        free(post);
+        free(stack);
+    }
+
+    /* combine_predictions (predictions.h:466-499), per row, cells in input order */
+    if (comb) {
+        for (int64_t c = 0; c < f->n_cells; ++c) {
+            int64_t r0 = f->row_off[c], r1 = f->row_off[c + 1];
+            for (int64_t r = r0; r < r1; ++r) {
+                double tm[ORA_STATE];
+                memcpy(tm, F + ORA_STATE * r, sizeof tm);
+                mult_gauss(tm, tm + 4, B + ORA_STATE * r, B + ORA_STATE * r + 4);
+                const double *p;
+                if (r == r0) {
+                    if (f->parent[c] == -1) p = seg_params(params, n_seg, seg, r0);
+                    else p = seg_params(params, n_seg, seg, f->row_off[f->parent[c] + 1] - 1);
+                } else {
+                    p = seg_params(params, n_seg, seg, r);
+                }
+                divide_prior(tm, tm + 4, p);
+                memcpy(comb + ORA_STATE * r, tm, sizeof tm);
+            }
+        }
+    }
+    if (!fwd) free(F);
+    if (!bwd) free(B);
+    free(order);
+    return 0;
+}

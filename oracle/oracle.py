@@ -1,0 +1,143 @@
+"""ctypes front-end of the CPU oracle (oracle/liboracle.so).  TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg -- never by
+the product package.  See ggp_oracle.h for what is restated from where and the pinning
+status ("parity unpinned" for the Eigen-dependent part: the reference cannot be built
+here without Eigen 3.3.7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_FADDEEVA = os.path.join(HERE, "_ref", "libfaddeeva_ref.so")
+
+
+class OraForest(ctypes.Structure):
+    _fields_ = [("n_cells", ctypes.c_int64), ("n_rows", ctypes.c_int64),
+                ("row_off", ctypes.c_void_p), ("parent", ctypes.c_void_p), ("d1", ctypes.c_void_p),
+                ("d2", ctypes.c_void_p), ("time", ctypes.c_void_p), ("log_length", ctypes.c_void_p),
+                ("fp", ctypes.c_void_p), ("segment", ctypes.c_void_p),
+                ("root_mean_xg", ctypes.c_double * 2), ("root_var_xg", ctypes.c_double * 2),
+                ("leaf_mean_xg", ctypes.c_double * 2), ("leaf_var_xg", ctypes.c_double * 2),
+                ("noise_scaled", ctypes.c_int), ("div_binomial", ctypes.c_int), ("fp_auto", ctypes.c_double)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.ora_dawson.restype = ctypes.c_double
+        L.ora_dawson.argtypes = [ctypes.c_double]
+        L.ora_tauint.restype = ctypes.c_double
+        L.ora_tauint.argtypes = [ctypes.c_int] + [ctypes.c_double] * 5
+        L.ora_mean_cov_model.restype = None
+        L.ora_mean_cov_model.argtypes = [dp, dp, ctypes.c_double, dp]
+        L.ora_cross_cov_model.restype = None
+        L.ora_cross_cov_model.argtypes = [dp, dp, ctypes.c_double, dp, dp]
+        L.ora_total_loglik.restype = ctypes.c_double
+        L.ora_total_loglik.argtypes = [ctypes.POINTER(OraForest), dp, dp,
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), dp]
+        L.ora_predict.restype = ctypes.c_int
+        L.ora_predict.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, dp]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def make_forest(a: dict) -> OraForest:
+    """a: the arrays dict of gfp_gaussian_process_amd.HostForest (.a)"""
+    f = OraForest()
+    keep = {k: np.ascontiguousarray(a[k]) for k in
+            ("row_offset", "parent", "daughter1", "daughter2", "time", "log_length", "fp", "segment")}
+    f._keep = keep
+    f.n_cells = len(keep["parent"])
+    f.n_rows = len(keep["time"])
+    f.row_off = keep["row_offset"].ctypes.data
+    f.parent = keep["parent"].ctypes.data
+    f.d1 = keep["daughter1"].ctypes.data
+    f.d2 = keep["daughter2"].ctypes.data
+    f.time = keep["time"].ctypes.data
+    f.log_length = keep["log_length"].ctypes.data
+    f.fp = keep["fp"].ctypes.data
+    f.segment = keep["segment"].ctypes.data if len(keep["segment"]) else None
+    f.root_mean_xg[:] = list(a["root_mean_xg"])
+    f.root_var_xg[:] = list(a["root_var_xg"])
+    f.leaf_mean_xg[:] = list(a["leaf_mean_xg"])
+    f.leaf_var_xg[:] = list(a["leaf_var_xg"])
+    f.noise_scaled = int(a["noise_scaled"])
+    f.div_binomial = int(a["division_binomial"])
+    f.fp_auto = float(a["fp_auto"])
+    return f
+
+
+class OracleForest:
+    """CPU oracle over the same arrays, with its own carried state."""
+
+    def __init__(self, arrays: dict):
+        self.f = make_forest(arrays)
+        self.state = np.zeros((self.f.n_cells, 20))
+        self.cell_ll = np.zeros(self.f.n_cells)
+
+    def total_likelihood(self, params):
+        p = np.ascontiguousarray(params, np.float64)
+        nc, nr = ctypes.c_int64(), ctypes.c_int64()
+        v = lib().ora_total_loglik(ctypes.byref(self.f), _dp(p), _dp(self.state), ctypes.byref(nc),
+                                   ctypes.byref(nr), _dp(self.cell_ll))
+        return v, nc.value, nr.value
+
+    def reset_state(self):
+        self.state[:] = 0.0
+
+    def predict(self, params_per_segment):
+        p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
+        st = np.zeros((self.f.n_cells, 20))
+        out = [np.zeros((self.f.n_rows, 20)) for _ in range(3)]
+        lib().ora_predict(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(st), *(_dp(o) for o in out))
+        return tuple(out)
+
+
+def dawson(x: float) -> float:
+    return lib().ora_dawson(float(x))
+
+
+def tauint(k: int, a: float, b: float, c: float, t1: float, t0: float = 0.0) -> float:
+    return lib().ora_tauint(k, a, b, c, t1, t0)
+
+
+def mean_cov_model(mean, cov, t: float, p7):
+    m = np.ascontiguousarray(mean, np.float64).copy()
+    C = np.ascontiguousarray(cov, np.float64).reshape(16).copy()
+    p = np.ascontiguousarray(p7, np.float64)
+    lib().ora_mean_cov_model(_dp(m), _dp(C), float(t), _dp(p))
+    return m, C.reshape(4, 4)
+
+
+def faddeeva_ref():
+    """Faddeeva::Dawson(double) of the reference's own Faddeeva.cc, compiled in place into
+    oracle/_ref by `make -C oracle ref` (only where /root/reference exists)."""
+    if not os.path.exists(REF_FADDEEVA):
+        return None
+    L = ctypes.CDLL(REF_FADDEEVA)
+    fn = L._ZN8Faddeeva6DawsonEd
+    fn.restype = ctypes.c_double
+    fn.argtypes = [ctypes.c_double]
+    return fn
