@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Benchmark: cell-timepoint Kalman updates/s of the lineage-tree log-likelihood.
+
+Workload (BASELINE.json configs[1], "C2"): a synthetic forest of 1,000 trees x 200 rows
+per GPU (root 100 rows + two daughters of 50, dt = 1 min, simulated from the model SDE with
+the example parameters, Philox4x32 keyed by (seed, tree)); one step = one full
+total-log-likelihood evaluation (likelihood.h:125-174 semantics, carried root state) with
+the inputs resident in HBM, plus -- for N > 1 -- the one all_gather of the per-rank
+partial (RCCL over xGMI).  Weak scaling: rank r evaluates trees [r*T, (r+1)*T).
+
+  python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group]
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (k_loglik_level),
+timed with HIP events on the engine's own stream; `cpu_baseline` is the CPU oracle
+(oracle/, a single-threaded C port of the reference path) timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
+P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
+             3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
+SEED = 20261015
+
+
+def cpu_baseline(hf, budget_s: float):
+    """time the CPU oracle on the same forest: whole evaluations until `budget_s` elapsed"""
+    from oracle import oracle as O
+    of = O.OracleForest(hf.a)
+    first = None
+    n_eval, t0 = 0, time.perf_counter()
+    while True:
+        v = of.total_likelihood(P_EXAMPLE)[0]
+        if first is None:
+            first = v
+        n_eval += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return first, n_eval * hf.n_rows / el, n_eval, el
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--trees", type=int, default=1000, help="trees per GPU")
+    ap.add_argument("--rows", type=int, default=200, help="rows per tree")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle work (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedObjective
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # ---- this rank's forest (weak scaling), resident on the GPU before timing ----
+    hf = g.HostForest.synthetic(args.trees, args.rows, seed=SEED, first_tree=rank * args.trees)
+    fg = g.Forest(hf, device=local, kernel=args.kernel)
+    obj = ShardedObjective(fg) if world > 1 else fg
+    rows_rank = hf.n_rows
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        obj.total_likelihood(P_EXAMPLE)
+
+    # ---- timed region: exactly K steps ----
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ll = obj.total_likelihood(P_EXAMPLE)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_rows = rows_rank * world * args.steps
+    value = total_rows / el
+
+    # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
+    fg.enable_profile()
+    ms_tot, rows_tot, n_launch = 0.0, 0, 0
+    for _ in range(max(3, min(args.steps, 10))):
+        fg.total_likelihood(P_EXAMPLE)
+        ms, rows = fg.launch_profile()
+        ms_tot += sum(ms)
+        rows_tot += sum(rows)
+        n_launch += len(ms)
+    avg_ms = ms_tot / max(n_launch, 1)
+    bytes_per_launch = BYTES_PER_UPDATE * rows_tot / max(n_launch, 1)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    info = fg.info()
+
+    result = None
+    if rank == 0:
+        result = {
+            "metric": "cell-timepoint Kalman updates/s",
+            "value": value,
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * el / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (model-SDE simulated forest, Philox4x32 seed 20261015)",
+            "config": {
+                "workload": f"C2: synthetic forest {args.trees} trees x {args.rows} timepoints per GPU "
+                            f"(root {args.rows // 2} + 2 x {args.rows // 4} rows), single total-log-likelihood "
+                            "evaluation per step, scaled noise + binomial division, example parameters",
+                "trees_per_gpu": args.trees, "rows_per_gpu": rows_rank, "levels": info["levels"],
+                "kernel": args.kernel, "parallelism": f"forest sharded by whole trees, {world} rank(s)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_loglik_level",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "bytes_per_update": BYTES_PER_UPDATE,
+                "avg_launch_ms": avg_ms,
+                "launches_timed": n_launch,
+                "note": "algorithmic bytes only; the path is FP64-latency/VALU bound (DESIGN.md)",
+            },
+            "total_log_likelihood": ll,
+        }
+        if world == 1 and not args.no_cpu:
+            fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
+            ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)
+            result["cpu_baseline"] = {
+                "value": rate, "unit": "updates/s", "cores": 1, "kind": "port",
+                "sample": f"{n_eval} full evaluations of the same {rows_rank}-row forest "
+                          f"({cel:.1f} s, single thread, oracle/ggp_oracle.c -O3)",
+            }
+            result["ll_rel_err_vs_cpu"] = abs(fresh - ref) / abs(ref)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    fg.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

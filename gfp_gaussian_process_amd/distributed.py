@@ -1,0 +1,118 @@
+"""Multi-GPU forest sharding: one process per GPU, torch.distributed over RCCL (xGMI).
+
+Trees are independent (no cross-tree term in total_likelihood, likelihood.h:125-159), so
+the forest is split into whole trees, balanced by longest-processing-time bin packing on
+row count (ties: critical-path length, then tree order).  Each rank keeps its shard's
+device-resident data and carried root state; one objective call = every rank evaluates
+its shard, then ONE collective exchanges one double per rank (all_gather), and the
+partials are summed in rank order so the result is bitwise reproducible run to run.
+The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
+Scan samples and optimiser steps stay sequential (carried state), only the forest is
+parallel.
+"""
+from __future__ import annotations
+
+import heapq
+import math
+
+import numpy as np
+
+from .forest import Forest, HostForest, LikelihoodIsNan
+
+
+def tree_sizes(hf: HostForest):
+    """(roots, rows per tree, critical path rows per tree) in root order"""
+    a = hf.a
+    ro = a["row_offset"]
+    rows_cell = np.diff(ro)
+    d1, d2 = a["daughter1"], a["daughter2"]
+    roots = hf.roots
+    tot, crit = [], []
+    for r in roots:
+        stack = [(int(r), int(rows_cell[r]))]
+        s, best = 0, 0
+        while stack:
+            c, path = stack.pop()
+            s += int(rows_cell[c])
+            best = max(best, path)
+            for ch in (d1[c], d2[c]):
+                if ch >= 0:
+                    stack.append((int(ch), path + int(rows_cell[ch])))
+        tot.append(s)
+        crit.append(best)
+    return roots, np.array(tot, np.int64), np.array(crit, np.int64)
+
+
+def lpt_partition(weights, world: int, secondary=None):
+    """Longest-processing-time bin packing: returns `world` lists of item indices.
+    Deterministic: items by (-weight, -secondary, index), ties on bins by (load, rank)."""
+    weights = np.asarray(weights, np.int64)
+    sec = np.zeros_like(weights) if secondary is None else np.asarray(secondary, np.int64)
+    order = sorted(range(len(weights)), key=lambda i: (-int(weights[i]), -int(sec[i]), i))
+    heap = [(0, r) for r in range(world)]
+    bins = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        bins[r].append(i)
+        heapq.heappush(heap, (load + int(weights[i]), r))
+    return [sorted(b) for b in bins]
+
+
+def shard(hf: HostForest, rank: int, world: int) -> HostForest:
+    """rank's whole-tree sub-forest (global init statistics kept)."""
+    roots, tot, crit = tree_sizes(hf)
+    parts = lpt_partition(tot, world, crit)
+    return hf.subset_trees(roots[parts[rank]])
+
+
+def combine_partials(partials, nan_flags):
+    """rank-order sum; first NaN = lowest rank that saw one"""
+    for r, flag in enumerate(nan_flags):
+        if flag:
+            return math.nan, r
+    s = 0.0
+    for v in partials:
+        s = s + float(v)
+    return s, -1
+
+
+class ShardedObjective:
+    """total_likelihood over a forest sharded across the ranks of a process group.
+
+    device_forest: this rank's Forest (or any object with .total_likelihood(params)).
+    """
+
+    def __init__(self, device_forest, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.f = device_forest
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        self.dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                                      if backend == "nccl" else torch.device("cpu"))
+        self._send = torch.zeros(2, dtype=torch.float64, device=self.dev)
+        self._recv = torch.zeros(2 * self.world, dtype=torch.float64, device=self.dev)
+
+    def local(self, params):
+        try:
+            return self.f.total_likelihood(params), False, None
+        except LikelihoodIsNan as e:
+            return math.nan, True, e
+
+    def total_likelihood(self, params) -> float:
+        v, isnan, err = self.local(params)
+        if self.world == 1:
+            if isnan:
+                raise err
+            return v
+        self._send[0] = v
+        self._send[1] = 1.0 if isnan else 0.0
+        self.dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+        got = self._recv.cpu().numpy().reshape(self.world, 2)
+        total, nan_rank = combine_partials(got[:, 0], got[:, 1] != 0)
+        if nan_rank >= 0:
+            raise err if (err is not None and nan_rank == self.dist.get_rank(self.group)) else \
+                LikelihoodIsNan(-1, -1, f"rank {nan_rank}")
+        return total

@@ -1,0 +1,110 @@
+"""World-size-2 gloo tests of the forest sharding + the one collective per objective call.
+
+The per-rank partial comes from the CPU oracle here (no GPU in this container); on the
+GPU box the same ShardedObjective wraps the HIP engine's Forest and runs over RCCL.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.usefixtures("built")
+
+P0 = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]
+
+
+class _OracleShard:
+    def __init__(self, hf):
+        from oracle import oracle as O
+        self.o = O.OracleForest(hf.a)
+
+    def total_likelihood(self, params):
+        from gfp_gaussian_process_amd import LikelihoodIsNan
+        v, c, r = self.o.total_likelihood(params)
+        if math.isnan(v):
+            raise LikelihoodIsNan(c, r)
+        return v
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedObjective, shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        full = g.HostForest.synthetic(12, 40)
+        # make tree sizes uneven so LPT matters
+        mine = shard(full, rank, world)
+        obj = ShardedObjective(_OracleShard(mine))
+        vals = [obj.total_likelihood(P0) for _ in range(3)]
+        bad = list(P0)
+        bad[2] = -1.0
+        try:
+            obj.total_likelihood(bad)
+            nan_ok = False
+        except g.LikelihoodIsNan:
+            nan_ok = True
+        q.put((rank, vals, mine.n_cells, nan_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_sum_equals_unsharded_oracle():
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    full = g.HostForest.synthetic(12, 40)
+    of = O.OracleForest(full.a)
+    want = [of.total_likelihood(P0)[0] for _ in range(3)]
+    for rank, vals, ncells, nan_ok in res:
+        assert nan_ok
+        assert ncells == 18                      # 12 equal trees -> 6 trees (18 cells) per rank
+        for v, w in zip(vals, want):
+            assert v == pytest.approx(w, rel=1e-13)
+    assert res[0][1] == res[1][1]                # every rank holds the same total (rank-order sum)
+
+
+def test_lpt_partition_balances_and_is_deterministic():
+    from gfp_gaussian_process_amd.distributed import lpt_partition
+    w = [100, 90, 80, 70, 60, 50, 40, 30, 20, 10]
+    parts = lpt_partition(w, 3)
+    loads = [sum(w[i] for i in p) for p in parts]
+    assert sorted(i for p in parts for i in p) == list(range(10))
+    assert max(loads) - min(loads) <= 10
+    assert parts == lpt_partition(w, 3)
+    assert lpt_partition(w, 1) == [list(range(10))]
+    assert lpt_partition([], 2) == [[], []]
+
+
+def test_shards_cover_the_forest_exactly():
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import shard
+    full = g.HostForest.synthetic(7, 40, with_ids=True)
+    ids = []
+    for r in range(3):
+        ids += shard(full, r, 3).ids
+    assert sorted(ids) == sorted(full.ids)

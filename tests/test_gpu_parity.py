@@ -1,0 +1,214 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Tolerance (BASELINE north star): total log-likelihood within 1e-9 relative; topology
+bit-exact (host ingest, tests/test_host.py).  Observed: ~1e-11 (libm ulp differences
+between ocml and glibc; DESIGN.md "Parity").
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+
+REL = 1e-9
+PARAMS = json.load(open(os.path.join(GOLDEN, "oracle_example.json")))
+CONFIGS = [(k.split("/")[0], k.split("/")[1], [float.fromhex(x) for x in v["params"]]) for k, v in PARAMS.items()]
+
+
+def _rel(a, b):
+    return abs(a - b) / abs(b)
+
+
+@pytest.fixture(scope="module")
+def example_forests(example_paths):
+    import gfp_gaussian_process_amd as g
+    out = {}
+    for noise, div, _ in CONFIGS:
+        out[(noise, div)] = g.HostForest.from_csv(example_paths["csv"], example_paths["config"], -1, noise, div)
+    return out
+
+
+@pytest.mark.parametrize("noise,div,params", CONFIGS, ids=[f"{a}-{b}" for a, b, _ in CONFIGS])
+def test_example_carried_state_chain(example_forests, noise, div, params):
+    """fresh call + two calls on carried root state (predictions.h:63-78), vs the oracle"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = example_forests[(noise, div)]
+    fg = g.Forest(hf)
+    of = O.OracleForest(hf.a)
+    for call in range(3):
+        vg = fg.total_likelihood(params)
+        vo, nc, nr = of.total_likelihood(params)
+        assert nc == -1
+        assert _rel(vg, vo) < REL, (call, vg, vo)
+
+
+def test_example_state_matches_oracle(example_forests):
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = example_forests[("scaled", "binomial")]
+    P = CONFIGS[0][2]
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    for _ in range(2):
+        fg.total_likelihood(P)
+        of.total_likelihood(P)
+    sg, so = fg.state(), of.state
+    assert np.all(np.isfinite(sg))
+    # means relative; covariances relative to sqrt(Cii Cjj).  The latent q is weakly
+    # observed: perturbing every exp() of the oracle itself by +-1 ulp moves mean_q by
+    # 1.5e-7 and the normalised cov by 4e-7 (DESIGN.md "Parity"), so the bound is 2e-6.
+    assert np.max(np.abs(sg[:, :4] - so[:, :4]) / np.abs(so[:, :4]).clip(1e-300)) < 2e-6
+    Cg, Co = sg[:, 4:].reshape(-1, 4, 4), so[:, 4:].reshape(-1, 4, 4)
+    d = np.sqrt(np.abs(np.einsum("nii->ni", Co)))
+    scale = d[:, :, None] * d[:, None, :]
+    assert np.max(np.abs(Cg - Co) / scale) < 2e-6
+
+
+def test_reset_state_and_determinism(example_forests):
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P = CONFIGS[0][2]
+    a, b = g.Forest(hf), g.Forest(hf)
+    first = a.total_likelihood(P)
+    assert b.total_likelihood(P) == first            # bitwise reproducible
+    second = a.total_likelihood(P)
+    assert second != first                            # carried state changes the objective
+    a.reset_state()
+    assert a.total_likelihood(P) == first             # "fresh cells" again
+    assert a.total_likelihood(P) == second
+
+
+def test_nan_reported_like_reference(example_forests):
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = example_forests[("scaled", "binomial")]
+    P = list(CONFIGS[0][2])
+    P[2] = -1.0                                       # var_lambda < 0: sqrt(a<0) in the propagator
+    _, oc, orow = O.OracleForest(hf.a).total_likelihood(P)
+    with pytest.raises(g.LikelihoodIsNan) as e:
+        g.Forest(hf).total_likelihood(P)
+    assert (e.value.cell, e.value.row) == (oc, orow)
+    assert e.value.cell_id == hf.ids[oc]
+
+
+@pytest.mark.parametrize("n_trees,rows", [(1000, 200), (37, 4), (5, 9)])
+def test_synthetic_forest_vs_oracle(n_trees, rows):
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(n_trees, rows)
+    P = CONFIGS[0][2]
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    for _ in range(2):
+        vg = fg.total_likelihood(P)
+        vo = of.total_likelihood(P)[0]
+        assert _rel(vg, vo) < REL
+
+
+def _ragged_roots(n_cells=40, seed=3):
+    """roots only, 1..13 rows each, irregular time steps: rows of synthetic root cells with
+    every 5th row dropped (dt = 2 gaps) -- data stay consistent with the model"""
+    import gfp_gaussian_process_amd as g
+    base = g.HostForest.synthetic(n_cells, 40)
+    ro_b = base.a["row_offset"]
+    a = dict(base.a)
+    rows, lens = [], []
+    for i in range(n_cells):
+        r0 = ro_b[3 * i]                                  # the root cell of tree i (20 rows)
+        keep = [r0 + k for k in range(20) if k % 5 != 3][: 1 + (i * 7) % 13]
+        rows += keep
+        lens.append(len(keep))
+    rows = np.array(rows)
+    a["row_offset"] = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    a["parent"] = np.full(n_cells, -1, np.int32)
+    a["daughter1"] = np.full(n_cells, -1, np.int32)
+    a["daughter2"] = np.full(n_cells, -1, np.int32)
+    for k in ("time", "log_length", "fp", "segment"):
+        a[k] = base.a[k][rows].copy()
+    return g.HostForest(a)
+
+
+def test_single_cells_and_ragged_rows():
+    """1-row cells (no propagation) and dt = 2 steps (t != 1 exercises every t-power term)"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = _ragged_roots()
+    assert np.any(np.diff(hf.a["time"]) == 2.0) and np.any(np.diff(hf.a["row_offset"]) == 1)
+    P = CONFIGS[0][2]
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    for _ in range(2):
+        assert _rel(fg.total_likelihood(P), of.total_likelihood(P)[0]) < REL
+
+
+def test_rescaled_time_units():
+    """time in hours (rescale_time = 60): dt = 1/60, a non-integer step"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(50, 40)
+    hf.a["time"] = hf.a["time"] / 60.0
+    P = list(CONFIGS[0][2])
+    for i in (0, 1, 2, 4, 5, 6):                          # rates per hour
+        P[i] *= 60.0 if i in (0, 1, 4, 6) else 1.0
+    P[2] *= 60.0 ** 3
+    P[5] *= 60.0
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    vg, vo = fg.total_likelihood(P), of.total_likelihood(P)[0]
+    assert math.isfinite(vo) and _rel(vg, vo) < REL
+
+
+def test_empty_forest():
+    import gfp_gaussian_process_amd as g
+    a = dict(g.HostForest.synthetic(1, 8).a)
+    for k in ("parent", "daughter1", "daughter2", "segment"):
+        a[k] = np.zeros(0, np.int32)
+    for k in ("time", "log_length", "fp"):
+        a[k] = np.zeros(0)
+    a["row_offset"] = np.zeros(1, np.int64)
+    assert g.Forest(g.HostForest(a)).total_likelihood(CONFIGS[0][2]) == 0.0
+
+
+def test_invalid_forest_rejected():
+    import gfp_gaussian_process_amd as g
+    a = dict(g.HostForest.synthetic(2, 8).a)
+    a["parent"] = a["parent"].copy()
+    a["parent"][1] = 99
+    with pytest.raises(g.GGPError, match="out of range"):
+        g.Forest(g.HostForest(a))
+
+
+def test_shards_on_one_device_sum_to_whole():
+    """additivity over trees (the multi-GPU invariant), here with 3 shards on cuda:0"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import combine_partials, shard
+    full = g.HostForest.synthetic(300, 60)
+    P = CONFIGS[0][2]
+    whole = g.Forest(full)
+    parts = [g.Forest(shard(full, r, 3)) for r in range(3)]
+    for _ in range(2):
+        w = whole.total_likelihood(P)
+        s, _ = combine_partials([p.total_likelihood(P) for p in parts], [False] * 3)
+        assert _rel(s, w) < 1e-12
+
+
+def test_baseline_size_properties():
+    """BASELINE C2 / C3 sizes: oracle agreement on C2, additivity + finiteness on C3"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    P = CONFIGS[0][2]
+    c2 = g.HostForest.synthetic(1000, 200)
+    assert _rel(g.Forest(c2).total_likelihood(P), O.OracleForest(c2.a).total_likelihood(P)[0]) < REL
+    c3 = g.HostForest.synthetic(10000, 200)
+    f3 = g.Forest(c3)
+    v = f3.total_likelihood(P)
+    assert math.isfinite(v)
+    lo, hi = g.HostForest.synthetic(5000, 200), g.HostForest.synthetic(5000, 200, first_tree=5000)
+    # shards carry the full forest's init statistics
+    for h in (lo, hi):
+        for k in ("root_mean_xg", "root_var_xg", "leaf_mean_xg", "leaf_var_xg"):
+            h.a[k] = c3.a[k]
+    s = g.Forest(lo).total_likelihood(P) + g.Forest(hi).total_likelihood(P)
+    assert _rel(s, v) < 1e-12

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Every GPU step is bounded by its own timeout and the chain stops at the first failure.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-r01}
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 120 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
+cat gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; cat gpurun_out/bench_${TAG}.err; exit 1; }
+cat gpurun_out/bench_${TAG}.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o bench --output-format csv -- python3 bench.py --steps 10 --no-cpu > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/prof_${TAG}.err || { echo "rocprof failed"; tail -20 gpurun_out/prof_${TAG}.err; exit 1; }
+find gpurun_out/prof_${TAG} -name "*stats*" | head
