@@ -2,19 +2,14 @@
 //
 // What is here, and the reference it restates:
 //   ggp_dawson          Faddeeva::Dawson / w_im / w_im_y100  Faddeeva.cc:467-471, 1458-1888
-//   ggp_propagate       mean_cov_model + mean_x..cov_qq       mean_cov_model.h:9-274
 //   ggp_innovation,     S = C[0:2,0:2] + D, S^-1, ll term,    likelihood.h:26-32, 53-69
 //   ggp_ll_term,        posterior                             predictions.h:84-89
 //   ggp_posterior
-//   ggp_after_division  mean_cov_after_division               predictions.h:18-61
+// The propagator (mean_cov_model.h) is in ggp_prop.h.
 //
 // Evaluation order follows the reference expression by expression (no FMA contraction:
-// the library is built with -ffp-contract=off), but every *bitwise-identical*
-// subexpression of one propagation step is evaluated once: the reference's 59 tauint
-// calls (118 Dawson, ~264 exp per step) collapse to 45 distinct integrals built from
-// 14 Dawson values and 74 distinct exponentials.  Identical inputs give identical bits,
-// so the CSE changes no rounding; transcendental libm differences (ocml vs glibc, <= 1
-// ulp) move the total log-likelihood by ~1e-11 relative (measured).
+// the library is built with -ffp-contract=off).  Transcendental libm differences (ocml vs
+// glibc, <= 1 ulp) move the total log-likelihood by ~1e-11 relative (measured).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -31,35 +26,31 @@
 // Dawson: w_im on y = 1/(1+|x|) with 97 polynomial pieces (degree 6..8, zero-padded to 9),
 // Taylor for y100 >= 97, continued fraction for |x| > 45.
 // ------------------------------------------------------------------------------------------
-GGP_DEV double ggp_w_im_pos(double x)   // x >= 0, finite
+// branch-free on |x| <= 45 so that the 14 Dawson values of a step overlap their table loads;
+// `tab` is the coefficient table (constant memory, or an LDS copy in the group schedule)
+GGP_DEV double ggp_w_im_abs(double ax, const double *tab)
 {
-    if (x > 45.0) {
-        if (x > 5e7) return GGP_ISPI / x;
-        return GGP_ISPI * ((x * x) * (x * x - 4.5) + 2) / (x * ((x * x) * (x * x - 5) + 3.75));
-    }
-    const double y100 = 100.0 / (1.0 + x);
-    const int k = (int)y100;
-    if (k < GGP_DAWSON_NINT) {
-        const double *c = ggp_dawson_coef + GGP_DAWSON_NCOEF * k;
-        const double t = 2.0 * y100 - (double)(2 * k + 1);
-        return c[0] + (c[1] + (c[2] + (c[3] + (c[4] + (c[5] + (c[6] + (c[7] + c[8] * t) * t) * t) * t) * t) * t) * t) * t;
-    }
-    const double x2 = x * x;
-    const double *c = ggp_dawson_taylor;
-    return x * (c[0] - x2 * (c[1] - x2 * (c[2] - x2 * (c[3] - x2 * c[4]))));
+    const double y100 = 100.0 / (1.0 + ax);
+    const int k = min((int)y100, GGP_DAWSON_NINT - 1);
+    const double *c = tab + GGP_DAWSON_NCOEF * k;
+    const double t = 2.0 * y100 - (double)(2 * k + 1);
+    const double poly = c[0] + (c[1] + (c[2] + (c[3] + (c[4] + (c[5] + (c[6] + (c[7] + c[8] * t) * t) * t) * t) * t) * t) * t) * t;
+    const double x2 = ax * ax;
+    const double *tc = ggp_dawson_taylor;
+    const double taylor = ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4]))));
+    const double cf = ax > 5e7 ? GGP_ISPI / ax
+                               : GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2) / (ax * ((ax * ax) * (ax * ax - 5) + 3.75));
+    return ax > 45.0 ? cf : (y100 >= (double)GGP_DAWSON_NINT ? taylor : poly);
 }
 
-GGP_DEV double ggp_dawson(double x)
+GGP_DEV double ggp_dawson_tab(double x, const double *tab)
 {
     if (x != x) return x;
-    if (x >= 0.0) return GGP_SPI2 * ggp_w_im_pos(x);
-    // negative: -w_im_y100(100/(1-x), -x), and the same odd continued fraction
-    if (x < -45.0) {
-        if (x < -5e7) return GGP_SPI2 * (GGP_ISPI / x);
-        return GGP_SPI2 * (GGP_ISPI * ((x * x) * (x * x - 4.5) + 2) / (x * ((x * x) * (x * x - 5) + 3.75)));
-    }
-    return GGP_SPI2 * (-ggp_w_im_pos(-x));
+    const double w = ggp_w_im_abs(fabs(x), tab);
+    return GGP_SPI2 * (x < 0.0 ? -w : w);
 }
+
+GGP_DEV double ggp_dawson(double x) { return ggp_dawson_tab(x, ggp_dawson_coef); }
 
 // ------------------------------------------------------------------------------------------
 // Parameters and state
@@ -67,301 +58,6 @@ GGP_DEV double ggp_dawson(double x)
 struct ggp_params {           // Parameters.h:175 order
     double p[11];
 };
-
-// ------------------------------------------------------------------------------------------
-// tauint integrals from precomputed pieces (mean_cov_model.h:9-67).
-//   ec  = exp(c)            ea0/ea1 = exp(t_i*(b + a*t_i))
-//   E0/E1 = exp(-(b*b)/(4a) + c + z_i^2)   (k >= 1 forms)
-//   Z0/Z1 = exp(a*t_i^2 + b*t_i + c)       (k == 0 form)
-//   D0/D1 = Dawson(z_i), z_i = (b + 2a t_i)/(2 sqrt a)
-// ------------------------------------------------------------------------------------------
-struct ggp_pk {               // per-step scalars shared by all integrals
-    double a, two_sa, two_a, four_p15, eight_p25, sixteen_p35, four_aa, m2sa, p2sa;
-};
-
-GGP_DEV double ggp_tau0(const ggp_pk &k, double Z0, double D0, double Z1, double D1)
-{   // zerotauint, mean_cov_model.h:9-21
-    double x = 2. * (-Z0 * D0 + Z1 * (D1));
-    return x / k.two_sa;
-}
-
-GGP_DEV double ggp_tau1(const ggp_pk &k, double ec, double ea0, double ea1, double B,
-                        double E0, double D0, double E1, double D1)
-{   // onetauint, mean_cov_model.h:23-34
-    double x = (k.m2sa * ec * (ea0 - ea1) + B * 2. * (E0 * D0 - E1 * D1));
-    return x / k.four_p15;
-}
-
-GGP_DEV double ggp_tau2(const ggp_pk &k, double ec, double ea0, double ea1, double t0, double t1,
-                        double B, double E0, double D0, double E1, double D1)
-{   // twotauint, mean_cov_model.h:36-49
-    double x = (k.p2sa * ec * (ea0 * (B - k.two_a * t0) - ea1 * (B - k.two_a * t1))
-                + (E0 * (k.two_a - B * B) * 2. * D0 + E1 * (-k.two_a + B * B) * 2. * D1));
-    return x / k.eight_p25;
-}
-
-GGP_DEV double ggp_tau3(const ggp_pk &k, double ec, double ea0, double ea1, double t0, double t1,
-                        double B, double E0, double D0, double E1, double D1)
-{   // treetauint, mean_cov_model.h:51-67
-    const double a = k.a;
-    double x = (k.m2sa * ec
-                * ((B * B) * (ea0 - ea1) - k.two_a * ea0 * (2. + B * t0) + k.two_a * ea1 * (2 + B * t1)
-                   + k.four_aa * (ea0 * (t0 * t0) - ea1 * (t1 * t1))))
-               + E0 * B * (-6. * a + B * B) * 2. * D0
-               - E1 * B * (-6 * a + B * B) * 2. * D1;
-    return x / k.sixteen_p35;
-}
-
-// ------------------------------------------------------------------------------------------
-// One propagation step z(t0) -> z(t0 + t) with no division: mean_cov_model.h:211-274.
-// m[4], C[16] row-major in/out.  Reads the mean, the diagonal and the UPPER triangle only;
-// writes a symmetric C (as the reference's nC(i,j) = nC(j,i) assignments do).
-// q = {ml, gl, sl2, mq, gq, sq2, beta} (already sign-flipped for mean_cov_model_r).
-// ------------------------------------------------------------------------------------------
-GGP_DEV void ggp_propagate(double *m, double *C, const double t, const double ml, const double gl,
-                           const double sl2, const double mq, const double gq, const double sq2,
-                           const double b)
-{
-    const double bx = m[0], bg = m[1], bl = m[2], bq = m[3];
-    const double Cxx = C[0], Cxg = C[1], Cxl = C[2], Cxq = C[3];
-    const double Cgg = C[5], Cgl = C[6], Cgq = C[7];
-    const double Cll = C[10], Clq = C[11], Cqq = C[15];
-
-    // ---- per-step scalars ----
-    ggp_pk k;
-    const double a = Cll / 2.;
-    const double sa = sqrt(a);
-    k.a = a;
-    k.two_sa = 2. * sa;
-    k.m2sa = -2. * sa;
-    k.p2sa = 2. * sa;
-    k.two_a = 2. * a;
-    k.four_p15 = 4. * pow(a, 1.5);
-    k.eight_p25 = 8. * pow(a, 2.5);
-    k.sixteen_p35 = 16. * pow(a, 3.5);
-    k.four_aa = 4 * (a * a);
-    const double four_a = 4. * a;
-    const double t2 = 2 * t;
-
-    // the six exponents-of-s coefficients b (tauint 2nd argument)
-    const double B1 = b + bl + Cxl;
-    const double B2 = b + bl + Cxl - gq;
-    const double B3 = b + bl + 2 * Cxl;
-    const double B4 = b + bl + 2 * Cxl - gq;
-    const double B5 = b + bl + Cxl + gq;
-    const double B6 = b + bl + 2 * Cxl + gq;
-    // the ten constants c (tauint 3rd argument)
-    const double cA = bx + Cxx / 2. - b * t;
-    const double cB = bx + Cxx / 2. - b * t - gl * t;
-    const double cJ = bx + Cxx / 2. - b * t - gq * t;
-    const double cG = bx + Cxx / 2. - 2 * b * t;
-    const double cC = 2 * (bx + Cxx - b * t);
-    const double cE = 2 * bx + 2 * Cxx - 2 * b * t;
-    const double cD = 2 * bx + 2 * Cxx - (2 * b + gq) * t;
-    const double cF = 2 * bx + 2 * Cxx - 2 * b * t + gq * t;
-    const double cH = 2 * bx + 2 * Cxx - 2 * b * t - 2 * gq * t;
-    const double cI = -b * t + bx + Cxx / 2. - gq * t;
-
-    // ---- 14 Dawson values D(B, t_i), z = (B + 2a t_i)/(2 sqrt a) ----
-    const double z10 = B1 / k.two_sa, z1t = (B1 + k.two_a * t) / k.two_sa;
-    const double z20 = B2 / k.two_sa, z2t = (B2 + k.two_a * t) / k.two_sa;
-    const double z30 = B3 / k.two_sa, z3t = (B3 + k.two_a * t) / k.two_sa, z32 = (B3 + k.two_a * t2) / k.two_sa;
-    const double z40 = B4 / k.two_sa, z4t = (B4 + k.two_a * t) / k.two_sa, z42 = (B4 + k.two_a * t2) / k.two_sa;
-    const double z50 = B5 / k.two_sa, z5t = (B5 + k.two_a * t) / k.two_sa;
-    const double z6t = (B6 + k.two_a * t) / k.two_sa, z62 = (B6 + k.two_a * t2) / k.two_sa;
-    const double D10 = ggp_dawson(z10), D1t = ggp_dawson(z1t);
-    const double D20 = ggp_dawson(z20), D2t = ggp_dawson(z2t);
-    const double D30 = ggp_dawson(z30), D3t = ggp_dawson(z3t), D32 = ggp_dawson(z32);
-    const double D40 = ggp_dawson(z40), D4t = ggp_dawson(z4t), D42 = ggp_dawson(z42);
-    const double D50 = ggp_dawson(z50), D5t = ggp_dawson(z5t);
-    const double D6t = ggp_dawson(z6t), D62 = ggp_dawson(z62);
-
-    // ---- exp(c) (== exp(a*0 + B*0 + c), the k=0 lower limit at t0 = 0) ----
-    const double ecA = exp(cA), ecB = exp(cB), ecJ = exp(cJ), ecG = exp(cG), ecC = exp(cC);
-    const double ecD = exp(cD), ecE = exp(cE), ecF = exp(cF), ecI = exp(cI);
-    // ---- exp(t_i (B + a t_i)) for k >= 1 (t_i = 0 gives exactly 1) ----
-    const double ea1t = exp(t * (B1 + a * t)), ea2t = exp(t * (B2 + a * t));
-    const double ea3t = exp(t * (B3 + a * t)), ea4t = exp(t * (B4 + a * t));
-    const double ea32 = exp(t2 * (B3 + a * t2)), ea42 = exp(t2 * (B4 + a * t2));
-    // ---- -(B*B)/(4a) ----
-    const double n1 = -(B1 * B1) / four_a, n2 = -(B2 * B2) / four_a;
-    const double n3 = -(B3 * B3) / four_a, n4 = -(B4 * B4) / four_a;
-#define GGP_E(n, c, z) exp((n) + (c) + (z) * (z))
-#define GGP_Z(B, c, ti) exp(a * ((ti) * (ti)) + (B) * (ti) + (c))
-
-    // ---- k = 1 integrals (onetauint) ----
-    const double O_B2_cA = ggp_tau1(k, ecA, 1.0, ea2t, B2, GGP_E(n2, cA, z20), D20, GGP_E(n2, cA, z2t), D2t);
-    const double O_B1_cA = ggp_tau1(k, ecA, 1.0, ea1t, B1, GGP_E(n1, cA, z10), D10, GGP_E(n1, cA, z1t), D1t);
-    const double O_B1_cB = ggp_tau1(k, ecB, 1.0, ea1t, B1, GGP_E(n1, cB, z10), D10, GGP_E(n1, cB, z1t), D1t);
-    const double O_B2_cB = ggp_tau1(k, ecB, 1.0, ea2t, B2, GGP_E(n2, cB, z20), D20, GGP_E(n2, cB, z2t), D2t);
-    const double O_B1_cJ = ggp_tau1(k, ecJ, 1.0, ea1t, B1, GGP_E(n1, cJ, z10), D10, GGP_E(n1, cJ, z1t), D1t);
-    const double O_B2_cJ = ggp_tau1(k, ecJ, 1.0, ea2t, B2, GGP_E(n2, cJ, z20), D20, GGP_E(n2, cJ, z2t), D2t);
-    // ---- k = 0 integrals (zerotauint) over [0, t] ----
-    const double Z_B1_cA = ggp_tau0(k, ecA, D10, GGP_Z(B1, cA, t), D1t);
-    const double Z_B2_cA = ggp_tau0(k, ecA, D20, GGP_Z(B2, cA, t), D2t);
-    const double Z_B1_cB = ggp_tau0(k, ecB, D10, GGP_Z(B1, cB, t), D1t);
-    const double Z_B2_cB = ggp_tau0(k, ecB, D20, GGP_Z(B2, cB, t), D2t);
-    const double Z_B1_cJ = ggp_tau0(k, ecJ, D10, GGP_Z(B1, cJ, t), D1t);
-    const double Z_B2_cJ = ggp_tau0(k, ecJ, D20, GGP_Z(B2, cJ, t), D2t);
-    const double Z_B2_cI = ggp_tau0(k, ecI, D20, GGP_Z(B2, cI, t), D2t);
-    const double Z_B5_cI = ggp_tau0(k, ecI, D50, GGP_Z(B5, cI, t), D5t);
-    // ---- k = 2 integrals (twotauint) ----
-    const double T_B2_cA = ggp_tau2(k, ecA, 1.0, ea2t, 0.0, t, B2, GGP_E(n2, cA, z20), D20, GGP_E(n2, cA, z2t), D2t);
-    const double T_B2_cB = ggp_tau2(k, ecB, 1.0, ea2t, 0.0, t, B2, GGP_E(n2, cB, z20), D20, GGP_E(n2, cB, z2t), D2t);
-    const double T_B2_cJ = ggp_tau2(k, ecJ, 1.0, ea2t, 0.0, t, B2, GGP_E(n2, cJ, z20), D20, GGP_E(n2, cJ, z2t), D2t);
-
-    // ---- simple exponentials ----
-    const double ebt = exp(b * t), ebglt = exp((b + gl) * t), e2bt = exp(2 * b * t);
-    const double ebgqt = exp((b + gq) * t), egl = exp(-gl * t), egq = exp(-gq * t);
-
-    // ---- means (mean_cov_model.h:73-87) ----
-    double nm[4];
-    nm[0] = bx + ml * t + (bl - ml) * (1 - egl) / gl;
-    nm[1] = bg / ebt + Clq * O_B2_cA + mq * Z_B1_cA + (bq + Cxq - mq) * Z_B2_cA;
-    nm[2] = ml + (bl - ml) * egl;
-    nm[3] = mq + (bq - mq) * egq;
-
-    // ---- cov_xg (mean_cov_model.h:97-115) ----
-    const double nxg =
-        (bg * bx) / ebt + Cxg / ebt + (bg * bl) / (ebt * gl) + Cgl / (ebt * gl)
-        - (bg * bl) / (ebglt * gl) - Cgl / (ebglt * gl) - (bg * ml) / (ebt * gl)
-        + (bg * ml) / (ebglt * gl) + (bg * ml * t) / ebt
-        + (Cxl * mq + (Cll * mq) / gl) * O_B1_cA
-        - (Cll * mq * O_B1_cB) / gl
-        + (bx * Clq + bq * Cxl + Cxl * Cxq + Clq * Cxx + (bq * Cll) / gl + (bl * Clq) / gl
-           + (Clq * Cxl) / gl + (Cll * Cxq) / gl - (Clq * ml) / gl - Cxl * mq - (Cll * mq) / gl
-           + Clq * ml * t) * O_B2_cA
-        + (-((bq * Cll) / gl) - (bl * Clq) / gl - (Clq * Cxl) / gl - (Cll * Cxq) / gl
-           + (Clq * ml) / gl + (Cll * mq) / gl) * O_B2_cB
-        + (Clq * Cxl + (Cll * Clq) / gl) * T_B2_cA
-        - (Cll * Clq * T_B2_cB) / gl
-        + (bx * mq + Cxx * mq + (bl * mq) / gl + (Cxl * mq) / gl - (ml * mq) / gl + ml * mq * t) * Z_B1_cA
-        + (-((bl * mq) / gl) - (Cxl * mq) / gl + (ml * mq) / gl) * Z_B1_cB
-        + (bq * bx + Cxq + bx * Cxq + bq * Cxx + Cxq * Cxx + (bl * bq) / gl + Clq / gl
-           + (bq * Cxl) / gl + (bl * Cxq) / gl + (Cxl * Cxq) / gl - (bq * ml) / gl - (Cxq * ml) / gl
-           - bx * mq - Cxx * mq - (bl * mq) / gl - (Cxl * mq) / gl + (ml * mq) / gl + bq * ml * t
-           + Cxq * ml * t - ml * mq * t) * Z_B2_cA
-        + (-((bl * bq) / gl) - Clq / gl - (bq * Cxl) / gl - (bl * Cxq) / gl - (Cxl * Cxq) / gl
-           + (bq * ml) / gl + (Cxq * ml) / gl + (bl * mq) / gl + (Cxl * mq) / gl - (ml * mq) / gl) * Z_B2_cB
-        - nm[1] * nm[0];
-
-    // ---- cov_xl, cov_xq (mean_cov_model.h:117-123) ----
-    const double nxl = sl2 / (2 * (gl * gl)) * ((1 - egl) * (1 - egl)) + Cll * egl * (1 - egl) / gl + Cxl * egl;
-    const double nxq = Clq * (1 - egl) * egq / gl + Cxq * egq;
-
-    // ---- cov_gl (mean_cov_model.h:172-181) ----
-    const double ngl =
-        (bg * bl) / ebglt + Cgl / ebglt + (bg * ml) / ebt - (bg * ml) / ebglt
-        + Cll * mq * O_B1_cB + Clq * ml * O_B2_cA
-        + (bq * Cll + bl * Clq + Clq * Cxl + Cll * Cxq - Clq * ml - Cll * mq) * O_B2_cB
-        + Cll * Clq * T_B2_cB + ml * mq * Z_B1_cA
-        + (bl * mq + Cxl * mq - ml * mq) * Z_B1_cB
-        + (bq * ml + Cxq * ml - ml * mq) * Z_B2_cA
-        + (bl * bq + Clq + bq * Cxl + bl * Cxq + Cxl * Cxq - bq * ml - Cxq * ml - bl * mq - Cxl * mq
-           + ml * mq) * Z_B2_cB
-        - nm[1] * nm[2];
-
-    // ---- cov_gq (mean_cov_model.h:183-196) ----
-    const double ngq =
-        (bg * bq) / ebgqt + Cgq / ebgqt + (bg * mq) / ebt - (bg * mq) / ebgqt
-        + Clq * mq * O_B1_cJ + Clq * mq * O_B2_cA
-        + (2 * bq * Clq + 2 * Clq * Cxq - 2 * Clq * mq) * O_B2_cJ
-        + (Clq * Clq) * T_B2_cJ + (mq * mq) * Z_B1_cA
-        + (bq * mq + Cxq * mq - (mq * mq)) * Z_B1_cJ
-        + (bq * mq + Cxq * mq - (mq * mq)) * Z_B2_cA
-        - (sq2 * Z_B2_cI) / (2. * gq)
-        + ((bq * bq) + Cqq + 2 * bq * Cxq + (Cxq * Cxq) - 2 * bq * mq - 2 * Cxq * mq + (mq * mq)) * Z_B2_cJ
-        + (sq2 * Z_B5_cI) / (2. * gq)
-        - nm[1] * nm[3];
-
-    // ---- cov_gg (mean_cov_model.h:125-170): its 28 integrals ----
-    // exponent pieces on [t, 2t] and at 2t
-    const double Z_B1_cG = ggp_tau0(k, ecG, D10, GGP_Z(B1, cG, t), D1t);
-    const double Z_B2_cG = ggp_tau0(k, ecG, D20, GGP_Z(B2, cG, t), D2t);
-    const double zB3cCt = GGP_Z(B3, cC, t), zB4cCt = GGP_Z(B4, cC, t);
-    const double zB3cEt = GGP_Z(B3, cE, t), zB4cEt = GGP_Z(B4, cE, t);
-    const double Z_B3_cC = ggp_tau0(k, ecC, D30, zB3cCt, D3t);
-    const double Z_B4_cC = ggp_tau0(k, ecC, D40, zB4cCt, D4t);
-    const double Z_B3_cE = ggp_tau0(k, ecE, D30, zB3cEt, D3t);
-    const double Z_B4_cE = ggp_tau0(k, ecE, D40, zB4cEt, D4t);
-    const double Z_B3_cE_2 = ggp_tau0(k, zB3cEt, D3t, GGP_Z(B3, cE, t2), D32);
-    const double Z_B3_cC_2 = ggp_tau0(k, zB3cCt, D3t, GGP_Z(B3, cC, t2), D32);
-    const double Z_B3_cD_2 = ggp_tau0(k, GGP_Z(B3, cD, t), D3t, GGP_Z(B3, cD, t2), D32);
-    const double Z_B4_cE_2 = ggp_tau0(k, zB4cEt, D4t, GGP_Z(B4, cE, t2), D42);
-    const double Z_B4_cC_2 = ggp_tau0(k, zB4cCt, D4t, GGP_Z(B4, cC, t2), D42);
-    const double Z_B4_cF_2 = ggp_tau0(k, GGP_Z(B4, cF, t), D4t, GGP_Z(B4, cF, t2), D42);
-    const double Z_B6_cH_2 = ggp_tau0(k, GGP_Z(B6, cH, t), D6t, GGP_Z(B6, cH, t2), D62);
-
-    const double eB3cC0 = GGP_E(n3, cC, z30), eB3cCt = GGP_E(n3, cC, z3t), eB3cC2 = GGP_E(n3, cC, z32);
-    const double eB4cC0 = GGP_E(n4, cC, z40), eB4cCt = GGP_E(n4, cC, z4t), eB4cC2 = GGP_E(n4, cC, z42);
-    const double eB4cE0 = GGP_E(n4, cE, z40), eB4cEt = GGP_E(n4, cE, z4t), eB4cE2 = GGP_E(n4, cE, z42);
-    const double O_B1_cG = ggp_tau1(k, ecG, 1.0, ea1t, B1, GGP_E(n1, cG, z10), D10, GGP_E(n1, cG, z1t), D1t);
-    const double O_B2_cG = ggp_tau1(k, ecG, 1.0, ea2t, B2, GGP_E(n2, cG, z20), D20, GGP_E(n2, cG, z2t), D2t);
-    const double O_B3_cC = ggp_tau1(k, ecC, 1.0, ea3t, B3, eB3cC0, D30, eB3cCt, D3t);
-    const double O_B4_cC = ggp_tau1(k, ecC, 1.0, ea4t, B4, eB4cC0, D40, eB4cCt, D4t);
-    const double O_B3_cC_2 = ggp_tau1(k, ecC, ea3t, ea32, B3, eB3cCt, D3t, eB3cC2, D32);
-    const double O_B3_cD_2 = ggp_tau1(k, ecD, ea3t, ea32, B3, GGP_E(n3, cD, z3t), D3t, GGP_E(n3, cD, z32), D32);
-    const double O_B4_cE = ggp_tau1(k, ecE, 1.0, ea4t, B4, eB4cE0, D40, eB4cEt, D4t);
-    const double O_B4_cE_2 = ggp_tau1(k, ecE, ea4t, ea42, B4, eB4cEt, D4t, eB4cE2, D42);
-    const double O_B4_cC_2 = ggp_tau1(k, ecC, ea4t, ea42, B4, eB4cCt, D4t, eB4cC2, D42);
-    const double O_B4_cF_2 = ggp_tau1(k, ecF, ea4t, ea42, B4, GGP_E(n4, cF, z4t), D4t, GGP_E(n4, cF, z42), D42);
-    const double T_B2_cG = ggp_tau2(k, ecG, 1.0, ea2t, 0.0, t, B2, GGP_E(n2, cG, z20), D20, GGP_E(n2, cG, z2t), D2t);
-    const double T_B4_cC = ggp_tau2(k, ecC, 1.0, ea4t, 0.0, t, B4, eB4cC0, D40, eB4cCt, D4t);
-    const double T_B4_cC_2 = ggp_tau2(k, ecC, ea4t, ea42, t, t2, B4, eB4cCt, D4t, eB4cC2, D42);
-    const double H_B4_cC = ggp_tau3(k, ecC, 1.0, ea4t, 0.0, t, B4, eB4cC0, D40, eB4cCt, D4t);
-    const double H_B4_cC_2 = ggp_tau3(k, ecC, ea4t, ea42, t, t2, B4, eB4cCt, D4t, eB4cC2, D42);
-#undef GGP_E
-#undef GGP_Z
-
-    const double ngg =
-        ((bg * bg) + Cgg) / e2bt
-        + 2 * Cgl * mq * O_B1_cG
-        + (mq * (2 * Clq + gq * mq) * O_B3_cC) / gq
-        + 2 * (bq * Cgl + bg * Clq + Clq * Cxg + Cgl * Cxq - Cgl * mq) * O_B2_cG
-        + (((bq * bq) * gq + Cqq * gq + 4 * bq * Cxq * gq + 4 * (Cxq * Cxq) * gq - 2 * Clq * mq
-            - 2 * bq * gq * mq - 4 * Cxq * gq * mq + gq * (mq * mq)) * O_B4_cC) / gq
-        - (mq * mq) * O_B3_cC_2
-        - (2 * Clq * mq * O_B3_cD_2) / gq
-        - (sq2 * O_B4_cE) / (2. * gq)
-        + (sq2 * O_B4_cE_2) / (2. * gq)
-        + (-(bq * bq) - Cqq - 4 * bq * Cxq - 4 * (Cxq * Cxq) + 2 * bq * mq + 4 * Cxq * mq - (mq * mq)
-           + 4 * bq * Clq * t + 8 * Clq * Cxq * t - 4 * Clq * mq * t) * O_B4_cC_2
-        + (2 * Clq * mq * O_B4_cF_2) / gq
-        + (Clq * Clq) * H_B4_cC
-        - (Clq * Clq) * H_B4_cC_2
-        + 2 * Cgl * Clq * T_B2_cG
-        + (2 * bq * Clq + 4 * Clq * Cxq - 2 * Clq * mq) * T_B4_cC
-        + (-2 * bq * Clq - 4 * Clq * Cxq + 2 * Clq * mq + 2 * (Clq * Clq) * t) * T_B4_cC_2
-        + (2 * bg * mq + 2 * Cxg * mq) * Z_B1_cG
-        + ((2 * bq * mq) / gq + (4 * Cxq * mq) / gq - (2 * (mq * mq)) / gq) * Z_B3_cC
-        + (2 * bg * bq + 2 * Cgq + 2 * bq * Cxg + 2 * bg * Cxq + 2 * Cxg * Cxq - 2 * bg * mq
-           - 2 * Cxg * mq) * Z_B2_cG
-        + ((-2 * bq * mq) / gq - (4 * Cxq * mq) / gq + (2 * (mq * mq)) / gq) * Z_B4_cC
-        + (sq2 * Z_B3_cE) / (2. * (gq * gq))
-        + (sq2 * Z_B3_cE_2) / (2. * (gq * gq))
-        + 2 * (mq * mq) * t * Z_B3_cC_2
-        + ((-2 * bq * mq) / gq - (4 * Cxq * mq) / gq + (2 * (mq * mq)) / gq) * Z_B3_cD_2
-        - (sq2 * Z_B4_cE) / (2. * (gq * gq))
-        - (sq2 * t * Z_B4_cE_2) / gq
-        + (2 * (bq * bq) * t + 2 * Cqq * t + 8 * bq * Cxq * t + 8 * (Cxq * Cxq) * t - 4 * bq * mq * t
-           - 8 * Cxq * mq * t + 2 * (mq * mq) * t) * Z_B4_cC_2
-        + ((2 * bq * mq) / gq + (4 * Cxq * mq) / gq - (2 * (mq * mq)) / gq) * Z_B4_cF_2
-        - (sq2 * Z_B6_cH_2) / (2. * (gq * gq))
-        - (nm[1] * nm[1]);
-
-    // ---- cov_xx, cov_ll, cov_lq, cov_qq (mean_cov_model.h:93-95, 198-208) ----
-    const double nxx = Cll * ((1 - egl) * (1 - egl)) / (gl * gl) + 2 * Cxl * (1 - egl) / gl + Cxx
-                       + sl2 / (2 * pow(gl, 3)) * (2 * gl * t - 3 + 4 * egl - (egl * egl));
-    const double nll = Cll * (egl * egl) + sl2 / (2 * gl) * (1 - (egl * egl));
-    const double nlq = Clq * egl * egq;
-    const double nqq = sq2 / (2 * gq) * (1 - (egq * egq)) + Cqq * (egq * egq);
-
-    m[0] = nm[0]; m[1] = nm[1]; m[2] = nm[2]; m[3] = nm[3];
-    C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
-    C[4] = nxg;  C[5] = ngg;  C[6] = ngl;  C[7] = ngq;
-    C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[11] = nlq;
-    C[12] = nxq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
-}
 
 // ------------------------------------------------------------------------------------------
 // Kalman measurement step (likelihood.h:53-95, predictions.h:84-89)
@@ -431,25 +127,3 @@ GGP_DEV void ggp_posterior(double *m, double *C, const double x0, const double x
         for (int j = 0; j < 4; ++j) C[4 * i + j] = C[4 * i + j] - (KS0[i] * K[j] + KS1[i] * K[4 + j]);
 }
 
-// mean_cov_after_division (predictions.h:18-61); m/C hold a copy of the parent's state.
-GGP_DEV void ggp_after_division(double *m, double *C, const double dt, const ggp_params &P,
-                                const int binomial, const double log2)
-{
-    const double *p = P.p;
-    ggp_propagate(m, C, dt, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
-    const double var_dx = p[9], var_dg = p[10];
-    if (binomial) {
-        C[0] += var_dx;
-        C[1] = C[4] = m[1] / 2. * var_dx + C[1];
-        C[5] = var_dx * (m[1] * m[1] + C[5]) / 2. + var_dg * m[1] / 4. * (1 - var_dx) + C[5] / 4.;
-        C[9] /= 2; C[6] /= 2;
-        C[13] /= 2; C[7] /= 2;
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { C[4 + j] *= 0.5; C[4 * j + 1] *= 0.5; }
-        C[0] = var_dx + C[0];
-        C[5] = var_dg + C[5];
-    }
-    m[0] = m[0] + -log2;
-    m[1] = 0.5 * m[1];
-}

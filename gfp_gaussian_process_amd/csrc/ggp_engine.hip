@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -27,6 +28,8 @@
 
 #include "ggp.h"
 #include "ggp_device.h"
+#include "ggp_prop.h"
+#include "ggp_predict.h"
 
 #define GGP_VERSION "ggp-mi355x 0.1.0 (reference gfp_gaussian_process 0.4.2)"
 
@@ -44,30 +47,26 @@ struct DevForest {
 
 constexpr int kNanNone = 0x7fffffff;
 
-// ------------------------------------------------------------------------------------------
-// likelihood, one lane per cell.  sc_likelihood (likelihood.h:36-103) for every cell of
-// one generation depth.  `cpw` cells per 64-lane wave: < 64 spreads a small level over
-// more SIMDs (latency), 64 packs waves (throughput); results do not depend on it.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
-                                                      const int32_t *__restrict__ cells, int n,
-                                                      int cpw, double *__restrict__ state,
-                                                      double *__restrict__ cell_ll,
-                                                      int32_t *__restrict__ cell_nan)
+// Dawson coefficient table copied to LDS once per workgroup (LDS gather ~100 cycles vs an
+// L2 round trip per coefficient from constant memory)
+constexpr int kDawsonTab = GGP_DAWSON_NINT * GGP_DAWSON_NCOEF;
+GGP_DEV void load_dawson_table(double *s_tab, int lane)
 {
-    const int lane = threadIdx.x;
-    if (lane >= cpw) return;
-    const int i = blockIdx.x * cpw + lane;
-    if (i >= n) return;
-    const int c = cells[i];
-    const double *p = P.p;
-    double m[4], C[16];
-    double *st = state + (size_t)20 * c;
-    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+    for (int k = lane; k < kDawsonTab; k += 64) s_tab[k] = ggp_dawson_coef[k];
+}
+
+// ------------------------------------------------------------------------------------------
+// Cell prologue shared by both schedules: init_sc_distribution (predictions.h:63-82).
+// Root: mean + diagonal from init_cells_f and the parameters; the off-diagonals keep this
+// root's state from the previous evaluation (carried state).  Daughter: a copy of the
+// parent's final posterior, to be propagated over dt and mapped through the division.
+// ------------------------------------------------------------------------------------------
+GGP_DEV bool cell_prologue(const DevForest &F, const double *p, const double *state, int c,
+                           int64_t r0, double *m, double *C, double &dt_div)
+{
     const int par = F.parent[c];
     if (par < 0) {
-        // init_sc_distribution root branch (predictions.h:63-78): the off-diagonals keep
-        // this root's state from the previous evaluation (carried state)
+        const double *st = state + (size_t)20 * c;
 #pragma unroll
         for (int k = 0; k < 16; ++k) C[k] = st[4 + k];
         m[0] = F.root_mean0;
@@ -78,44 +77,338 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
         m[3] = p[3];
         C[10] = p[2] / (2. * p[1]);
         C[15] = p[5] / (2. * p[4]);
-    } else {
-        const double *ps = state + (size_t)20 * par;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = ps[k];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) C[k] = ps[4 + k];
-        const double dt = F.time[r0] - F.time[F.row_off[par + 1] - 1];
-        ggp_after_division(m, C, dt, P, F.binomial, F.log2);
+        dt_div = 0.0;
+        return false;
     }
+    const double *ps = state + (size_t)20 * par;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = ps[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) C[k] = ps[4 + k];
+    dt_div = F.time[r0] - F.time[F.row_off[par + 1] - 1];
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// LANE schedule: one lane per cell.  sc_likelihood (likelihood.h:36-103) for every cell of
+// one generation depth.  `cpw` cells per 64-lane wave: < 64 spreads a small level over
+// more SIMDs (latency), 64 packs waves (throughput); results do not depend on it.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
+                                                      const int32_t *__restrict__ cells, int n,
+                                                      int cpw, double *__restrict__ state,
+                                                      double *__restrict__ cell_ll,
+                                                      int32_t *__restrict__ cell_nan)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    if (lane >= cpw) return;
+    const int i = blockIdx.x * cpw + lane;
+    if (i >= n) return;
+    const int c = cells[i];
+    const double *p = P.p;
+    double m[4], C[16];
+    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+    double dt = 0.0;
+    bool pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+    bool divide = pending;
     double cl = 0.0;
     int nan_row = kNanNone;
-    double tn = F.time[r0], xn = F.logl[r0], gn = F.fp[r0];
     for (int64_t r = r0; r < r1; ++r) {
-        const double tc = tn, x = xn, g = gn;
-        if (r + 1 < r1) {   // prefetch the next row while this one computes
-            tn = F.time[r + 1];
-            xn = F.logl[r + 1];
-            gn = F.fp[r + 1];
+        if (pending) {   // mean_cov_model over dt (likelihood.h:97-101 / predictions.h:28-31)
+            ggp::propagate_lane(m, C, dt, p[0], p[1], p[2], p[3], p[4], p[5], p[6], s_tab);
+            if (divide) {
+                ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                divide = false;
+            }
         }
-        const double x0 = x - m[0];
-        const double x1 = g - m[1];
+        const double x0 = F.logl[r] - m[0];
+        const double x1 = F.fp[r] - m[1];
         ggp_innov v;
         ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
-        const double term = ggp_ll_term(x0, x1, v, F.two_log_2pi);
-        cl += term;
+        cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
         if (cl != cl) {
             nan_row = (int)(r - r0);
             break;
         }
         ggp_posterior(m, C, x0, x1, v);
-        if (r + 1 < r1) ggp_propagate(m, C, tn - tc, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        pending = r + 1 < r1;
+        if (pending) dt = F.time[r + 1] - F.time[r];
     }
+    double *st = state + (size_t)20 * c;
 #pragma unroll
     for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
     for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
     cell_ll[c] = cl;
     cell_nan[c] = nan_row;
+}
+
+// ------------------------------------------------------------------------------------------
+// GROUP schedule: G lanes per cell, 64/G cells per single-wave workgroup.  The Kalman update
+// and the scalar bookkeeping run redundantly in the G lanes of a cell; the propagation's
+// 74 exponentials + 14 Dawson values + 3 powers and then its 45 integrals are spread over
+// the G lanes through LDS (ggp_prop.h tasks), cutting the per-step latency that bounds
+// small forests.  Bitwise identical to the lane schedule.
+// ------------------------------------------------------------------------------------------
+constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI;   // doubles of LDS per cell
+constexpr int kStageB = ggp::NXT + ggp::ND + 3;                  // exp + Dawson + pow tasks
+
+template <int G>
+__global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
+                                                     const int32_t *__restrict__ cells, int n,
+                                                     double *__restrict__ state,
+                                                     double *__restrict__ cell_ll,
+                                                     int32_t *__restrict__ cell_nan)
+{
+    constexpr int CPW = 64 / G;
+    __shared__ double lds[CPW * kSlot];
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    const int slot = lane / G, lg = lane % G;
+    const int i = blockIdx.x * CPW + slot;
+    const bool valid = i < n;
+    double *Xl = lds + slot * kSlot;
+    double *Dl = Xl + ggp::NX;
+    double *Pl = Dl + ggp::ND;
+    double *Il = Pl + ggp::NPW;
+    const double *p = P.p;
+    double m[4] = {0, 0, 0, 0}, C[16] = {0};
+    int c = 0;
+    int64_t r = 0, r1 = 0, r0 = 0;
+    double dt = 0.0;
+    bool pending = false, divide = false;
+    if (valid) {
+        c = cells[i];
+        r0 = F.row_off[c];
+        r1 = F.row_off[c + 1];
+        r = r0;
+        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        divide = pending;
+    }
+    if (lg == 0) Xl[ggp::X_ONE] = 1.0;
+    double cl = 0.0;
+    int nan_row = kNanNone;
+    bool live = valid;
+    while (__any(live)) {   // wave-uniform loop over steps
+        const bool prop = live && pending;
+        ggp::Step S;
+        if (prop) {
+            ggp::step_init(S, m, C, dt, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+            for (int j = lg; j < kStageB; j += G) {
+                if (j < ggp::NXT) {
+                    Xl[j] = ggp::exp_task(S, j);
+                } else if (j < ggp::NXT + ggp::ND) {
+                    Dl[j - ggp::NXT] = ggp::dawson_task(S, j - ggp::NXT, s_tab);
+                } else {
+                    const int q = j - ggp::NXT - ggp::ND;
+                    const double v = ggp::pow_task(S, q);
+                    Pl[q] = v;
+                    Pl[3 + q] = 1.0 / v;
+                }
+            }
+        }
+        __syncthreads();
+        if (prop)
+            for (int j = lg; j < ggp::NI; j += G) Il[j] = ggp::tau_task(S, j, Xl, Dl, Pl);
+        __syncthreads();
+        if (prop) {
+            ggp::outputs(S, Il, Xl, m, C);
+            if (divide) {
+                ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                divide = false;
+            }
+        }
+        if (live) {
+            const double x0 = F.logl[r] - m[0];
+            const double x1 = F.fp[r] - m[1];
+            ggp_innov v;
+            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+            cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
+            if (cl != cl) {
+                nan_row = (int)(r - r0);
+                live = false;
+            } else {
+                ggp_posterior(m, C, x0, x1, v);
+                pending = r + 1 < r1;
+                if (pending) dt = F.time[r + 1] - F.time[r];
+                ++r;
+                live = r < r1;
+            }
+        }
+        __syncthreads();   // LDS slots are rewritten by the next step
+    }
+    if (valid && lg == 0) {
+        double *st = state + (size_t)20 * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[k] = m[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+        cell_ll[c] = cl;
+        cell_nan[c] = nan_row;
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// -p smoother kernels (lane schedule).  Parameters per row come from the segment table.
+// ------------------------------------------------------------------------------------------
+GGP_DEV const double *seg_params(const DevForest &F, const double *ptab, int n_seg, int64_t r)
+{
+    int s = F.seg ? F.seg[r] : 0;
+    if (s < 0 || s >= n_seg) s = 0;
+    return ptab + 11 * s;
+}
+
+GGP_DEV void store20(double *dst, const double *m, const double *C)
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = m[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[4 + k] = C[k];
+}
+
+// prediction_forward / sc_prediction_forward (predictions.h:93-173)
+__global__ __launch_bounds__(64) void k_fwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                  const int32_t *__restrict__ cells, int n, int cpw,
+                                                  double *__restrict__ pstate, double *__restrict__ out)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    if (lane >= cpw) return;
+    const int i = blockIdx.x * cpw + lane;
+    if (i >= n) return;
+    const int c = cells[i];
+    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+    const int par = F.parent[c];
+    // root: segment of its first row; daughter: the parent's last segment (:103-108)
+    const double *pi = seg_params(F, ptab, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);
+    double m[4], C[16], dt = 0.0;
+    bool pending = cell_prologue(F, pi, pstate, c, r0, m, C, dt);
+    bool divide = pending;
+    const double *pprop = pi;
+    for (int64_t r = r0; r < r1; ++r) {
+        if (pending) {
+            ggp::propagate_lane(m, C, dt, pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6], s_tab);
+            if (divide) {
+                ggp::division_map(m, C, pi[9], pi[10], F.binomial, F.log2);
+                divide = false;
+            }
+        }
+        const double *p = seg_params(F, ptab, n_seg, r);
+        const double x0 = F.logl[r] - m[0];
+        const double x1 = F.fp[r] - m[1];
+        ggp_innov v;
+        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+        ggp_posterior(m, C, x0, x1, v);
+        store20(out + (size_t)20 * r, m, C);
+        pending = r + 1 < r1;
+        if (pending) dt = F.time[r + 1] - F.time[r];
+        pprop = p;   // the step t -> t+1 uses row t's parameters (:143-146)
+    }
+    store20(pstate + (size_t)20 * c, m, C);
+}
+
+// prediction_backward / sc_prediction_backward (predictions.h:368-444), levels bottom-up
+__global__ __launch_bounds__(64) void k_bwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                  const int32_t *__restrict__ cells, int n, int cpw,
+                                                  double *__restrict__ pstate, double *__restrict__ out)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    if (lane >= cpw) return;
+    const int i = blockIdx.x * cpw + lane;
+    if (i >= n) return;
+    const int c = cells[i];
+    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+    const double *pi = seg_params(F, ptab, n_seg, r1 - 1);          // :376-378
+    const int d1 = F.d1[c], d2 = F.d2[c];
+    double m[4], C[16];
+    if (d1 < 0 && d2 < 0) {
+        // init_sc_distribution_r leaf branch (:317-332): on top of the forward final state
+        const double *st = pstate + (size_t)20 * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = st[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) C[k] = st[4 + k];
+        m[0] = F.leaf_mean0;
+        m[1] = F.leaf_mean1;
+        C[0] = F.leaf_var0;
+        C[5] = F.leaf_var1;
+        m[2] = -pi[0];
+        m[3] = -pi[3];
+        C[10] = pi[2] / (2. * pi[1]);
+        C[15] = pi[5] / (2. * pi[4]);
+    } else {
+        // mean_cov_after_division_r (:201-275); a cell with only daughter2 does not occur
+        // (build_cell_genealogy fills daughter1 first)
+        const double *s1 = pstate + (size_t)20 * d1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = s1[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) C[k] = s1[4 + k];
+        ggp::division_map_r(m, C, pi[9], pi[10], F.binomial, F.log2);
+        if (d2 >= 0) {
+            double m2[4], C2[16];
+            const double *s2 = pstate + (size_t)20 * d2;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m2[k] = s2[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) C2[k] = s2[4 + k];
+            ggp::division_map_r(m2, C2, pi[9], pi[10], F.binomial, F.log2);
+            ggp::mult_gauss(m, C, m2, C2);
+        }
+        const double dt = F.time[F.row_off[d1]] - F.time[r1 - 1];
+        ggp::propagate_lane(m, C, dt, -pi[0], pi[1], pi[2], -pi[3], pi[4], pi[5], -pi[6], s_tab);
+    }
+    for (int64_t r = r1 - 1; r >= r0; --r) {
+        double rm[4], rC[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rm[k] = m[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rC[k] = C[k];
+        ggp::reverse_state(rm, rC);
+        store20(out + (size_t)20 * r, rm, rC);                    // the prior, before the update
+        const double *p = seg_params(F, ptab, n_seg, r);
+        const double x0 = F.logl[r] - m[0];
+        const double x1 = F.fp[r] - m[1];
+        ggp_innov v;
+        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+        ggp_posterior(m, C, x0, x1, v);
+        if (r > r0) {
+            const double *q = seg_params(F, ptab, n_seg, r - 1);
+            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], -q[0], q[1], q[2], -q[3], q[4], q[5], -q[6], s_tab);
+        }
+    }
+    store20(pstate + (size_t)20 * c, m, C);
+}
+
+// combine_predictions (predictions.h:466-499): one lane per row
+__global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab, int n_seg,
+                                                 const int32_t *__restrict__ prior_seg, int64_t n_rows,
+                                                 const double *__restrict__ fwd, const double *__restrict__ bwd,
+                                                 double *__restrict__ out)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    double m[4], C[16], mb[4], Cb[16];
+    const double *f = fwd + (size_t)20 * r, *b = bwd + (size_t)20 * r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { m[k] = f[k]; mb[k] = b[k]; }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { C[k] = f[4 + k]; Cb[k] = b[4 + k]; }
+    ggp::mult_gauss(m, C, mb, Cb);
+    int s = prior_seg[r];
+    if (s < 0 || s >= n_seg) s = 0;
+    ggp::divide_prior(m, C, ptab + 11 * s);
+    store20(out + (size_t)20 * r, m, C);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -193,6 +486,8 @@ struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0;
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
+    int64_t group_max_cells = 12 * 1024;   // auto: group schedule for levels up to this size
+    int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int kernel_used = GGP_KERNEL_LANE;
     DevForest F{};
     // device buffers
@@ -200,6 +495,7 @@ struct ggp_forest {
     int64_t *d_row_off = nullptr;
     int32_t *d_parent = nullptr, *d_d1 = nullptr, *d_d2 = nullptr, *d_seg = nullptr;
     int32_t *d_level_cells = nullptr, *d_dfs_order = nullptr;
+    int32_t *d_prior_seg = nullptr;   // -p: segment of the stationary prior per row
     double *d_state = nullptr, *d_cell_ll = nullptr;
     int32_t *d_cell_nan = nullptr;
     double *d_out_ll = nullptr;
@@ -225,22 +521,42 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
         const int64_t a = f->level_start[L], b = f->level_start[L + 1];
         const int n = (int)(b - a);
         if (n <= 0) continue;
-        // spread small levels: aim for >= 4 waves per CU before packing lanes
-        const int64_t target_waves = (int64_t)f->n_cu * 8;
-        int cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + target_waves - 1) / target_waves));
-        const int blocks = (n + cpw - 1) / cpw;
         if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof], f->stream));
         }
-        hipLaunchKernelGGL(k_loglik_level, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
-                           f->d_level_cells + a, n, cpw, f->d_state, f->d_cell_ll, f->d_cell_nan);
+        const int64_t n_simd = (int64_t)f->n_cu * 4;
+        const bool group = f->kernel_pref == GGP_KERNEL_GROUP ||
+                           (f->kernel_pref == GGP_KERNEL_AUTO && n <= f->group_max_cells);
+        if (group) {
+            // fewest cells per wave that still fits one wave per SIMD (latency first)
+            int cpw = 1;
+            while (cpw < 8 && (n + cpw - 1) / cpw > n_simd) cpw *= 2;
+            if (f->tune_group_cpw > 0) cpw = f->tune_group_cpw;
+            const int blocks = (n + cpw - 1) / cpw;
+            switch (cpw) {
+            case 1: hipLaunchKernelGGL(k_loglik_group<64>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
+                                       f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
+            case 2: hipLaunchKernelGGL(k_loglik_group<32>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
+                                       f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
+            case 4: hipLaunchKernelGGL(k_loglik_group<16>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
+                                       f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
+            default: hipLaunchKernelGGL(k_loglik_group<8>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
+                                        f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
+            }
+            f->kernel_used = GGP_KERNEL_GROUP;
+        } else {
+            // spread small levels over SIMDs before packing lanes
+            const int64_t target_waves = (int64_t)f->n_cu * 8;
+            int cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + target_waves - 1) / target_waves));
+            if (f->tune_lane_cpw > 0) cpw = f->tune_lane_cpw;
+            const int blocks = (n + cpw - 1) / cpw;
+            hipLaunchKernelGGL(k_loglik_level, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
+                               f->d_level_cells + a, n, cpw, f->d_state, f->d_cell_ll, f->d_cell_nan);
+            f->kernel_used = GGP_KERNEL_LANE;
+        }
         HIPCHK(hipGetLastError());
         if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof + 1], f->stream));
-            int64_t rows = 0;
-            // rows of this level (host copy of offsets kept implicitly via ev_rows)
-            rows = f->ev_rows.empty() ? 0 : f->ev_rows[L];
-            (void)rows;
             f->n_prof++;
         }
     }
@@ -283,7 +599,7 @@ void ggp_forest_destroy(ggp_forest *f)
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
                     (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
-                    (void *)f->d_level_cells, (void *)f->d_dfs_order, (void *)f->d_state,
+                    (void *)f->d_level_cells, (void *)f->d_dfs_order, (void *)f->d_prior_seg, (void *)f->d_state,
                     (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_out_ll,
                     (void *)f->d_out_nan})
         if (p) (void)hipFree(p);
@@ -359,6 +675,13 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess) f->n_cu = prop.multiProcessorCount;
+    f->group_max_cells = (int64_t)f->n_cu * 4 * 12;
+    if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
+    if (const char *e = getenv("GGP_GROUP_CPW")) {
+        const int v = atoi(e);
+        f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+    }
+    if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
     int rc = GGP_OK;
     auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
     check(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? GGP_OK : GGP_EDEV);
@@ -386,6 +709,19 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     if (d->segment) check(dev_upload(&f->d_seg, d->segment, nr));
     check(dev_upload(&f->d_level_cells, level_cells.data(), nc));
     check(dev_upload(&f->d_dfs_order, dfs.data(), nc));
+    {
+        // combine_predictions' prior (predictions.h:475-490): a cell's first row divides by the
+        // parameters that initialised it (its own for a root, the parent's last row otherwise)
+        std::vector<int32_t> prior(nr, 0);
+        if (d->segment) {
+            for (int64_t c = 0; c < nc; ++c) {
+                const int64_t r0 = d->row_offset[c];
+                for (int64_t r = r0; r < d->row_offset[c + 1]; ++r) prior[r] = d->segment[r];
+                if (d->parent[c] >= 0) prior[r0] = d->segment[d->row_offset[d->parent[c] + 1] - 1];
+            }
+        }
+        check(dev_upload(&f->d_prior_seg, prior.data(), nr));
+    }
     check(dev_upload<double>(&f->d_state, nullptr, (size_t)nc * 20));
     check(dev_upload<double>(&f->d_cell_ll, nullptr, nc));
     check(dev_upload<int32_t>(&f->d_cell_nan, nullptr, nc));
@@ -522,9 +858,70 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, 
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd, double *out_bwd,
                 double *out_comb)
 {
-    (void)f; (void)params; (void)n_seg; (void)out_fwd; (void)out_bwd; (void)out_comb;
-    g_last_err = "ggp_predict: not built in this version";
-    return GGP_EINVAL;
+    if (!f || !params || n_seg < 1) { g_last_err = "ggp_predict: null params or n_seg < 1"; return GGP_EINVAL; }
+    HIPCHK(hipSetDevice(f->device));
+    HIPCHK(hipStreamSynchronize(f->stream));
+    const int64_t nc = f->n_cells, nr = f->n_rows;
+    if (nc == 0) return GGP_OK;
+    // fresh cells (main.cpp:434-438): the smoother never touches the likelihood's carried state
+    double *d_ptab = nullptr, *d_pstate = nullptr, *d_fwd = nullptr, *d_bwd = nullptr, *d_comb = nullptr;
+    int rc = GGP_OK;
+    auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+    check(dev_upload(&d_ptab, params, (size_t)n_seg * 11));
+    check(dev_upload<double>(&d_pstate, nullptr, (size_t)nc * 20));
+    check(dev_upload<double>(&d_fwd, nullptr, (size_t)nr * 20));
+    check(dev_upload<double>(&d_bwd, nullptr, (size_t)nr * 20));
+    check(dev_upload<double>(&d_comb, nullptr, (size_t)nr * 20));
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(f->stream);
+        for (double *p : {d_ptab, d_pstate, d_fwd, d_bwd, d_comb})
+            if (p) (void)hipFree(p);
+    };
+    if (rc == GGP_OK && hipMemsetAsync(d_pstate, 0, (size_t)nc * 20 * sizeof(double), f->stream) != hipSuccess)
+        rc = GGP_EDEV;
+    if (rc != GGP_OK) { cleanup(); return rc; }
+    const int n_levels = (int)f->level_start.size() - 1;
+    auto lane_cpw = [&](int n) {
+        const int64_t target_waves = (int64_t)f->n_cu * 8;
+        int cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + target_waves - 1) / target_waves));
+        return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : cpw;
+    };
+    hipError_t e = hipSuccess;
+    for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
+        const int64_t a = f->level_start[L];
+        const int n = (int)(f->level_start[L + 1] - a);
+        if (n <= 0) continue;
+        const int cpw = lane_cpw(n);
+        hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                           f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        e = hipGetLastError();
+    }
+    for (int L = n_levels - 1; L >= 0 && e == hipSuccess; --L) {   // backward: leaves first
+        const int64_t a = f->level_start[L];
+        const int n = (int)(f->level_start[L + 1] - a);
+        if (n <= 0) continue;
+        const int cpw = lane_cpw(n);
+        hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                           f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        const int64_t blocks = (nr + 255) / 256;
+        hipLaunchKernelGGL(k_combine, dim3((unsigned)blocks), dim3(256), 0, f->stream, d_ptab, n_seg,
+                           f->d_prior_seg, nr, d_fwd, d_bwd, d_comb);
+        e = hipGetLastError();
+    }
+    const size_t bytes = (size_t)nr * 20 * sizeof(double);
+    if (e == hipSuccess && out_fwd) e = hipMemcpyAsync(out_fwd, d_fwd, bytes, hipMemcpyDeviceToHost, f->stream);
+    if (e == hipSuccess && out_bwd) e = hipMemcpyAsync(out_bwd, d_bwd, bytes, hipMemcpyDeviceToHost, f->stream);
+    if (e == hipSuccess && out_comb) e = hipMemcpyAsync(out_comb, d_comb, bytes, hipMemcpyDeviceToHost, f->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    cleanup();
+    if (e != hipSuccess) {
+        g_last_err = std::string("ggp_predict: ") + hipGetErrorString(e);
+        return GGP_EDEV;
+    }
+    return GGP_OK;
 }
 
 }  // extern "C"

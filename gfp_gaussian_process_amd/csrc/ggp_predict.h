@@ -1,0 +1,178 @@
+// ggp_predict.h -- the -p smoother on the device (predictions.h:93-499).
+//
+//   k_fwd_level   prediction_forward / sc_prediction_forward  predictions.h:93-173
+//                 (per-row segment parameters; the posterior of every row is stored)
+//   k_bwd_level   prediction_backward / sc_prediction_backward predictions.h:368-444
+//                 (reverse time: ml, mq, beta negated; leaves start on top of the forward
+//                 pass's final state, internal cells fuse both daughters)
+//   k_combine     combine_predictions                          predictions.h:466-499
+//                 (forward x backward, divided by the stationary prior; 5 dense 4x4
+//                 inverses per row by partial-pivot LU, one lane per row)
+// Levels are processed top-down for the forward pass and bottom-up for the backward pass;
+// every row of the combine is independent.
+#pragma once
+#include "ggp_device.h"
+#include "ggp_prop.h"
+
+namespace ggp {
+
+// dense 4x4 inverse by partial-pivot LU (first max |a| pivot, unit-lower L), solved column by
+// column against the identity -- the algorithm of oracle/ggp_oracle.c inv4
+GGP_DEV void inv4(const double *A, double *R)
+{
+    double lu[16];
+    int perm[4] = {0, 1, 2, 3};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lu[i] = A[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int piv = k;
+        double big = fabs(lu[4 * k + k]);
+#pragma unroll
+        for (int i = k + 1; i < 4; ++i) {
+            const double v = fabs(lu[4 * i + k]);
+            if (v > big) { big = v; piv = i; }
+        }
+        if (piv != k) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                // swap rows k and piv without dynamic register indexing
+                double rk = lu[4 * k + j], rp = 0.0;
+#pragma unroll
+                for (int i = k + 1; i < 4; ++i) rp = (i == piv) ? lu[4 * i + j] : rp;
+                lu[4 * k + j] = rp;
+#pragma unroll
+                for (int i = k + 1; i < 4; ++i) lu[4 * i + j] = (i == piv) ? rk : lu[4 * i + j];
+            }
+            int pk = perm[k], pp = 0;
+#pragma unroll
+            for (int i = k + 1; i < 4; ++i) pp = (i == piv) ? perm[i] : pp;
+            perm[k] = pp;
+#pragma unroll
+            for (int i = k + 1; i < 4; ++i) perm[i] = (i == piv) ? pk : perm[i];
+        }
+        if (big != 0.0) {
+#pragma unroll
+            for (int i = k + 1; i < 4; ++i) lu[4 * i + k] /= lu[4 * k + k];
+#pragma unroll
+            for (int i = k + 1; i < 4; ++i)
+#pragma unroll
+                for (int j = k + 1; j < 4; ++j) lu[4 * i + j] -= lu[4 * i + k] * lu[4 * k + j];
+        }
+    }
+#pragma unroll
+    for (int col = 0; col < 4; ++col) {
+        double y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (perm[i] == col) ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) y[i] -= lu[4 * i + j] * y[j];
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+#pragma unroll
+            for (int j = i + 1; j < 4; ++j) y[i] -= lu[4 * i + j] * y[j];
+            y[i] /= lu[4 * i + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) R[4 * i + col] = y[i];
+    }
+}
+
+GGP_DEV void mm4(const double *A, const double *B, double *R)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double s = A[4 * i] * B[j];
+#pragma unroll
+            for (int k = 1; k < 4; ++k) s = s + A[4 * i + k] * B[4 * k + j];
+            R[4 * i + j] = s;
+        }
+}
+
+GGP_DEV void mv4(const double *A, const double *v, double *r)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double s = A[4 * i] * v[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) s = s + A[4 * i + k] * v[k];
+        r[i] = s;
+    }
+}
+
+// multiply_gaussian (predictions.h:183-188): in place on (m1, c1)
+GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
+{
+    double i1[16], i2[16], sum[16], nc[16], t1[16], t2[16], v1[4], v2[4];
+    inv4(c1, i1);
+    inv4(c2, i2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sum[k] = i1[k] + i2[k];
+    inv4(sum, nc);
+    mm4(nc, i1, t1);
+    mm4(nc, i2, t2);
+    mv4(t1, m1, v1);
+    mv4(t2, m2, v2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m1[k] = v1[k] + v2[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c1[k] = nc[k];
+}
+
+// divide_by_prior (predictions.h:446-463)
+GGP_DEV void divide_prior(double *m, double *c, const double *p)
+{
+    const double mp[4] = {0, 0, p[0], p[3]};
+    double ip[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ip[k] = 0.0;
+    ip[10] = (2. * p[1]) / p[2];
+    ip[15] = (2. * p[4]) / p[5];
+    double ic[16], d[16], nc[16], a[4], bv[4], r[4];
+    inv4(c, ic);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = ic[k] - ip[k];
+    inv4(d, nc);
+    mv4(ic, m, a);
+    mv4(ip, mp, bv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = a[k] - bv[k];
+    mv4(nc, r, m);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = nc[k];
+}
+
+// reverse_mean / reverse_cov (predictions.h:278-301)
+GGP_DEV void reverse_state(double *m, double *C)
+{
+    m[2] = -m[2]; m[3] = -m[3];
+    C[2] = -C[2]; C[8] = -C[8]; C[3] = -C[3]; C[12] = -C[12];
+    C[6] = -C[6]; C[9] = -C[9]; C[7] = -C[7]; C[13] = -C[13];
+}
+
+// the per-daughter map of mean_cov_after_division_r (predictions.h:214-237)
+GGP_DEV void division_map_r(double *m, double *C, const double var_dx, const double var_dg,
+                            const int binomial, const double log2)
+{
+    if (binomial) {
+        C[0] += var_dx;
+        C[5] = 8. * var_dx * (m[1] * m[1] + C[5]) + 2. * var_dg * m[1] + 8. * C[5];
+        C[1] = C[4] = 2. * m[1] * var_dx + 4. * C[1];
+        C[9] *= 2; C[6] *= 2; C[13] *= 2; C[7] *= 2;
+        m[0] += log2;
+        m[1] *= 2;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { C[4 + j] *= 2.0; C[4 * j + 1] *= 2.0; }
+        C[0] = var_dx + C[0];
+        C[5] = var_dg + C[5];
+        m[0] = m[0] + log2;
+        m[1] = 2.0 * m[1];
+    }
+}
+
+}  // namespace ggp

@@ -1,0 +1,501 @@
+// ggp_prop.h -- the propagation step mean_cov_model (mean_cov_model.h:211-274) as a set of
+// data-parallel TASKS over one step's shared scalars, so that two schedules can run it:
+//
+//   lane kernel  : one lane owns a cell; every task index is a compile-time constant
+//                  (unrolled), arrays live in registers;
+//   group kernel : G lanes own a cell; lane l runs tasks l, l+G, ...; arrays live in LDS.
+//
+// Both schedules execute the SAME expression for every value, so they are bitwise equal
+// (tests/test_gpu_parity.py).  Every expression keeps the reference's evaluation order;
+// the 59 tauint calls of one step dedupe to 45 distinct integrals over 74 distinct
+// exponentials and 14 Dawson values (identical inputs -> identical bits).
+//
+// Division: x/d for a denominator used several times per step is evaluated as
+// q = x*r, e = fma(-q,d,x), q' = fma(e,r,q) with r = 1/d correctly rounded (Markstein):
+// correctly rounded, i.e. bitwise equal to IEEE x/d for finite normal operands (checked on
+// 2e8 random pairs); 3 instructions instead of ~11.
+#pragma once
+#include <utility>
+
+#include "ggp_device.h"
+
+namespace ggp {
+
+GGP_DEV double rdiv(double x, double d, double r)
+{
+    const double q = x * r;
+    const double e = __builtin_fma(-q, d, x);
+    return __builtin_fma(e, r, q);
+}
+
+// ---- indices -------------------------------------------------------------------------
+// b values (tauint 2nd argument)            B1..B6  -> 0..5
+// c values (tauint 3rd argument)            cA cB cJ cG cC cD cE cF cI cH -> 0..9
+// time points                               0, t, 2t -> 0..2
+enum { cA = 0, cB, cJ, cG, cC, cD, cE, cF, cI, cH };
+enum { KX_C = 0, KX_A, KX_S, KX_E, KX_Z };      // exp kinds
+
+// exponential slots
+enum {
+    XC_A = 0, XC_B, XC_J, XC_G, XC_C, XC_D, XC_E, XC_F, XC_I,                 // exp(c)
+    XA_1t, XA_2t, XA_3t, XA_4t, XA_32, XA_42,                                  // exp(ti (B + a ti))
+    XS_bt, XS_bglt, XS_2bt, XS_bgqt, XS_gl, XS_gq,                             // exp(s t)
+    XE_2A0, XE_2At, XE_1A0, XE_1At, XE_1B0, XE_1Bt, XE_2B0, XE_2Bt, XE_1J0, XE_1Jt,
+    XE_2J0, XE_2Jt, XE_1G0, XE_1Gt, XE_2G0, XE_2Gt, XE_3C0, XE_3Ct, XE_3C2, XE_4C0,
+    XE_4Ct, XE_4C2, XE_3Dt, XE_3D2, XE_4E0, XE_4Et, XE_4E2, XE_4Ft, XE_4F2,    // exp(-B^2/4a + c + z^2)
+    XZ_1At, XZ_2At, XZ_1Bt, XZ_2Bt, XZ_1Jt, XZ_2Jt, XZ_2It, XZ_5It, XZ_1Gt, XZ_2Gt,
+    XZ_3Ct, XZ_4Ct, XZ_3Et, XZ_4Et, XZ_3E2, XZ_3C2, XZ_3Dt, XZ_3D2, XZ_4E2, XZ_4C2,
+    XZ_4Ft, XZ_4F2, XZ_6Ht, XZ_6H2,                                            // exp(a ti^2 + B ti + c)
+    X_ONE,                                                                     // 1.0 (t0 = 0)
+    NX
+};
+constexpr int NXT = X_ONE;   // 74 exponentials to compute
+
+struct XTask { unsigned char kind, iB, ic, it; };
+// kind, B (or s for KX_S), c, t
+constexpr XTask kXT[NXT] = {
+    {KX_C, 0, cA, 0}, {KX_C, 0, cB, 0}, {KX_C, 0, cJ, 0}, {KX_C, 0, cG, 0}, {KX_C, 0, cC, 0},
+    {KX_C, 0, cD, 0}, {KX_C, 0, cE, 0}, {KX_C, 0, cF, 0}, {KX_C, 0, cI, 0},
+    {KX_A, 0, 0, 1}, {KX_A, 1, 0, 1}, {KX_A, 2, 0, 1}, {KX_A, 3, 0, 1}, {KX_A, 2, 0, 2}, {KX_A, 3, 0, 2},
+    {KX_S, 0, 0, 0}, {KX_S, 1, 0, 0}, {KX_S, 2, 0, 0}, {KX_S, 3, 0, 0}, {KX_S, 4, 0, 0}, {KX_S, 5, 0, 0},
+    {KX_E, 1, cA, 0}, {KX_E, 1, cA, 1}, {KX_E, 0, cA, 0}, {KX_E, 0, cA, 1}, {KX_E, 0, cB, 0},
+    {KX_E, 0, cB, 1}, {KX_E, 1, cB, 0}, {KX_E, 1, cB, 1}, {KX_E, 0, cJ, 0}, {KX_E, 0, cJ, 1},
+    {KX_E, 1, cJ, 0}, {KX_E, 1, cJ, 1}, {KX_E, 0, cG, 0}, {KX_E, 0, cG, 1}, {KX_E, 1, cG, 0},
+    {KX_E, 1, cG, 1}, {KX_E, 2, cC, 0}, {KX_E, 2, cC, 1}, {KX_E, 2, cC, 2}, {KX_E, 3, cC, 0},
+    {KX_E, 3, cC, 1}, {KX_E, 3, cC, 2}, {KX_E, 2, cD, 1}, {KX_E, 2, cD, 2}, {KX_E, 3, cE, 0},
+    {KX_E, 3, cE, 1}, {KX_E, 3, cE, 2}, {KX_E, 3, cF, 1}, {KX_E, 3, cF, 2},
+    {KX_Z, 0, cA, 1}, {KX_Z, 1, cA, 1}, {KX_Z, 0, cB, 1}, {KX_Z, 1, cB, 1}, {KX_Z, 0, cJ, 1},
+    {KX_Z, 1, cJ, 1}, {KX_Z, 1, cI, 1}, {KX_Z, 4, cI, 1}, {KX_Z, 0, cG, 1}, {KX_Z, 1, cG, 1},
+    {KX_Z, 2, cC, 1}, {KX_Z, 3, cC, 1}, {KX_Z, 2, cE, 1}, {KX_Z, 3, cE, 1}, {KX_Z, 2, cE, 2},
+    {KX_Z, 2, cC, 2}, {KX_Z, 2, cD, 1}, {KX_Z, 2, cD, 2}, {KX_Z, 3, cE, 2}, {KX_Z, 3, cC, 2},
+    {KX_Z, 3, cF, 1}, {KX_Z, 3, cF, 2}, {KX_Z, 5, cH, 1}, {KX_Z, 5, cH, 2},
+};
+
+// Dawson slots D(B, t_i)
+enum { D_1_0 = 0, D_1_t, D_2_0, D_2_t, D_3_0, D_3_t, D_3_2, D_4_0, D_4_t, D_4_2, D_5_0, D_5_t,
+       D_6_t, D_6_2, ND };
+struct DTask { unsigned char iB, it; };
+constexpr DTask kDT[ND] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {2, 0}, {2, 1}, {2, 2},
+                           {3, 0}, {3, 1}, {3, 2}, {4, 0}, {4, 1}, {5, 1}, {5, 2}};
+
+// tauint slots (k = 1 first, then k = 0, 2, 3)
+enum {
+    O_2A = 0, O_1A, O_1B, O_2B, O_1J, O_2J, O_1G, O_2G, O_3C, O_4C, O_3C2, O_3D2, O_4E, O_4E2,
+    O_4C2, O_4F2,
+    Z_1A, Z_2A, Z_1B, Z_2B, Z_1J, Z_2J, Z_2I, Z_5I, Z_1G, Z_2G, Z_3C, Z_4C, Z_3E, Z_4E, Z_3E2,
+    Z_3C2, Z_3D2, Z_4E2, Z_4C2, Z_4F2, Z_6H2,
+    T_2A, T_2B, T_2J, T_2G, T_4C, T_4C2,
+    H_4C, H_4C2,
+    NI
+};
+struct ITask { unsigned char k, iB, it0, it1, xc, x0, x1, xa0, xa1, d0, d1; };
+constexpr ITask kIT[NI] = {
+    // k = 1: ec, E0, E1, ea0, ea1, D0, D1
+    {1, 1, 0, 1, XC_A, XE_2A0, XE_2At, X_ONE, XA_2t, D_2_0, D_2_t},
+    {1, 0, 0, 1, XC_A, XE_1A0, XE_1At, X_ONE, XA_1t, D_1_0, D_1_t},
+    {1, 0, 0, 1, XC_B, XE_1B0, XE_1Bt, X_ONE, XA_1t, D_1_0, D_1_t},
+    {1, 1, 0, 1, XC_B, XE_2B0, XE_2Bt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {1, 0, 0, 1, XC_J, XE_1J0, XE_1Jt, X_ONE, XA_1t, D_1_0, D_1_t},
+    {1, 1, 0, 1, XC_J, XE_2J0, XE_2Jt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {1, 0, 0, 1, XC_G, XE_1G0, XE_1Gt, X_ONE, XA_1t, D_1_0, D_1_t},
+    {1, 1, 0, 1, XC_G, XE_2G0, XE_2Gt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {1, 2, 0, 1, XC_C, XE_3C0, XE_3Ct, X_ONE, XA_3t, D_3_0, D_3_t},
+    {1, 3, 0, 1, XC_C, XE_4C0, XE_4Ct, X_ONE, XA_4t, D_4_0, D_4_t},
+    {1, 2, 1, 2, XC_C, XE_3Ct, XE_3C2, XA_3t, XA_32, D_3_t, D_3_2},
+    {1, 2, 1, 2, XC_D, XE_3Dt, XE_3D2, XA_3t, XA_32, D_3_t, D_3_2},
+    {1, 3, 0, 1, XC_E, XE_4E0, XE_4Et, X_ONE, XA_4t, D_4_0, D_4_t},
+    {1, 3, 1, 2, XC_E, XE_4Et, XE_4E2, XA_4t, XA_42, D_4_t, D_4_2},
+    {1, 3, 1, 2, XC_C, XE_4Ct, XE_4C2, XA_4t, XA_42, D_4_t, D_4_2},
+    {1, 3, 1, 2, XC_F, XE_4Ft, XE_4F2, XA_4t, XA_42, D_4_t, D_4_2},
+    // k = 0: Z0 (lower limit, = exp(c) at t0 = 0), Z1, D0, D1
+    {0, 0, 0, 1, 0, XC_A, XZ_1At, 0, 0, D_1_0, D_1_t},
+    {0, 1, 0, 1, 0, XC_A, XZ_2At, 0, 0, D_2_0, D_2_t},
+    {0, 0, 0, 1, 0, XC_B, XZ_1Bt, 0, 0, D_1_0, D_1_t},
+    {0, 1, 0, 1, 0, XC_B, XZ_2Bt, 0, 0, D_2_0, D_2_t},
+    {0, 0, 0, 1, 0, XC_J, XZ_1Jt, 0, 0, D_1_0, D_1_t},
+    {0, 1, 0, 1, 0, XC_J, XZ_2Jt, 0, 0, D_2_0, D_2_t},
+    {0, 1, 0, 1, 0, XC_I, XZ_2It, 0, 0, D_2_0, D_2_t},
+    {0, 4, 0, 1, 0, XC_I, XZ_5It, 0, 0, D_5_0, D_5_t},
+    {0, 0, 0, 1, 0, XC_G, XZ_1Gt, 0, 0, D_1_0, D_1_t},
+    {0, 1, 0, 1, 0, XC_G, XZ_2Gt, 0, 0, D_2_0, D_2_t},
+    {0, 2, 0, 1, 0, XC_C, XZ_3Ct, 0, 0, D_3_0, D_3_t},
+    {0, 3, 0, 1, 0, XC_C, XZ_4Ct, 0, 0, D_4_0, D_4_t},
+    {0, 2, 0, 1, 0, XC_E, XZ_3Et, 0, 0, D_3_0, D_3_t},
+    {0, 3, 0, 1, 0, XC_E, XZ_4Et, 0, 0, D_4_0, D_4_t},
+    {0, 2, 1, 2, 0, XZ_3Et, XZ_3E2, 0, 0, D_3_t, D_3_2},
+    {0, 2, 1, 2, 0, XZ_3Ct, XZ_3C2, 0, 0, D_3_t, D_3_2},
+    {0, 2, 1, 2, 0, XZ_3Dt, XZ_3D2, 0, 0, D_3_t, D_3_2},
+    {0, 3, 1, 2, 0, XZ_4Et, XZ_4E2, 0, 0, D_4_t, D_4_2},
+    {0, 3, 1, 2, 0, XZ_4Ct, XZ_4C2, 0, 0, D_4_t, D_4_2},
+    {0, 3, 1, 2, 0, XZ_4Ft, XZ_4F2, 0, 0, D_4_t, D_4_2},
+    {0, 5, 1, 2, 0, XZ_6Ht, XZ_6H2, 0, 0, D_6_t, D_6_2},
+    // k = 2
+    {2, 1, 0, 1, XC_A, XE_2A0, XE_2At, X_ONE, XA_2t, D_2_0, D_2_t},
+    {2, 1, 0, 1, XC_B, XE_2B0, XE_2Bt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {2, 1, 0, 1, XC_J, XE_2J0, XE_2Jt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {2, 1, 0, 1, XC_G, XE_2G0, XE_2Gt, X_ONE, XA_2t, D_2_0, D_2_t},
+    {2, 3, 0, 1, XC_C, XE_4C0, XE_4Ct, X_ONE, XA_4t, D_4_0, D_4_t},
+    {2, 3, 1, 2, XC_C, XE_4Ct, XE_4C2, XA_4t, XA_42, D_4_t, D_4_2},
+    // k = 3
+    {3, 3, 0, 1, XC_C, XE_4C0, XE_4Ct, X_ONE, XA_4t, D_4_0, D_4_t},
+    {3, 3, 1, 2, XC_C, XE_4Ct, XE_4C2, XA_4t, XA_42, D_4_t, D_4_2},
+};
+
+// ---- per-step scalars ------------------------------------------------------------------
+struct Step {
+    // z(t0) state (mean_cov_model.h:221-235) and OU parameters (already sign-flipped for _r)
+    double bx, bg, bl, bq, Cxx, Cxg, Cxl, Cxq, Cgg, Cgl, Cgq, Cll, Clq, Cqq;
+    double ml, gl, sl2, mq, gq, sq2, b, t, t2;
+    // derived
+    double a, two_sa, m2sa, two_a, four_a, four_aa;
+    double B0, B1, B2, B3, B4, B5;                     // B1..B6
+    double c0, c1, c2, c3, c4, c5, c6, c7, c8, c9;     // cA cB cJ cG cC cD cE cF cI cH
+    double r_two_sa, r_four_a, r_gl, r_gq;
+};
+
+GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t, const double ml,
+                       const double gl, const double sl2, const double mq, const double gq,
+                       const double sq2, const double b)
+{
+    S.bx = m[0]; S.bg = m[1]; S.bl = m[2]; S.bq = m[3];
+    S.Cxx = C[0]; S.Cxg = C[1]; S.Cxl = C[2]; S.Cxq = C[3];
+    S.Cgg = C[5]; S.Cgl = C[6]; S.Cgq = C[7];
+    S.Cll = C[10]; S.Clq = C[11]; S.Cqq = C[15];
+    S.ml = ml; S.gl = gl; S.sl2 = sl2; S.mq = mq; S.gq = gq; S.sq2 = sq2; S.b = b;
+    S.t = t;
+    S.t2 = 2 * t;
+    const double a = S.Cll / 2.;
+    const double sa = sqrt(a);
+    S.a = a;
+    S.two_sa = 2. * sa;
+    S.m2sa = -2. * sa;
+    S.two_a = 2. * a;
+    S.four_a = 4. * a;
+    S.four_aa = 4 * (a * a);
+    const double bx = S.bx, Cxx = S.Cxx, bl = S.bl, Cxl = S.Cxl;
+    S.B0 = b + bl + Cxl;
+    S.B1 = b + bl + Cxl - gq;
+    S.B2 = b + bl + 2 * Cxl;
+    S.B3 = b + bl + 2 * Cxl - gq;
+    S.B4 = b + bl + Cxl + gq;
+    S.B5 = b + bl + 2 * Cxl + gq;
+    S.c0 = bx + Cxx / 2. - b * t;                  // cA
+    S.c1 = bx + Cxx / 2. - b * t - gl * t;         // cB
+    S.c2 = bx + Cxx / 2. - b * t - gq * t;         // cJ
+    S.c3 = bx + Cxx / 2. - 2 * b * t;              // cG
+    S.c4 = 2 * (bx + Cxx - b * t);                 // cC
+    S.c5 = 2 * bx + 2 * Cxx - (2 * b + gq) * t;    // cD
+    S.c6 = 2 * bx + 2 * Cxx - 2 * b * t;           // cE
+    S.c7 = 2 * bx + 2 * Cxx - 2 * b * t + gq * t;  // cF
+    S.c8 = -b * t + bx + Cxx / 2. - gq * t;        // cI
+    S.c9 = 2 * bx + 2 * Cxx - 2 * b * t - 2 * gq * t;  // cH
+    S.r_two_sa = 1.0 / S.two_sa;
+    S.r_four_a = 1.0 / S.four_a;
+    S.r_gl = 1.0 / gl;
+    S.r_gq = 1.0 / gq;
+}
+
+// select without dynamic register indexing (compile-time index folds to one operand)
+GGP_DEV double pickB(const Step &S, int i)
+{
+    return i == 0 ? S.B0 : i == 1 ? S.B1 : i == 2 ? S.B2 : i == 3 ? S.B3 : i == 4 ? S.B4 : S.B5;
+}
+GGP_DEV double pickC(const Step &S, int i)
+{
+    return i == 0 ? S.c0 : i == 1 ? S.c1 : i == 2 ? S.c2 : i == 3 ? S.c3 : i == 4 ? S.c4
+         : i == 5 ? S.c5 : i == 6 ? S.c6 : i == 7 ? S.c7 : i == 8 ? S.c8 : S.c9;
+}
+GGP_DEV double pickT(const Step &S, int i) { return i == 0 ? 0.0 : i == 1 ? S.t : S.t2; }
+
+// z = (B + 2a t_i) / (2 sqrt a)  (t_i = 0: B / (2 sqrt a))
+GGP_DEV double zval(const Step &S, int iB, int it)
+{
+    const double B = pickB(S, iB);
+    const double num = it == 0 ? B : B + S.two_a * pickT(S, it);
+    return rdiv(num, S.two_sa, S.r_two_sa);
+}
+
+GGP_DEV double exp_body(const Step &S, const XTask T)
+{
+    // branch-free: every candidate argument is formed from selected operands and the kind
+    // picks one, so lanes holding different kinds do not serialise (group schedule)
+    const double ti = pickT(S, T.it);
+    const double B = pickB(S, T.iB);
+    const double c = pickC(S, T.ic);
+    const int s = T.iB;
+    const double sv = s == 0 ? S.b : s == 1 ? S.b + S.gl : s == 2 ? 2 * S.b : s == 3 ? S.b + S.gq
+                    : s == 4 ? -S.gl : -S.gq;
+    const double n = rdiv(-(B * B), S.four_a, S.r_four_a);
+    const double zn = T.it == 0 ? B : B + S.two_a * ti;
+    const double z = rdiv(zn, S.two_sa, S.r_two_sa);
+    const double argA = ti * (B + S.a * ti);
+    const double argS = sv * S.t;
+    const double argE = n + c + z * z;
+    const double argZ = S.a * (ti * ti) + B * ti + c;
+    const double arg = T.kind == KX_C ? c : T.kind == KX_A ? argA : T.kind == KX_S ? argS
+                     : T.kind == KX_E ? argE : argZ;
+    return exp(arg);
+}
+
+GGP_DEV double exp_task(const Step &S, int j) { return exp_body(S, kXT[j]); }
+
+GGP_DEV double dawson_task(const Step &S, int d, const double *tab)
+{
+    const DTask T = kDT[d];
+    return ggp_dawson_tab(zval(S, T.iB, T.it), tab);
+}
+
+// the three tauint denominators 4 a^1.5, 8 a^2.5, 16 a^3.5.  pow(a, k + 1/2) is formed as
+// a^k * sqrt(a) (sqrt correctly rounded, <= 2 ulp from glibc's pow; the total
+// log-likelihood moves by ~1e-11 relative, DESIGN.md "Parity") -- ~10x cheaper than ocml pow.
+GGP_DEV double pow_task(const Step &S, int p)
+{
+    const double sa = S.two_sa * 0.5;           // sqrt(a), exact
+    const double a = S.a;
+    return p == 0 ? 4. * (a * sa) : p == 1 ? 8. * ((a * a) * sa) : 16. * (((a * a) * a) * sa);
+}
+constexpr int NPW = 6;   // 3 denominators + 3 reciprocals
+
+// ---- tauint from its pieces (mean_cov_model.h:9-67) ----------------------------------
+// PW = {4 a^1.5, 8 a^2.5, 16 a^3.5, and their reciprocals}
+template <class XA, class DA, class PA>
+GGP_DEV double tau_body(const Step &S, const ITask T, const XA &X, const DA &Dw, const PA &PW)
+{
+    const double D0 = Dw[T.d0], D1 = Dw[T.d1];
+    if (T.k == 0) {   // zerotauint
+        const double Z0 = X[T.x0], Z1 = X[T.x1];
+        const double x = 2. * (-Z0 * D0 + Z1 * (D1));
+        return rdiv(x, S.two_sa, S.r_two_sa);
+    }
+    const double B = pickB(S, T.iB);
+    const double ec = X[T.xc], E0 = X[T.x0], E1 = X[T.x1], ea0 = X[T.xa0], ea1 = X[T.xa1];
+    if (T.k == 1) {   // onetauint
+        const double x = (S.m2sa * ec * (ea0 - ea1) + B * 2. * (E0 * D0 - E1 * D1));
+        return rdiv(x, PW[0], PW[3]);
+    }
+    const double t0 = pickT(S, T.it0), t1 = pickT(S, T.it1);
+    if (T.k == 2) {   // twotauint
+        const double x = (S.two_sa * ec * (ea0 * (B - S.two_a * t0) - ea1 * (B - S.two_a * t1))
+                          + (E0 * (S.two_a - B * B) * 2. * D0 + E1 * (-S.two_a + B * B) * 2. * D1));
+        return rdiv(x, PW[1], PW[4]);
+    }
+    // treetauint
+    const double a = S.a;
+    const double x = (S.m2sa * ec
+                      * ((B * B) * (ea0 - ea1) - S.two_a * ea0 * (2. + B * t0) + S.two_a * ea1 * (2 + B * t1)
+                         + S.four_aa * (ea0 * (t0 * t0) - ea1 * (t1 * t1))))
+                     + E0 * B * (-6. * a + B * B) * 2. * D0
+                     - E1 * B * (-6 * a + B * B) * 2. * D1;
+    return rdiv(x, PW[2], PW[5]);
+}
+
+template <class XA, class DA, class PA>
+GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const PA &PW)
+{
+    return tau_body(S, kIT[j], X, Dw, PW);
+}
+
+// ---- the outputs: new mean and covariance (mean_cov_model.h:73-208) -------------------
+template <class IA, class XA>
+GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
+{
+    const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
+    const double Cxx = S.Cxx, Cxg = S.Cxg, Cxl = S.Cxl, Cxq = S.Cxq, Cgg = S.Cgg, Cgl = S.Cgl;
+    const double Cgq = S.Cgq, Cll = S.Cll, Clq = S.Clq, Cqq = S.Cqq;
+    const double ml = S.ml, gl = S.gl, sl2 = S.sl2, mq = S.mq, gq = S.gq, sq2 = S.sq2;
+    const double rgl = S.r_gl, rgq = S.r_gq;
+    const double ebt = X[XS_bt], ebglt = X[XS_bglt], e2bt = X[XS_2bt], ebgqt = X[XS_bgqt];
+    const double egl = X[XS_gl], egq = X[XS_gq];
+    const double r_ebt = 1.0 / ebt, r_ebglt = 1.0 / ebglt, r_ebgqt = 1.0 / ebgqt;
+    const double ebt_gl = ebt * gl, ebglt_gl = ebglt * gl;
+    const double r_ebt_gl = 1.0 / ebt_gl, r_ebglt_gl = 1.0 / ebglt_gl;
+    const double gq2 = 2. * gq, gqq2 = 2. * (gq * gq);
+    const double r_gq2 = 1.0 / gq2, r_gqq2 = 1.0 / gqq2;
+#define DGL(x) rdiv((x), gl, rgl)
+#define DGQ(x) rdiv((x), gq, rgq)
+
+    double nm[4];
+    nm[0] = bx + ml * t + DGL((bl - ml) * (1 - egl));
+    nm[1] = rdiv(bg, ebt, r_ebt) + Clq * I[O_2A] + mq * I[Z_1A] + (bq + Cxq - mq) * I[Z_2A];
+    nm[2] = ml + (bl - ml) * egl;
+    nm[3] = mq + (bq - mq) * egq;
+
+    // cov_xg (mean_cov_model.h:97-115)
+    const double nxg =
+        rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + rdiv(bg * bl, ebt_gl, r_ebt_gl)
+        + rdiv(Cgl, ebt_gl, r_ebt_gl) - rdiv(bg * bl, ebglt_gl, r_ebglt_gl) - rdiv(Cgl, ebglt_gl, r_ebglt_gl)
+        - rdiv(bg * ml, ebt_gl, r_ebt_gl) + rdiv(bg * ml, ebglt_gl, r_ebglt_gl) + rdiv(bg * ml * t, ebt, r_ebt)
+        + (Cxl * mq + DGL(Cll * mq)) * I[O_1A]
+        - DGL(Cll * mq * I[O_1B])
+        + (bx * Clq + bq * Cxl + Cxl * Cxq + Clq * Cxx + DGL(bq * Cll) + DGL(bl * Clq) + DGL(Clq * Cxl)
+           + DGL(Cll * Cxq) - DGL(Clq * ml) - Cxl * mq - DGL(Cll * mq) + Clq * ml * t) * I[O_2A]
+        + (-(DGL(bq * Cll)) - DGL(bl * Clq) - DGL(Clq * Cxl) - DGL(Cll * Cxq) + DGL(Clq * ml)
+           + DGL(Cll * mq)) * I[O_2B]
+        + (Clq * Cxl + DGL(Cll * Clq)) * I[T_2A]
+        - DGL(Cll * Clq * I[T_2B])
+        + (bx * mq + Cxx * mq + DGL(bl * mq) + DGL(Cxl * mq) - DGL(ml * mq) + ml * mq * t) * I[Z_1A]
+        + (-(DGL(bl * mq)) - DGL(Cxl * mq) + DGL(ml * mq)) * I[Z_1B]
+        + (bq * bx + Cxq + bx * Cxq + bq * Cxx + Cxq * Cxx + DGL(bl * bq) + DGL(Clq) + DGL(bq * Cxl)
+           + DGL(bl * Cxq) + DGL(Cxl * Cxq) - DGL(bq * ml) - DGL(Cxq * ml) - bx * mq - Cxx * mq
+           - DGL(bl * mq) - DGL(Cxl * mq) + DGL(ml * mq) + bq * ml * t + Cxq * ml * t - ml * mq * t) * I[Z_2A]
+        + (-(DGL(bl * bq)) - DGL(Clq) - DGL(bq * Cxl) - DGL(bl * Cxq) - DGL(Cxl * Cxq) + DGL(bq * ml)
+           + DGL(Cxq * ml) + DGL(bl * mq) + DGL(Cxl * mq) - DGL(ml * mq)) * I[Z_2B]
+        - nm[1] * nm[0];
+
+    // cov_xl, cov_xq (mean_cov_model.h:117-123)
+    const double nxl = sl2 / (2 * (gl * gl)) * ((1 - egl) * (1 - egl))
+                       + DGL(Cll * egl * (1 - egl)) + Cxl * egl;
+    const double nxq = DGL(Clq * (1 - egl) * egq) + Cxq * egq;
+
+    // cov_gl (mean_cov_model.h:172-181)
+    const double ngl =
+        rdiv(bg * bl, ebglt, r_ebglt) + rdiv(Cgl, ebglt, r_ebglt) + rdiv(bg * ml, ebt, r_ebt)
+        - rdiv(bg * ml, ebglt, r_ebglt)
+        + Cll * mq * I[O_1B] + Clq * ml * I[O_2A]
+        + (bq * Cll + bl * Clq + Clq * Cxl + Cll * Cxq - Clq * ml - Cll * mq) * I[O_2B]
+        + Cll * Clq * I[T_2B] + ml * mq * I[Z_1A]
+        + (bl * mq + Cxl * mq - ml * mq) * I[Z_1B]
+        + (bq * ml + Cxq * ml - ml * mq) * I[Z_2A]
+        + (bl * bq + Clq + bq * Cxl + bl * Cxq + Cxl * Cxq - bq * ml - Cxq * ml - bl * mq - Cxl * mq
+           + ml * mq) * I[Z_2B]
+        - nm[1] * nm[2];
+
+    // cov_gq (mean_cov_model.h:183-196)
+    const double ngq =
+        rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)
+        - rdiv(bg * mq, ebgqt, r_ebgqt)
+        + Clq * mq * I[O_1J] + Clq * mq * I[O_2A]
+        + (2 * bq * Clq + 2 * Clq * Cxq - 2 * Clq * mq) * I[O_2J]
+        + (Clq * Clq) * I[T_2J] + (mq * mq) * I[Z_1A]
+        + (bq * mq + Cxq * mq - (mq * mq)) * I[Z_1J]
+        + (bq * mq + Cxq * mq - (mq * mq)) * I[Z_2A]
+        - rdiv(sq2 * I[Z_2I], gq2, r_gq2)
+        + ((bq * bq) + Cqq + 2 * bq * Cxq + (Cxq * Cxq) - 2 * bq * mq - 2 * Cxq * mq + (mq * mq)) * I[Z_2J]
+        + rdiv(sq2 * I[Z_5I], gq2, r_gq2)
+        - nm[1] * nm[3];
+
+    // cov_gg (mean_cov_model.h:125-170)
+    const double k17 = DGQ(2 * bq * mq) + DGQ(4 * Cxq * mq) - DGQ(2 * (mq * mq));
+    const double k19 = DGQ(-2 * bq * mq) - DGQ(4 * Cxq * mq) + DGQ(2 * (mq * mq));
+    const double ngg =
+        ((bg * bg) + Cgg) / e2bt
+        + 2 * Cgl * mq * I[O_1G]
+        + DGQ(mq * (2 * Clq + gq * mq) * I[O_3C])
+        + 2 * (bq * Cgl + bg * Clq + Clq * Cxg + Cgl * Cxq - Cgl * mq) * I[O_2G]
+        + DGQ(((bq * bq) * gq + Cqq * gq + 4 * bq * Cxq * gq + 4 * (Cxq * Cxq) * gq - 2 * Clq * mq
+               - 2 * bq * gq * mq - 4 * Cxq * gq * mq + gq * (mq * mq)) * I[O_4C])
+        - (mq * mq) * I[O_3C2]
+        - DGQ(2 * Clq * mq * I[O_3D2])
+        - rdiv(sq2 * I[O_4E], gq2, r_gq2)
+        + rdiv(sq2 * I[O_4E2], gq2, r_gq2)
+        + (-(bq * bq) - Cqq - 4 * bq * Cxq - 4 * (Cxq * Cxq) + 2 * bq * mq + 4 * Cxq * mq - (mq * mq)
+           + 4 * bq * Clq * t + 8 * Clq * Cxq * t - 4 * Clq * mq * t) * I[O_4C2]
+        + DGQ(2 * Clq * mq * I[O_4F2])
+        + (Clq * Clq) * I[H_4C]
+        - (Clq * Clq) * I[H_4C2]
+        + 2 * Cgl * Clq * I[T_2G]
+        + (2 * bq * Clq + 4 * Clq * Cxq - 2 * Clq * mq) * I[T_4C]
+        + (-2 * bq * Clq - 4 * Clq * Cxq + 2 * Clq * mq + 2 * (Clq * Clq) * t) * I[T_4C2]
+        + (2 * bg * mq + 2 * Cxg * mq) * I[Z_1G]
+        + k17 * I[Z_3C]
+        + (2 * bg * bq + 2 * Cgq + 2 * bq * Cxg + 2 * bg * Cxq + 2 * Cxg * Cxq - 2 * bg * mq
+           - 2 * Cxg * mq) * I[Z_2G]
+        + k19 * I[Z_4C]
+        + rdiv(sq2 * I[Z_3E], gqq2, r_gqq2)
+        + rdiv(sq2 * I[Z_3E2], gqq2, r_gqq2)
+        + 2 * (mq * mq) * t * I[Z_3C2]
+        + k19 * I[Z_3D2]
+        - rdiv(sq2 * I[Z_4E], gqq2, r_gqq2)
+        - DGQ(sq2 * t * I[Z_4E2])
+        + (2 * (bq * bq) * t + 2 * Cqq * t + 8 * bq * Cxq * t + 8 * (Cxq * Cxq) * t - 4 * bq * mq * t
+           - 8 * Cxq * mq * t + 2 * (mq * mq) * t) * I[Z_4C2]
+        + k17 * I[Z_4F2]
+        - rdiv(sq2 * I[Z_6H2], gqq2, r_gqq2)
+        - (nm[1] * nm[1]);
+
+    // cov_xx, cov_ll, cov_lq, cov_qq (mean_cov_model.h:93-95, 198-208)
+    const double nxx = Cll * ((1 - egl) * (1 - egl)) / (gl * gl) + rdiv(2 * Cxl * (1 - egl), gl, rgl) + Cxx
+                       + sl2 / (2 * pow(gl, 3)) * (2 * gl * t - 3 + 4 * egl - (egl * egl));
+    const double nll = Cll * (egl * egl) + sl2 / (2 * gl) * (1 - (egl * egl));
+    const double nlq = Clq * egl * egq;
+    const double nqq = rdiv(sq2, 2 * gq, r_gq2) * (1 - (egq * egq)) + Cqq * (egq * egq);
+
+#undef DGL
+#undef DGQ
+    m[0] = nm[0]; m[1] = nm[1]; m[2] = nm[2]; m[3] = nm[3];
+    C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
+    C[4] = nxg;  C[5] = ngg;  C[6] = ngl;  C[7] = ngq;
+    C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[11] = nlq;
+    C[12] = nxq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
+}
+
+// ---- lane schedule: one lane runs every task of its own cell; the task descriptors are
+// constexpr template arguments, so every array index is a compile-time constant and the
+// arrays stay in registers.
+template <size_t... J>
+GGP_DEV void lane_exps(const Step &S, double *X, std::index_sequence<J...>)
+{
+    ((X[J] = exp_body(S, XTask{kXT[J].kind, kXT[J].iB, kXT[J].ic, kXT[J].it})), ...);
+}
+template <size_t... J>
+GGP_DEV void lane_dawsons(const Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
+{
+    ((Dw[J] = ggp_dawson_tab(zval(S, kDT[J].iB, kDT[J].it), tab)), ...);
+}
+template <int J, class XA, class DA, class PA>
+GGP_DEV double lane_tau(const Step &S, const XA &X, const DA &Dw, const PA &PW)
+{
+    constexpr ITask T = kIT[J];
+    return tau_body(S, T, X, Dw, PW);
+}
+template <class XA, class DA, class PA, size_t... J>
+GGP_DEV void lane_taus(const Step &S, const XA &X, const DA &Dw, const PA &PW, double *I,
+                       std::index_sequence<J...>)
+{
+    ((I[J] = lane_tau<(int)J>(S, X, Dw, PW)), ...);
+}
+
+// ---- lane schedule: one lane runs every task of its own cell
+GGP_DEV void propagate_lane(double *m, double *C, const double t, const double ml, const double gl,
+                            const double sl2, const double mq, const double gq, const double sq2,
+                            const double b, const double *tab)
+{
+    Step S;
+    step_init(S, m, C, t, ml, gl, sl2, mq, gq, sq2, b);
+    double X[NX];
+    lane_exps(S, X, std::make_index_sequence<NXT>{});
+    X[X_ONE] = 1.0;
+    double Dw[ND];
+    lane_dawsons(S, Dw, tab, std::make_index_sequence<ND>{});
+    double PW[NPW];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        PW[p] = pow_task(S, p);
+        PW[3 + p] = 1.0 / PW[p];
+    }
+    double I[NI];
+    lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
+    outputs(S, I, X, m, C);
+}
+
+// division map of mean_cov_after_division (predictions.h:40-60), after the propagation
+GGP_DEV void division_map(double *m, double *C, const double var_dx, const double var_dg,
+                          const int binomial, const double log2)
+{
+    if (binomial) {
+        C[0] += var_dx;
+        C[1] = C[4] = m[1] / 2. * var_dx + C[1];
+        C[5] = var_dx * (m[1] * m[1] + C[5]) / 2. + var_dg * m[1] / 4. * (1 - var_dx) + C[5] / 4.;
+        C[9] /= 2; C[6] /= 2;
+        C[13] /= 2; C[7] /= 2;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { C[4 + j] *= 0.5; C[4 * j + 1] *= 0.5; }
+        C[0] = var_dx + C[0];
+        C[5] = var_dg + C[5];
+    }
+    m[0] = m[0] + -log2;
+    m[1] = 0.5 * m[1];
+}
+
+}  // namespace ggp

@@ -212,3 +212,83 @@ def test_baseline_size_properties():
             h.a[k] = c3.a[k]
     s = g.Forest(lo).total_likelihood(P) + g.Forest(hi).total_likelihood(P)
     assert _rel(s, v) < 1e-12
+
+
+@pytest.mark.parametrize("which", ["example", "synthetic", "ragged"])
+def test_lane_and_group_schedules_bitwise_equal(example_forests, which):
+    """the two schedules run the same task expressions (csrc/ggp_prop.h): identical bits"""
+    import gfp_gaussian_process_amd as g
+    hf = {"example": lambda: example_forests[("scaled", "binomial")],
+          "synthetic": lambda: g.HostForest.synthetic(300, 40),
+          "ragged": _ragged_roots}[which]()
+    P = CONFIGS[0][2]
+    lane, group = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel="group")
+    for _ in range(3):
+        assert lane.total_likelihood(P) == group.total_likelihood(P)
+    assert np.array_equal(lane.state(), group.state())
+
+
+# ------------------------------------------------------------------------------------------
+# -p smoother (predictions.h:93-499) against the oracle's ora_predict
+# ------------------------------------------------------------------------------------------
+# Tolerance: means relative to (|m| + sd), covariances relative to sqrt(Cii Cjj).  The
+# smoother inherits the latent-q sensitivity of the propagator (+-1 ulp on every exp moves
+# the normalised state by ~4e-7, see test_example_state_matches_oracle) and adds five 4x4
+# inverses per row; 1e-5 leaves an order of magnitude of margin.
+PRED_TOL = 1e-5
+
+
+def _smoother_err(a, b):
+    m_a, m_b = a[:, :4], b[:, :4]
+    C_a, C_b = a[:, 4:].reshape(-1, 4, 4), b[:, 4:].reshape(-1, 4, 4)
+    sd = np.sqrt(np.abs(np.einsum("nii->ni", C_b)))
+    em = np.max(np.abs(m_a - m_b) / (np.abs(m_b) + sd).clip(1e-300))
+    ec = np.max(np.abs(C_a - C_b) / (sd[:, :, None] * sd[:, None, :]).clip(1e-300))
+    return float(em), float(ec)
+
+
+def _check_predict(hf, params):
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    got = g.Forest(hf).predict(params)
+    ref = O.OracleForest(hf.a).predict(params)
+    for name, x, y in zip(("forward", "backward", "combined"), got, ref):
+        assert np.all(np.isfinite(y)), name
+        assert np.all(np.isfinite(x)), name
+        em, ec = _smoother_err(x, y)
+        assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
+
+
+@pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
+def test_predict_example_vs_oracle(example_forests, noise, div):
+    params = next(p for n, d, p in CONFIGS if (n, d) == (noise, div))
+    _check_predict(example_forests[(noise, div)], params)
+
+
+def test_predict_segments_vs_oracle():
+    """two parameter segments switching along time (get_segment_indices, main.cpp:120-151)"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(40, 40)
+    t = hf.a["time"]
+    hf.a["segment"] = (t >= np.median(t)).astype(np.int32)
+    P0 = np.array(CONFIGS[0][2])
+    P1 = P0.copy()
+    P1[0] *= 1.1
+    P1[3] *= 0.95
+    P1[7] *= 1.2
+    _check_predict(hf, np.stack([P0, P1]))
+
+
+def test_predict_ragged_and_single_rows():
+    _check_predict(_ragged_roots(), CONFIGS[0][2])
+
+
+def test_predict_leaves_carried_state_alone(example_forests):
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P = CONFIGS[0][2]
+    a, b = g.Forest(hf), g.Forest(hf)
+    a.total_likelihood(P)
+    b.total_likelihood(P)
+    a.predict(P)
+    assert a.total_likelihood(P) == b.total_likelihood(P)
