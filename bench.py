@@ -10,8 +10,8 @@ partial (RCCL over xGMI).  Weak scaling: rank r evaluates trees [r*T, (r+1)*T).
 
   python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group]
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (k_loglik_level),
-timed with HIP events on the engine's own stream; `cpu_baseline` is the CPU oracle
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the one with the
+largest share of the evaluation), timed with HIP events on the engine's own stream; `cpu_baseline` is the CPU oracle
 (oracle/, a single-threaded C port of the reference path) timed on this host.
 """
 from __future__ import annotations
@@ -30,6 +30,16 @@ BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
              3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
 SEED = 20261015
+
+
+def traffic_for(kernel: str, args):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/traffic.json,
+    tools/pmc_traffic.py) when they were taken on this same default workload; else None"""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if args.trees != 1000 or args.rows != 200 or not os.path.exists(path):
+        return None
+    k = json.load(open(path)).get("kernels", {}).get(kernel)
+    return None if k is None else k["bytes_per_launch"]
 
 
 def cpu_baseline(hf, budget_s: float):
@@ -59,6 +69,8 @@ def main() -> int:
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--large-trees", type=int, default=12500,
+                    help="also time a C4-shard-sized forest (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -105,17 +117,41 @@ def main() -> int:
 
     # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
     fg.enable_profile()
-    ms_tot, rows_tot, n_launch = 0.0, 0, 0
+    per = {}                                   # kernel name -> [ms, rows, launches]
     for _ in range(max(3, min(args.steps, 10))):
         fg.total_likelihood(P_EXAMPLE)
-        ms, rows = fg.launch_profile()
-        ms_tot += sum(ms)
-        rows_tot += sum(rows)
-        n_launch += len(ms)
-    avg_ms = ms_tot / max(n_launch, 1)
-    bytes_per_launch = BYTES_PER_UPDATE * rows_tot / max(n_launch, 1)
+        for ms, rows, name in zip(*fg.launch_profile()):
+            acc = per.setdefault(name, [0.0, 0, 0])
+            acc[0] += ms
+            acc[1] += rows
+            acc[2] += 1
+    dom = max(per, key=lambda k: per[k][0])
+    d_ms, d_rows, d_n = per[dom]
+    avg_ms = d_ms / d_n
+    bytes_per_launch = BYTES_PER_UPDATE * d_rows / d_n
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     info = fg.info()
+
+    # ---- the same path on a C4-shard-sized forest (BASELINE configs[3]: 100k trees over 8
+    # GPUs = 12.5k trees per GPU), reported beside the C2 headline ----
+    large = None
+    if args.large_trees > 0:
+        hl = g.HostForest.synthetic(args.large_trees, args.rows, seed=SEED,
+                                    first_tree=world * args.trees + rank * args.large_trees)
+        fl = g.Forest(hl, device=local, kernel=args.kernel)
+        for _ in range(2):
+            fl.total_likelihood(P_EXAMPLE)
+        barrier()
+        t1 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            fl.total_likelihood(P_EXAMPLE)
+        torch.cuda.synchronize()
+        lel = (time.perf_counter() - t1) / reps
+        large = {"trees_per_gpu": args.large_trees, "rows_per_gpu": hl.n_rows,
+                 "ms_per_eval": 1e3 * lel, "updates_per_s_per_gpu": hl.n_rows / lel,
+                 "note": "same path, per-GPU shard of BASELINE configs[3] (C4); not the headline value"}
+        fl.close()
 
     result = None
     if rank == 0:
@@ -141,19 +177,22 @@ def main() -> int:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_loglik_level",
+                "kernel": dom,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic_for(dom, args),
                 "bytes_per_update": BYTES_PER_UPDATE,
                 "avg_launch_ms": avg_ms,
-                "launches_timed": n_launch,
+                "launches_timed": d_n,
+                "per_kernel_ms": {k: v[0] / v[2] for k, v in per.items()},
                 "note": "algorithmic bytes only; the path is FP64-latency/VALU bound (DESIGN.md)",
             },
             "total_log_likelihood": ll,
         }
+        if large is not None:
+            result["large_forest"] = large
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

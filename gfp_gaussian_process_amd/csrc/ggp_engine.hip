@@ -486,9 +486,10 @@ struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0;
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
-    int64_t group_max_cells = 12 * 1024;   // auto: group schedule for levels up to this size
+    int64_t group_max_cells = 2048;   // auto: group schedule for levels up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int kernel_used = GGP_KERNEL_LANE;
+    int32_t last_code = 0;
     DevForest F{};
     // device buffers
     double *d_time = nullptr, *d_logl = nullptr, *d_fp = nullptr;
@@ -510,8 +511,16 @@ struct ggp_forest {
     bool profile = false;
     std::vector<hipEvent_t> ev;
     std::vector<int64_t> ev_rows;
+    std::vector<int32_t> ev_kernel;   // per profiled launch: kind << 8 | lanes per cell
+    std::vector<int64_t> ev_rows_launch;
     int n_prof = 0;
 };
+
+// Lane schedule: a wave's cost per step does not depend on how many of its lanes hold a
+// cell (FP64 issue is per wave-instruction, and the clock falls with the number of busy
+// SIMDs), so cells are packed 64 per wave at every level size (tools/lane_scan.py: 1k-30k
+// trees, cpw 64 fastest everywhere).
+static int lane_cpw(const ggp_forest *f) { return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : 64; }
 
 static int launch_levels(ggp_forest *f, const ggp_params &P)
 {
@@ -528,9 +537,11 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
         const bool group = f->kernel_pref == GGP_KERNEL_GROUP ||
                            (f->kernel_pref == GGP_KERNEL_AUTO && n <= f->group_max_cells);
         if (group) {
-            // fewest cells per wave that still fits one wave per SIMD (latency first)
+            // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
+            // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
             int cpw = 1;
             while (cpw < 8 && (n + cpw - 1) / cpw > n_simd) cpw *= 2;
+            if (f->kernel_pref == GGP_KERNEL_AUTO) cpw = std::min(cpw, 2);
             if (f->tune_group_cpw > 0) cpw = f->tune_group_cpw;
             const int blocks = (n + cpw - 1) / cpw;
             switch (cpw) {
@@ -544,19 +555,20 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
                                         f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
             }
             f->kernel_used = GGP_KERNEL_GROUP;
+            f->last_code = GGP_KERNEL_GROUP << 8 | (64 / cpw);
         } else {
-            // spread small levels over SIMDs before packing lanes
-            const int64_t target_waves = (int64_t)f->n_cu * 8;
-            int cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + target_waves - 1) / target_waves));
-            if (f->tune_lane_cpw > 0) cpw = f->tune_lane_cpw;
+            const int cpw = lane_cpw(f);
             const int blocks = (n + cpw - 1) / cpw;
             hipLaunchKernelGGL(k_loglik_level, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
                                f->d_level_cells + a, n, cpw, f->d_state, f->d_cell_ll, f->d_cell_nan);
             f->kernel_used = GGP_KERNEL_LANE;
+            f->last_code = GGP_KERNEL_LANE << 8 | 1;
         }
         HIPCHK(hipGetLastError());
         if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof + 1], f->stream));
+            f->ev_kernel[f->n_prof] = f->last_code;
+            f->ev_rows_launch[f->n_prof] = f->ev_rows[L];
             f->n_prof++;
         }
     }
@@ -675,7 +687,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess) f->n_cu = prop.multiProcessorCount;
-    f->group_max_cells = (int64_t)f->n_cu * 4 * 12;
+    f->group_max_cells = (int64_t)f->n_cu * 4 * 2;
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
     if (const char *e = getenv("GGP_GROUP_CPW")) {
         const int v = atoi(e);
@@ -819,14 +831,16 @@ int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *n
     return ggp_loglik_result(f, ll, nan_cell, nan_row);
 }
 
-int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t cap, int32_t *n)
+int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)
 {
     if (!f || !n) return GGP_EINVAL;
     if (!f->profile) {
         // enable for subsequent calls: one event pair per level
-        const size_t need = 2 * (f->level_start.size() - 1);
-        f->ev.resize(need);
+        const size_t levels = f->level_start.size() - 1;
+        f->ev.resize(2 * levels);
         for (auto &e : f->ev) HIPCHK(hipEventCreate(&e));
+        f->ev_kernel.assign(levels, 0);
+        f->ev_rows_launch.assign(levels, 0);
         f->profile = true;
         *n = 0;
         return GGP_OK;
@@ -837,7 +851,8 @@ int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t cap
         float t = 0;
         HIPCHK(hipEventElapsedTime(&t, f->ev[2 * L], f->ev[2 * L + 1]));
         if (ms) ms[k] = t;
-        if (rows) rows[k] = f->ev_rows[L];
+        if (rows) rows[k] = f->ev_rows_launch[L];
+        if (kernel) kernel[k] = f->ev_kernel[L];
     }
     *n = k;
     return GGP_OK;
@@ -881,17 +896,12 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
         rc = GGP_EDEV;
     if (rc != GGP_OK) { cleanup(); return rc; }
     const int n_levels = (int)f->level_start.size() - 1;
-    auto lane_cpw = [&](int n) {
-        const int64_t target_waves = (int64_t)f->n_cu * 8;
-        int cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + target_waves - 1) / target_waves));
-        return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : cpw;
-    };
     hipError_t e = hipSuccess;
     for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
         const int64_t a = f->level_start[L];
         const int n = (int)(f->level_start[L + 1] - a);
         if (n <= 0) continue;
-        const int cpw = lane_cpw(n);
+        const int cpw = lane_cpw(f);
         hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
                            f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
         e = hipGetLastError();
@@ -900,7 +910,7 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
         const int64_t a = f->level_start[L];
         const int n = (int)(f->level_start[L + 1] - a);
         if (n <= 0) continue;
-        const int cpw = lane_cpw(n);
+        const int cpw = lane_cpw(f);
         hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
                            f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
         e = hipGetLastError();

@@ -282,6 +282,12 @@ class HostForest:
 
 
 # ------------------------------------------------------------------------------------------
+def kernel_name(code: int) -> str:
+    """the HIP kernel symbol behind a launch-profile code (include/ggp.h)"""
+    kind, lanes = code >> 8, code & 0xFF
+    return "k_loglik_level" if kind == N.KERNELS["lane"] else f"k_loglik_group<{lanes}>"
+
+
 class Forest:
     """Device-resident forest + carried state (one HIP device).  Owns a ggp_forest handle."""
 
@@ -346,15 +352,16 @@ class Forest:
 
     def enable_profile(self) -> None:
         n = ctypes.c_int32()
-        self._check(self._lib.ggp_last_launch_profile(self._h, None, None, 0, ctypes.byref(n)))
+        self._check(self._lib.ggp_last_launch_profile(self._h, None, None, None, 0, ctypes.byref(n)))
 
     def launch_profile(self):
         cap = 4096
         ms = (ctypes.c_float * cap)()
         rows = (ctypes.c_int64 * cap)()
+        kern = (ctypes.c_int32 * cap)()
         n = ctypes.c_int32()
-        self._check(self._lib.ggp_last_launch_profile(self._h, ms, rows, cap, ctypes.byref(n)))
-        return list(ms[: n.value]), list(rows[: n.value])
+        self._check(self._lib.ggp_last_launch_profile(self._h, ms, rows, kern, cap, ctypes.byref(n)))
+        return list(ms[: n.value]), list(rows[: n.value]), [kernel_name(k) for k in kern[: n.value]]
 
     def info(self) -> dict:
         nl, mx = ctypes.c_int64(), ctypes.c_int64()
