@@ -109,6 +109,7 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
     if (i >= n) return;
     const int c = cells[i];
     const double *p = P.p;
+    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
     double m[4], C[16];
     const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
     double dt = 0.0;
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
     int nan_row = kNanNone;
     for (int64_t r = r0; r < r1; ++r) {
         if (pending) {   // mean_cov_model over dt (likelihood.h:97-101 / predictions.h:28-31)
-            ggp::propagate_lane(m, C, dt, p[0], p[1], p[2], p[3], p[4], p[5], p[6], s_tab);
+            ggp::propagate_lane(m, C, dt, ou, s_tab);
             if (divide) {
                 ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
                 divide = false;
@@ -153,8 +154,37 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
 // the G lanes through LDS (ggp_prop.h tasks), cutting the per-step latency that bounds
 // small forests.  Bitwise identical to the lane schedule.
 // ------------------------------------------------------------------------------------------
+// Optional per-stage cycle stamps (tools/stamp_group.hip builds this file with GGP_STAMPS;
+// the shipped library never does).
+#ifdef GGP_STAMPS
+__device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + stage]
+#define GGP_STAMP_DECL unsigned long long st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, st_now = 0; int st_steps = 0
+#define GGP_STAMP(k)                                                                       \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_now)::"memory");   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        if ((k) > 0) st_acc[(k) - 1] += st_now - st_prev;                                  \
+        st_prev = st_now;                                                                  \
+    } while (0)
+#define GGP_STAMP_STEP() ++st_steps
+#define GGP_STAMP_FLUSH()                                                                  \
+    do {                                                                                   \
+        if (threadIdx.x == 0) {                                                            \
+            const int o_ = 16 * (CPW == 1 ? 0 : CPW == 2 ? 1 : CPW == 4 ? 2 : 3);          \
+            for (int k_ = 0; k_ < 9; ++k_) atomicAdd(&g_stamp[o_ + k_], st_acc[k_]);       \
+            atomicAdd(&g_stamp[o_ + 15], (unsigned long long)st_steps);                    \
+        }                                                                                  \
+    } while (0)
+#else
+#define GGP_STAMP_DECL
+#define GGP_STAMP(k)
+#define GGP_STAMP_STEP()
+#define GGP_STAMP_FLUSH()
+#endif
+
 constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI;   // doubles of LDS per cell
-constexpr int kStageB = ggp::NXT + ggp::ND + 3;                  // exp + Dawson + pow tasks
+
 
 template <int G>
 __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
@@ -164,6 +194,9 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
                                                      int32_t *__restrict__ cell_nan)
 {
     constexpr int CPW = 64 / G;
+    constexpr int NXB = (ggp::NXT + G - 1) / G;   // exponential slots per lane
+    constexpr int NDB = (ggp::ND + G - 1) / G;    // Dawson slots per lane
+    constexpr int NCB = (ggp::NI + G - 1) / G;    // integral slots per lane
     __shared__ double lds[CPW * kSlot];
     __shared__ double s_tab[kDawsonTab];
     const int lane = threadIdx.x;
@@ -175,11 +208,32 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
     double *Dl = Xl + ggp::NX;
     double *Pl = Dl + ggp::ND;
     double *Il = Pl + ggp::NPW;
+    // this lane's task descriptors never change: keep them in registers (no loads in the step
+    // loop).  Slots past the end of a list run task 0 and are not stored, so every slot is
+    // computed unconditionally and the compiler can overlap their dependency chains.
+    uint32_t xd[NXB], dd[NDB];
+    ggp::ITask cd[NCB];
+#pragma unroll
+    for (int q = 0; q < NXB; ++q) {
+        const int j = lg + q * G;
+        xd[q] = ggp::pack_x(ggp::kXT[j < ggp::NXT ? j : 0]);
+    }
+#pragma unroll
+    for (int q = 0; q < NDB; ++q) {
+        const int j = lg + q * G;
+        dd[q] = ggp::pack_d(ggp::kDT[j < ggp::ND ? j : 0]);
+    }
+#pragma unroll
+    for (int q = 0; q < NCB; ++q) {
+        const int j = lg + q * G;
+        cd[q] = ggp::kIT[j < ggp::NI ? j : 0];
+    }
     const double *p = P.p;
+    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
     int c = 0;
     int64_t r = 0, r1 = 0, r0 = 0;
-    double dt = 0.0;
+    double dt = 0.0, t_cur = 0.0;
     bool pending = false, divide = false;
     if (valid) {
         c = cells[i];
@@ -188,33 +242,61 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         r = r0;
         pending = cell_prologue(F, p, state, c, r0, m, C, dt);
         divide = pending;
+        t_cur = F.time[r0];
     }
     if (lg == 0) Xl[ggp::X_ONE] = 1.0;
     double cl = 0.0;
     int nan_row = kNanNone;
     bool live = valid;
+    GGP_STAMP_DECL;
     while (__any(live)) {   // wave-uniform loop over steps
+        GGP_STAMP(0);
+        GGP_STAMP_STEP();
+        // row data of this step, loaded now and consumed after the propagation (~10k cycles)
+        double y_l = 0.0, y_f = 0.0, t_next = 0.0;
+        if (live) {
+            y_l = F.logl[r];
+            y_f = F.fp[r];
+            if (r + 1 < r1) t_next = F.time[r + 1];
+        }
         const bool prop = live && pending;
         ggp::Step S;
         if (prop) {
-            ggp::step_init(S, m, C, dt, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
-            for (int j = lg; j < kStageB; j += G) {
-                if (j < ggp::NXT) {
-                    Xl[j] = ggp::exp_task(S, j);
-                } else if (j < ggp::NXT + ggp::ND) {
-                    Dl[j - ggp::NXT] = ggp::dawson_task(S, j - ggp::NXT, s_tab);
-                } else {
-                    const int q = j - ggp::NXT - ggp::ND;
-                    const double v = ggp::pow_task(S, q);
-                    Pl[q] = v;
-                    Pl[3 + q] = 1.0 / v;
-                }
+            ggp::step_init(S, m, C, dt, ou);
+        }
+        GGP_STAMP(1);
+        if (prop) {
+            double ev[NXB], dv[NDB];
+#pragma unroll
+            for (int q = 0; q < NXB; ++q) ev[q] = ggp::exp_body(S, ggp::unpack_x(xd[q]));
+#pragma unroll
+            for (int q = 0; q < NDB; ++q) dv[q] = ggp::dawson_body(S, ggp::unpack_d(dd[q]), s_tab);
+            const double pw = ggp::pow_task(S, lg < 3 ? lg : 0);
+#pragma unroll
+            for (int q = 0; q < NXB; ++q)
+                if (lg + q * G < ggp::NXT) Xl[lg + q * G] = ev[q];
+#pragma unroll
+            for (int q = 0; q < NDB; ++q)
+                if (lg + q * G < ggp::ND) Dl[lg + q * G] = dv[q];
+            if (lg < 3) {
+                Pl[lg] = pw;
+                Pl[3 + lg] = 1.0 / pw;
             }
         }
+        GGP_STAMP(2);
         __syncthreads();
-        if (prop)
-            for (int j = lg; j < ggp::NI; j += G) Il[j] = ggp::tau_task(S, j, Xl, Dl, Pl);
+        GGP_STAMP(3);
+        if (prop) {
+            double iv[NCB];
+#pragma unroll
+            for (int q = 0; q < NCB; ++q) iv[q] = ggp::tau_body(S, cd[q], Xl, Dl, Pl);
+#pragma unroll
+            for (int q = 0; q < NCB; ++q)
+                if (lg + q * G < ggp::NI) Il[lg + q * G] = iv[q];
+        }
+        GGP_STAMP(4);
         __syncthreads();
+        GGP_STAMP(5);
         if (prop) {
             ggp::outputs(S, Il, Xl, m, C);
             if (divide) {
@@ -222,9 +304,10 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
                 divide = false;
             }
         }
+        GGP_STAMP(6);
         if (live) {
-            const double x0 = F.logl[r] - m[0];
-            const double x1 = F.fp[r] - m[1];
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
             ggp_innov v;
             ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
             cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
@@ -234,13 +317,17 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
             } else {
                 ggp_posterior(m, C, x0, x1, v);
                 pending = r + 1 < r1;
-                if (pending) dt = F.time[r + 1] - F.time[r];
+                if (pending) dt = t_next - t_cur;
+                t_cur = t_next;
                 ++r;
                 live = r < r1;
             }
         }
+        GGP_STAMP(7);
         __syncthreads();   // LDS slots are rewritten by the next step
+        GGP_STAMP(8);
     }
+    GGP_STAMP_FLUSH();
     if (valid && lg == 0) {
         double *st = state + (size_t)20 * c;
 #pragma unroll
@@ -294,7 +381,7 @@ __global__ __launch_bounds__(64) void k_fwd_level(DevForest F, const double *__r
     const double *pprop = pi;
     for (int64_t r = r0; r < r1; ++r) {
         if (pending) {
-            ggp::propagate_lane(m, C, dt, pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6], s_tab);
+            ggp::propagate_lane(m, C, dt, ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]), s_tab);
             if (divide) {
                 ggp::division_map(m, C, pi[9], pi[10], F.binomial, F.log2);
                 divide = false;
@@ -366,7 +453,7 @@ __global__ __launch_bounds__(64) void k_bwd_level(DevForest F, const double *__r
             ggp::mult_gauss(m, C, m2, C2);
         }
         const double dt = F.time[F.row_off[d1]] - F.time[r1 - 1];
-        ggp::propagate_lane(m, C, dt, -pi[0], pi[1], pi[2], -pi[3], pi[4], pi[5], -pi[6], s_tab);
+        ggp::propagate_lane(m, C, dt, ggp::make_ou(-pi[0], pi[1], pi[2], -pi[3], pi[4], pi[5], -pi[6]), s_tab);
     }
     for (int64_t r = r1 - 1; r >= r0; --r) {
         double rm[4], rC[16];
@@ -384,7 +471,7 @@ __global__ __launch_bounds__(64) void k_bwd_level(DevForest F, const double *__r
         ggp_posterior(m, C, x0, x1, v);
         if (r > r0) {
             const double *q = seg_params(F, ptab, n_seg, r - 1);
-            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], -q[0], q[1], q[2], -q[3], q[4], q[5], -q[6], s_tab);
+            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], ggp::make_ou(-q[0], q[1], q[2], -q[3], q[4], q[5], -q[6]), s_tab);
         }
     }
     store20(pstate + (size_t)20 * c, m, C);

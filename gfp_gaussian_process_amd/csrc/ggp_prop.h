@@ -141,6 +141,35 @@ constexpr ITask kIT[NI] = {
     {3, 3, 1, 2, XC_C, XE_4Ct, XE_4C2, XA_4t, XA_42, D_4_t, D_4_2},
 };
 
+// ---- OU parameters and the parameter-only constants of one step -----------------------
+// Everything here depends on the 7 propagator parameters only, so a kernel forms it once
+// instead of once per step (values identical: the same expressions).
+struct OU {
+    double ml, gl, sl2, mq, gq, sq2, b;
+    double r_gl, r_gq, gq2, gqq2, r_gq2, r_gqq2, gl2, r_gl2;
+    double k_xl, k_xx, k_ll, k_qq;   // the sl2 / sq2 prefactors of cov_xl, cov_xx, cov_ll, cov_qq
+};
+
+GGP_DEV OU make_ou(const double ml, const double gl, const double sl2, const double mq, const double gq,
+                   const double sq2, const double b)
+{
+    OU P;
+    P.ml = ml; P.gl = gl; P.sl2 = sl2; P.mq = mq; P.gq = gq; P.sq2 = sq2; P.b = b;
+    P.r_gl = 1.0 / gl;
+    P.r_gq = 1.0 / gq;
+    P.gq2 = 2. * gq;
+    P.gqq2 = 2. * (gq * gq);
+    P.r_gq2 = 1.0 / P.gq2;
+    P.r_gqq2 = 1.0 / P.gqq2;
+    P.gl2 = gl * gl;
+    P.r_gl2 = 1.0 / P.gl2;
+    P.k_xl = sl2 / (2 * (gl * gl));
+    P.k_xx = sl2 / (2 * pow(gl, 3));
+    P.k_ll = sl2 / (2 * gl);
+    P.k_qq = rdiv(sq2, 2 * gq, P.r_gq2);
+    return P;
+}
+
 // ---- per-step scalars ------------------------------------------------------------------
 struct Step {
     // z(t0) state (mean_cov_model.h:221-235) and OU parameters (already sign-flipped for _r)
@@ -151,17 +180,21 @@ struct Step {
     double B0, B1, B2, B3, B4, B5;                     // B1..B6
     double c0, c1, c2, c3, c4, c5, c6, c7, c8, c9;     // cA cB cJ cG cC cD cE cF cI cH
     double r_two_sa, r_four_a, r_gl, r_gq;
+    double gq2, gqq2, r_gq2, r_gqq2, gl2, r_gl2, k_xl, k_xx, k_ll, k_qq;
 };
 
-GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t, const double ml,
-                       const double gl, const double sl2, const double mq, const double gq,
-                       const double sq2, const double b)
+GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t, const OU &P)
 {
+    const double ml = P.ml, gl = P.gl, gq = P.gq, b = P.b;
     S.bx = m[0]; S.bg = m[1]; S.bl = m[2]; S.bq = m[3];
     S.Cxx = C[0]; S.Cxg = C[1]; S.Cxl = C[2]; S.Cxq = C[3];
     S.Cgg = C[5]; S.Cgl = C[6]; S.Cgq = C[7];
     S.Cll = C[10]; S.Clq = C[11]; S.Cqq = C[15];
-    S.ml = ml; S.gl = gl; S.sl2 = sl2; S.mq = mq; S.gq = gq; S.sq2 = sq2; S.b = b;
+    S.ml = ml; S.gl = gl; S.sl2 = P.sl2; S.mq = P.mq; S.gq = gq; S.sq2 = P.sq2; S.b = b;
+    S.r_gl = P.r_gl; S.r_gq = P.r_gq;
+    S.gq2 = P.gq2; S.gqq2 = P.gqq2; S.r_gq2 = P.r_gq2; S.r_gqq2 = P.r_gqq2;
+    S.gl2 = P.gl2; S.r_gl2 = P.r_gl2;
+    S.k_xl = P.k_xl; S.k_xx = P.k_xx; S.k_ll = P.k_ll; S.k_qq = P.k_qq;
     S.t = t;
     S.t2 = 2 * t;
     const double a = S.Cll / 2.;
@@ -191,8 +224,6 @@ GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t
     S.c9 = 2 * bx + 2 * Cxx - 2 * b * t - 2 * gq * t;  // cH
     S.r_two_sa = 1.0 / S.two_sa;
     S.r_four_a = 1.0 / S.four_a;
-    S.r_gl = 1.0 / gl;
-    S.r_gq = 1.0 / gq;
 }
 
 // select without dynamic register indexing (compile-time index folds to one operand)
@@ -239,11 +270,22 @@ GGP_DEV double exp_body(const Step &S, const XTask T)
 
 GGP_DEV double exp_task(const Step &S, int j) { return exp_body(S, kXT[j]); }
 
-GGP_DEV double dawson_task(const Step &S, int d, const double *tab)
+GGP_DEV double dawson_body(const Step &S, const DTask T, const double *tab)
 {
-    const DTask T = kDT[d];
     return ggp_dawson_tab(zval(S, T.iB, T.it), tab);
 }
+
+GGP_DEV double dawson_task(const Step &S, int d, const double *tab) { return dawson_body(S, kDT[d], tab); }
+
+// task descriptors packed in one register word (group schedule: loaded once per kernel)
+GGP_DEV uint32_t pack_x(const XTask T) { return T.kind | T.iB << 8 | T.ic << 16 | (uint32_t)T.it << 24; }
+GGP_DEV XTask unpack_x(const uint32_t w)
+{
+    return XTask{(unsigned char)(w & 0xff), (unsigned char)(w >> 8 & 0xff), (unsigned char)(w >> 16 & 0xff),
+                 (unsigned char)(w >> 24)};
+}
+GGP_DEV uint32_t pack_d(const DTask T) { return T.iB | T.it << 8; }
+GGP_DEV DTask unpack_d(const uint32_t w) { return DTask{(unsigned char)(w & 0xff), (unsigned char)(w >> 8 & 0xff)}; }
 
 // the three tauint denominators 4 a^1.5, 8 a^2.5, 16 a^3.5.  pow(a, k + 1/2) is formed as
 // a^k * sqrt(a) (sqrt correctly rounded, <= 2 ulp from glibc's pow; the total
@@ -309,8 +351,8 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     const double r_ebt = 1.0 / ebt, r_ebglt = 1.0 / ebglt, r_ebgqt = 1.0 / ebgqt;
     const double ebt_gl = ebt * gl, ebglt_gl = ebglt * gl;
     const double r_ebt_gl = 1.0 / ebt_gl, r_ebglt_gl = 1.0 / ebglt_gl;
-    const double gq2 = 2. * gq, gqq2 = 2. * (gq * gq);
-    const double r_gq2 = 1.0 / gq2, r_gqq2 = 1.0 / gqq2;
+    const double gq2 = S.gq2, gqq2 = S.gqq2;
+    const double r_gq2 = S.r_gq2, r_gqq2 = S.r_gqq2;
 #define DGL(x) rdiv((x), gl, rgl)
 #define DGQ(x) rdiv((x), gq, rgq)
 
@@ -320,8 +362,10 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     nm[2] = ml + (bl - ml) * egl;
     nm[3] = mq + (bq - mq) * egq;
 
+    double nxg = 0, nxl = 0, nxq = 0, ngl = 0, nxx = 0, nll = 0, ngq = 0, ngg = 0, nlq = 0, nqq = 0;
+    {
     // cov_xg (mean_cov_model.h:97-115)
-    const double nxg =
+    nxg =
         rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + rdiv(bg * bl, ebt_gl, r_ebt_gl)
         + rdiv(Cgl, ebt_gl, r_ebt_gl) - rdiv(bg * bl, ebglt_gl, r_ebglt_gl) - rdiv(Cgl, ebglt_gl, r_ebglt_gl)
         - rdiv(bg * ml, ebt_gl, r_ebt_gl) + rdiv(bg * ml, ebglt_gl, r_ebglt_gl) + rdiv(bg * ml * t, ebt, r_ebt)
@@ -343,12 +387,12 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
         - nm[1] * nm[0];
 
     // cov_xl, cov_xq (mean_cov_model.h:117-123)
-    const double nxl = sl2 / (2 * (gl * gl)) * ((1 - egl) * (1 - egl))
+    nxl = S.k_xl * ((1 - egl) * (1 - egl))
                        + DGL(Cll * egl * (1 - egl)) + Cxl * egl;
-    const double nxq = DGL(Clq * (1 - egl) * egq) + Cxq * egq;
+    nxq = DGL(Clq * (1 - egl) * egq) + Cxq * egq;
 
     // cov_gl (mean_cov_model.h:172-181)
-    const double ngl =
+    ngl =
         rdiv(bg * bl, ebglt, r_ebglt) + rdiv(Cgl, ebglt, r_ebglt) + rdiv(bg * ml, ebt, r_ebt)
         - rdiv(bg * ml, ebglt, r_ebglt)
         + Cll * mq * I[O_1B] + Clq * ml * I[O_2A]
@@ -360,8 +404,14 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
            + ml * mq) * I[Z_2B]
         - nm[1] * nm[2];
 
+    // cov_xx, cov_ll (mean_cov_model.h:93-95, 198-200)
+    nxx = rdiv(Cll * ((1 - egl) * (1 - egl)), S.gl2, S.r_gl2) + rdiv(2 * Cxl * (1 - egl), gl, rgl) + Cxx
+          + S.k_xx * (2 * gl * t - 3 + 4 * egl - (egl * egl));
+    nll = Cll * (egl * egl) + S.k_ll * (1 - (egl * egl));
+    }
+    {
     // cov_gq (mean_cov_model.h:183-196)
-    const double ngq =
+    ngq =
         rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)
         - rdiv(bg * mq, ebgqt, r_ebgqt)
         + Clq * mq * I[O_1J] + Clq * mq * I[O_2A]
@@ -377,7 +427,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     // cov_gg (mean_cov_model.h:125-170)
     const double k17 = DGQ(2 * bq * mq) + DGQ(4 * Cxq * mq) - DGQ(2 * (mq * mq));
     const double k19 = DGQ(-2 * bq * mq) - DGQ(4 * Cxq * mq) + DGQ(2 * (mq * mq));
-    const double ngg =
+    ngg =
         ((bg * bg) + Cgg) / e2bt
         + 2 * Cgl * mq * I[O_1G]
         + DGQ(mq * (2 * Clq + gq * mq) * I[O_3C])
@@ -413,12 +463,10 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
         - rdiv(sq2 * I[Z_6H2], gqq2, r_gqq2)
         - (nm[1] * nm[1]);
 
-    // cov_xx, cov_ll, cov_lq, cov_qq (mean_cov_model.h:93-95, 198-208)
-    const double nxx = Cll * ((1 - egl) * (1 - egl)) / (gl * gl) + rdiv(2 * Cxl * (1 - egl), gl, rgl) + Cxx
-                       + sl2 / (2 * pow(gl, 3)) * (2 * gl * t - 3 + 4 * egl - (egl * egl));
-    const double nll = Cll * (egl * egl) + sl2 / (2 * gl) * (1 - (egl * egl));
-    const double nlq = Clq * egl * egq;
-    const double nqq = rdiv(sq2, 2 * gq, r_gq2) * (1 - (egq * egq)) + Cqq * (egq * egq);
+    // cov_lq, cov_qq (mean_cov_model.h:202-208)
+    nlq = Clq * egl * egq;
+    nqq = S.k_qq * (1 - (egq * egq)) + Cqq * (egq * egq);
+    }
 
 #undef DGL
 #undef DGQ
@@ -456,12 +504,10 @@ GGP_DEV void lane_taus(const Step &S, const XA &X, const DA &Dw, const PA &PW, d
 }
 
 // ---- lane schedule: one lane runs every task of its own cell
-GGP_DEV void propagate_lane(double *m, double *C, const double t, const double ml, const double gl,
-                            const double sl2, const double mq, const double gq, const double sq2,
-                            const double b, const double *tab)
+GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, const double *tab)
 {
     Step S;
-    step_init(S, m, C, t, ml, gl, sl2, mq, gq, sq2, b);
+    step_init(S, m, C, t, P);
     double X[NX];
     lane_exps(S, X, std::make_index_sequence<NXT>{});
     X[X_ONE] = 1.0;

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(64) void probe(const double *m0, const double *C0, 
         unsigned long long t0, t1, t2, t3, t4, t5;
         STAMP(t0);
         ggp::Step S;
-        ggp::step_init(S, m, C, 1.0, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        ggp::step_init(S, m, C, 1.0, ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
         STAMP(t1);
         unsigned long long u1, u2, u3;
         Xl[lg] = ggp::exp_task(S, lg);                        // exps 0..63
