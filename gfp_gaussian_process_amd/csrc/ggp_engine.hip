@@ -183,7 +183,7 @@ __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + sta
 #define GGP_STAMP_FLUSH()
 #endif
 
-constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI;   // doubles of LDS per cell
+constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI + ggp::SB_N;   // doubles of LDS per cell
 
 
 template <int G>
@@ -198,6 +198,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
     constexpr int NDB = (ggp::ND + G - 1) / G;    // Dawson slots per lane
     constexpr int NCB = (ggp::NI + G - 1) / G;    // integral slots per lane
     __shared__ double lds[CPW * kSlot];
+    __shared__ double s_ou[ggp::OU_N];
     __shared__ double s_tab[kDawsonTab];
     const int lane = threadIdx.x;
     load_dawson_table(s_tab, lane);
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
     double *Dl = Xl + ggp::NX;
     double *Pl = Dl + ggp::ND;
     double *Il = Pl + ggp::NPW;
+    double *Sb = Il + ggp::NI;        // the step block (ggp_prop.h)
     // this lane's task descriptors never change: keep them in registers (no loads in the step
     // loop).  Slots past the end of a list run task 0 and are not stored, so every slot is
     // computed unconditionally and the compiler can overlap their dependency chains.
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         cd[q] = ggp::kIT[j < ggp::NI ? j : 0];
     }
     const double *p = P.p;
-    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    if (lane == 0) ggp::store_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]), s_ou);
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
     int c = 0;
     int64_t r = 0, r1 = 0, r0 = 0;
@@ -245,6 +247,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         t_cur = F.time[r0];
     }
     if (lg == 0) Xl[ggp::X_ONE] = 1.0;
+    __syncthreads();   // s_tab, s_ou
     double cl = 0.0;
     int nan_row = kNanNone;
     bool live = valid;
@@ -260,11 +263,14 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
             if (r + 1 < r1) t_next = F.time[r + 1];
         }
         const bool prop = live && pending;
-        ggp::Step S;
-        if (prop) {
-            ggp::step_init(S, m, C, dt, ou);
+        if (prop && lg == 0) {
+            ggp::Step S;
+            ggp::step_init(S, m, C, dt, ggp::load_ou(s_ou));
+            ggp::store_step(S, Sb);
         }
+        __syncthreads();
         GGP_STAMP(1);
+        const ggp::StepL S(Sb);
         if (prop) {
             double ev[NXB], dv[NDB];
 #pragma unroll
@@ -298,7 +304,9 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         __syncthreads();
         GGP_STAMP(5);
         if (prop) {
-            ggp::outputs(S, Il, Xl, m, C);
+            ggp::Step SR;
+            ggp::load_step(SR, Sb, s_ou);
+            ggp::outputs(SR, Il, Xl, m, C);
             if (divide) {
                 ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
                 divide = false;

@@ -181,6 +181,11 @@ struct Step {
     double c0, c1, c2, c3, c4, c5, c6, c7, c8, c9;     // cA cB cJ cG cC cD cE cF cI cH
     double r_two_sa, r_four_a, r_gl, r_gq;
     double gq2, gqq2, r_gq2, r_gqq2, gl2, r_gl2, k_xl, k_xx, k_ll, k_qq;
+    // indexed operands of the tasks (selects: no dynamic register indexing)
+    GGP_DEV double Bv(int i) const;
+    GGP_DEV double Cv(int i) const;
+    GGP_DEV double Tv(int i) const;
+    GGP_DEV double SVv(int s) const;
 };
 
 GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t, const OU &P)
@@ -237,25 +242,116 @@ GGP_DEV double pickC(const Step &S, int i)
          : i == 5 ? S.c5 : i == 6 ? S.c6 : i == 7 ? S.c7 : i == 8 ? S.c8 : S.c9;
 }
 GGP_DEV double pickT(const Step &S, int i) { return i == 0 ? 0.0 : i == 1 ? S.t : S.t2; }
-
-// z = (B + 2a t_i) / (2 sqrt a)  (t_i = 0: B / (2 sqrt a))
-GGP_DEV double zval(const Step &S, int iB, int it)
+// the exponents s of exp(s t) (mean_cov_model.h: b, b + gl, 2b, b + gq, -gl, -gq)
+GGP_DEV double pickSV(const Step &S, int s)
 {
-    const double B = pickB(S, iB);
-    const double num = it == 0 ? B : B + S.two_a * pickT(S, it);
+    return s == 0 ? S.b : s == 1 ? S.b + S.gl : s == 2 ? 2 * S.b : s == 3 ? S.b + S.gq : s == 4 ? -S.gl : -S.gq;
+}
+GGP_DEV double Step::Bv(int i) const { return pickB(*this, i); }
+GGP_DEV double Step::Cv(int i) const { return pickC(*this, i); }
+GGP_DEV double Step::Tv(int i) const { return pickT(*this, i); }
+GGP_DEV double Step::SVv(int s) const { return pickSV(*this, s); }
+
+// ---- the step block in LDS (group schedule) ----------------------------------------------
+// One lane forms the Step and stores it; the task lanes read their operands by index (one
+// LDS load instead of a select chain) and the Step does not stay live in registers across
+// the task stages.  Values are copies, so results are bitwise those of the register form.
+enum {
+    SB_B = 0, SB_C = SB_B + 6, SB_T = SB_C + 10, SB_SV = SB_T + 3,
+    SB_A = SB_SV + 6, SB_TWO_A, SB_FOUR_A, SB_R_FOUR_A, SB_TWO_SA, SB_R_TWO_SA, SB_M2SA, SB_FOUR_AA,
+    SB_STATE,                         // bx bg bl bq Cxx Cxg Cxl Cxq Cgg Cgl Cgq Cll Clq Cqq
+    SB_N = SB_STATE + 14
+};
+enum { OU_N = 19 };                   // the OU struct, once per workgroup
+
+GGP_DEV void store_ou(const OU &P, double *o)
+{
+    const double v[OU_N] = {P.ml, P.gl, P.sl2, P.mq, P.gq, P.sq2, P.b, P.r_gl, P.r_gq, P.gq2, P.gqq2,
+                            P.r_gq2, P.r_gqq2, P.gl2, P.r_gl2, P.k_xl, P.k_xx, P.k_ll, P.k_qq};
+#pragma unroll
+    for (int k = 0; k < OU_N; ++k) o[k] = v[k];
+}
+
+GGP_DEV OU load_ou(const double *o)
+{
+    OU P;
+    P.ml = o[0]; P.gl = o[1]; P.sl2 = o[2]; P.mq = o[3]; P.gq = o[4]; P.sq2 = o[5]; P.b = o[6];
+    P.r_gl = o[7]; P.r_gq = o[8]; P.gq2 = o[9]; P.gqq2 = o[10]; P.r_gq2 = o[11]; P.r_gqq2 = o[12];
+    P.gl2 = o[13]; P.r_gl2 = o[14]; P.k_xl = o[15]; P.k_xx = o[16]; P.k_ll = o[17]; P.k_qq = o[18];
+    return P;
+}
+
+GGP_DEV void store_step(const Step &S, double *sb)
+{
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sb[SB_B + i] = pickB(S, i);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) sb[SB_C + i] = pickC(S, i);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sb[SB_T + i] = pickT(S, i);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sb[SB_SV + i] = pickSV(S, i);
+    sb[SB_A] = S.a; sb[SB_TWO_A] = S.two_a; sb[SB_FOUR_A] = S.four_a; sb[SB_R_FOUR_A] = S.r_four_a;
+    sb[SB_TWO_SA] = S.two_sa; sb[SB_R_TWO_SA] = S.r_two_sa; sb[SB_M2SA] = S.m2sa; sb[SB_FOUR_AA] = S.four_aa;
+    const double st[14] = {S.bx, S.bg, S.bl, S.bq, S.Cxx, S.Cxg, S.Cxl, S.Cxq, S.Cgg, S.Cgl, S.Cgq, S.Cll, S.Clq, S.Cqq};
+#pragma unroll
+    for (int k = 0; k < 14; ++k) sb[SB_STATE + k] = st[k];
+}
+
+// the full Step back from the block (the outputs stage); unused fields are dead loads
+GGP_DEV void load_step(Step &S, const double *sb, const double *ou)
+{
+    const OU P = load_ou(ou);
+    S.ml = P.ml; S.gl = P.gl; S.sl2 = P.sl2; S.mq = P.mq; S.gq = P.gq; S.sq2 = P.sq2; S.b = P.b;
+    S.r_gl = P.r_gl; S.r_gq = P.r_gq;
+    S.gq2 = P.gq2; S.gqq2 = P.gqq2; S.r_gq2 = P.r_gq2; S.r_gqq2 = P.r_gqq2;
+    S.gl2 = P.gl2; S.r_gl2 = P.r_gl2;
+    S.k_xl = P.k_xl; S.k_xx = P.k_xx; S.k_ll = P.k_ll; S.k_qq = P.k_qq;
+    S.B0 = sb[SB_B]; S.B1 = sb[SB_B + 1]; S.B2 = sb[SB_B + 2]; S.B3 = sb[SB_B + 3]; S.B4 = sb[SB_B + 4];
+    S.B5 = sb[SB_B + 5];
+    S.c0 = sb[SB_C]; S.c1 = sb[SB_C + 1]; S.c2 = sb[SB_C + 2]; S.c3 = sb[SB_C + 3]; S.c4 = sb[SB_C + 4];
+    S.c5 = sb[SB_C + 5]; S.c6 = sb[SB_C + 6]; S.c7 = sb[SB_C + 7]; S.c8 = sb[SB_C + 8]; S.c9 = sb[SB_C + 9];
+    S.t = sb[SB_T + 1]; S.t2 = sb[SB_T + 2];
+    S.a = sb[SB_A]; S.two_a = sb[SB_TWO_A]; S.four_a = sb[SB_FOUR_A]; S.r_four_a = sb[SB_R_FOUR_A];
+    S.two_sa = sb[SB_TWO_SA]; S.r_two_sa = sb[SB_R_TWO_SA]; S.m2sa = sb[SB_M2SA]; S.four_aa = sb[SB_FOUR_AA];
+    S.bx = sb[SB_STATE]; S.bg = sb[SB_STATE + 1]; S.bl = sb[SB_STATE + 2]; S.bq = sb[SB_STATE + 3];
+    S.Cxx = sb[SB_STATE + 4]; S.Cxg = sb[SB_STATE + 5]; S.Cxl = sb[SB_STATE + 6]; S.Cxq = sb[SB_STATE + 7];
+    S.Cgg = sb[SB_STATE + 8]; S.Cgl = sb[SB_STATE + 9]; S.Cgq = sb[SB_STATE + 10]; S.Cll = sb[SB_STATE + 11];
+    S.Clq = sb[SB_STATE + 12]; S.Cqq = sb[SB_STATE + 13];
+}
+
+// task operand view of the block: the members the task bodies use, indexed loads for the rest
+struct StepL {
+    const double *sb;
+    double a, two_a, four_a, r_four_a, two_sa, r_two_sa, m2sa, four_aa, t;
+    GGP_DEV explicit StepL(const double *p)
+        : sb(p), a(p[SB_A]), two_a(p[SB_TWO_A]), four_a(p[SB_FOUR_A]), r_four_a(p[SB_R_FOUR_A]),
+          two_sa(p[SB_TWO_SA]), r_two_sa(p[SB_R_TWO_SA]), m2sa(p[SB_M2SA]), four_aa(p[SB_FOUR_AA]),
+          t(p[SB_T + 1]) {}
+    GGP_DEV double Bv(int i) const { return sb[SB_B + i]; }
+    GGP_DEV double Cv(int i) const { return sb[SB_C + i]; }
+    GGP_DEV double Tv(int i) const { return sb[SB_T + i]; }
+    GGP_DEV double SVv(int s) const { return sb[SB_SV + s]; }
+};
+
+// z = (B + 2a t_i) / (2 sqrt a)  (t_i = 0: B / (2 sqrt a)).  ST = Step (registers) or StepL.
+template <class ST>
+GGP_DEV double zval(const ST &S, int iB, int it)
+{
+    const double B = S.Bv(iB);
+    const double num = it == 0 ? B : B + S.two_a * S.Tv(it);
     return rdiv(num, S.two_sa, S.r_two_sa);
 }
 
-GGP_DEV double exp_body(const Step &S, const XTask T)
+template <class ST>
+GGP_DEV double exp_body(const ST &S, const XTask T)
 {
     // branch-free: every candidate argument is formed from selected operands and the kind
     // picks one, so lanes holding different kinds do not serialise (group schedule)
-    const double ti = pickT(S, T.it);
-    const double B = pickB(S, T.iB);
-    const double c = pickC(S, T.ic);
-    const int s = T.iB;
-    const double sv = s == 0 ? S.b : s == 1 ? S.b + S.gl : s == 2 ? 2 * S.b : s == 3 ? S.b + S.gq
-                    : s == 4 ? -S.gl : -S.gq;
+    const double ti = S.Tv(T.it);
+    const double B = S.Bv(T.iB);
+    const double c = S.Cv(T.ic);
+    const double sv = S.SVv(T.iB);
     const double n = rdiv(-(B * B), S.four_a, S.r_four_a);
     const double zn = T.it == 0 ? B : B + S.two_a * ti;
     const double z = rdiv(zn, S.two_sa, S.r_two_sa);
@@ -270,7 +366,8 @@ GGP_DEV double exp_body(const Step &S, const XTask T)
 
 GGP_DEV double exp_task(const Step &S, int j) { return exp_body(S, kXT[j]); }
 
-GGP_DEV double dawson_body(const Step &S, const DTask T, const double *tab)
+template <class ST>
+GGP_DEV double dawson_body(const ST &S, const DTask T, const double *tab)
 {
     return ggp_dawson_tab(zval(S, T.iB, T.it), tab);
 }
@@ -290,7 +387,8 @@ GGP_DEV DTask unpack_d(const uint32_t w) { return DTask{(unsigned char)(w & 0xff
 // the three tauint denominators 4 a^1.5, 8 a^2.5, 16 a^3.5.  pow(a, k + 1/2) is formed as
 // a^k * sqrt(a) (sqrt correctly rounded, <= 2 ulp from glibc's pow; the total
 // log-likelihood moves by ~1e-11 relative, DESIGN.md "Parity") -- ~10x cheaper than ocml pow.
-GGP_DEV double pow_task(const Step &S, int p)
+template <class ST>
+GGP_DEV double pow_task(const ST &S, int p)
 {
     const double sa = S.two_sa * 0.5;           // sqrt(a), exact
     const double a = S.a;
@@ -300,8 +398,8 @@ constexpr int NPW = 6;   // 3 denominators + 3 reciprocals
 
 // ---- tauint from its pieces (mean_cov_model.h:9-67) ----------------------------------
 // PW = {4 a^1.5, 8 a^2.5, 16 a^3.5, and their reciprocals}
-template <class XA, class DA, class PA>
-GGP_DEV double tau_body(const Step &S, const ITask T, const XA &X, const DA &Dw, const PA &PW)
+template <class ST, class XA, class DA, class PA>
+GGP_DEV double tau_body(const ST &S, const ITask T, const XA &X, const DA &Dw, const PA &PW)
 {
     const double D0 = Dw[T.d0], D1 = Dw[T.d1];
     if (T.k == 0) {   // zerotauint
@@ -309,13 +407,13 @@ GGP_DEV double tau_body(const Step &S, const ITask T, const XA &X, const DA &Dw,
         const double x = 2. * (-Z0 * D0 + Z1 * (D1));
         return rdiv(x, S.two_sa, S.r_two_sa);
     }
-    const double B = pickB(S, T.iB);
+    const double B = S.Bv(T.iB);
     const double ec = X[T.xc], E0 = X[T.x0], E1 = X[T.x1], ea0 = X[T.xa0], ea1 = X[T.xa1];
     if (T.k == 1) {   // onetauint
         const double x = (S.m2sa * ec * (ea0 - ea1) + B * 2. * (E0 * D0 - E1 * D1));
         return rdiv(x, PW[0], PW[3]);
     }
-    const double t0 = pickT(S, T.it0), t1 = pickT(S, T.it1);
+    const double t0 = S.Tv(T.it0), t1 = S.Tv(T.it1);
     if (T.k == 2) {   // twotauint
         const double x = (S.two_sa * ec * (ea0 * (B - S.two_a * t0) - ea1 * (B - S.two_a * t1))
                           + (E0 * (S.two_a - B * B) * 2. * D0 + E1 * (-S.two_a + B * B) * 2. * D1));
