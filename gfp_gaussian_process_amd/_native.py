@@ -20,6 +20,8 @@ KERNELS = {"auto": 0, "lane": 1, "group": 2}
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
 c_double_p = ctypes.POINTER(ctypes.c_double)
+# int (*)(const double *x, double *value, void *data)   (ggp_objective_fn, include/ggp_host.h)
+OBJECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_double_p, c_double_p, ctypes.c_void_p)
 
 
 class ForestDesc(ctypes.Structure):
@@ -85,6 +87,12 @@ HOST_SYMBOLS = {
     "ggp_host_forest_n_roots": (ctypes.c_int64, [ctypes.c_void_p]),
     "ggp_synthetic_forest": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                             ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_nldrmd_minimize": (ctypes.c_int, [ctypes.c_int32, OBJECTIVE_FN, ctypes.c_void_p, c_double_p, c_double_p,
+                                           c_double_p, c_double_p, ctypes.c_double, ctypes.c_int64, c_double_p,
+                                           c_int64_p]),
+    "ggp_num_hessian": (ctypes.c_int, [ctypes.c_int32, OBJECTIVE_FN, ctypes.c_void_p, c_double_p, c_int32_p,
+                                       ctypes.c_int32, ctypes.c_double, c_double_p]),
+    "ggp_inverse_pplu": (ctypes.c_int, [ctypes.c_int32, c_double_p, c_double_p]),
 }
 
 _cache: dict = {}

@@ -63,7 +63,9 @@ def build(verbose: bool = False, force: bool = False) -> dict:
     # --- host ingest ---
     host_src = os.path.join(CSRC, "host", "ggp_host.cpp")
     host = os.path.join(LIB, "libggp_host.so")
-    if force or not _newer(host, [host_src, os.path.join(INC, "ggp_host.h"), os.path.join(INC, "ggp.h")]):
+    host_deps = [host_src, os.path.join(CSRC, "host", "ggp_nelder_mead.h"), os.path.join(INC, "ggp_host.h"),
+                 os.path.join(INC, "ggp.h")]
+    if force or not _newer(host, host_deps):
         cxx = shutil.which("g++") or "g++"
         _run([cxx, *CXX_FLAGS, "-shared", f"-I{INC}", "-o", host, host_src, "-lpthread"], verbose)
     out["libggp_host"] = host

@@ -349,6 +349,145 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 
 
 // ------------------------------------------------------------------------------------------
+// GROUP2 schedule: one cell per 128-lane workgroup.  Wave 0 owns the cell (state, step block,
+// Kalman update); both waves share the exponential / Dawson / integral tasks and split the
+// outputs (ggp::outputs<0> / <1>), exchanging wave 1's half through LDS.  Nothing is
+// computed twice, so a level of at most one cell per SIMD gets two SIMDs' issue per cell.
+// Bitwise identical to the other schedules.
+// ------------------------------------------------------------------------------------------
+constexpr int kX2 = 37, kD2 = 7, kI2 = 23;   // per-wave task counts (exp, Dawson, integral)
+static_assert(2 * kX2 >= ggp::NXT && 2 * kD2 >= ggp::ND && 2 * kI2 >= ggp::NI, "task split");
+
+__global__ __launch_bounds__(128) void k_loglik_group2(DevForest F, ggp_params P,
+                                                       const int32_t *__restrict__ cells, int n,
+                                                       double *__restrict__ state,
+                                                       double *__restrict__ cell_ll,
+                                                       int32_t *__restrict__ cell_nan)
+{
+    __shared__ double lds[kSlot + 4];
+    __shared__ double s_ou[ggp::OU_N];
+    __shared__ double s_tab[kDawsonTab];
+    __shared__ int s_flag[4];                     // [iteration parity][live, prop]
+    const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
+    for (int k = tid; k < kDawsonTab; k += 128) s_tab[k] = ggp_dawson_coef[k];
+    double *Xl = lds;
+    double *Dl = Xl + ggp::NX;
+    double *Pl = Dl + ggp::ND;
+    double *Il = Pl + ggp::NPW;
+    double *Sb = Il + ggp::NI;
+    double *Ex = lds + kSlot;
+    const int je = wave * kX2 + l, jd = wave * kD2 + l, ji = wave * kI2 + l;
+    const bool ve = l < kX2 && je < ggp::NXT, vd = l < kD2 && jd < ggp::ND, vi = l < kI2 && ji < ggp::NI;
+    const bool vp = wave == 1 && l < 3;
+    const uint32_t xd = ggp::pack_x(ggp::kXT[ve ? je : 0]);
+    const uint32_t dd = ggp::pack_d(ggp::kDT[vd ? jd : 0]);
+    const ggp::ITask cd = ggp::kIT[vi ? ji : 0];
+    const double *p = P.p;
+    if (tid == 0) {
+        ggp::store_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]), s_ou);
+        Xl[ggp::X_ONE] = 1.0;
+    }
+    const int c = cells[blockIdx.x];
+    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+    int64_t r = r0;
+    double m[4] = {0, 0, 0, 0}, C[16] = {0};
+    double dt = 0.0, t_cur = 0.0, cl = 0.0;
+    bool pending = false, divide = false, live = true;
+    int nan_row = kNanNone;
+    if (wave == 0) {
+        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        divide = pending;
+        t_cur = F.time[r0];
+    }
+    __syncthreads();   // s_tab, s_ou
+    for (int it = 0;; ++it) {
+        double y_l = 0.0, y_f = 0.0, t_next = 0.0;
+        int *fl = s_flag + 2 * (it & 1);
+        if (wave == 0) {
+            if (live) {
+                y_l = F.logl[r];
+                y_f = F.fp[r];
+                if (r + 1 < r1) t_next = F.time[r + 1];
+            }
+            const bool prop = live && pending;
+            if (tid == 0) {
+                if (prop) {
+                    ggp::Step S;
+                    ggp::step_init(S, m, C, dt, ggp::load_ou(s_ou));
+                    ggp::store_step(S, Sb);
+                }
+                fl[0] = live;
+                fl[1] = prop;
+            }
+        }
+        __syncthreads();
+        if (!fl[0]) break;
+        if (fl[1]) {
+            const ggp::StepL S(Sb);
+            const double ev = ggp::exp_body(S, ggp::unpack_x(xd));
+            const double dv = ggp::dawson_body(S, ggp::unpack_d(dd), s_tab);
+            const double pw = ggp::pow_task(S, vp ? l : 0);
+            if (ve) Xl[je] = ev;
+            if (vd) Dl[jd] = dv;
+            if (vp) {
+                Pl[l] = pw;
+                Pl[3 + l] = 1.0 / pw;
+            }
+            __syncthreads();
+            const double iv = ggp::tau_body(S, cd, Xl, Dl, Pl);
+            if (vi) Il[ji] = iv;
+            __syncthreads();
+            ggp::Step SR;
+            ggp::load_step(SR, Sb, s_ou);
+            if (wave == 0) {
+                ggp::outputs<0>(SR, Il, Xl, m, C);
+            } else {
+                double m1[4], C1[16];
+                ggp::outputs<1>(SR, Il, Xl, m1, C1);
+                if (l == 0) {
+                    Ex[0] = C1[5]; Ex[1] = C1[7]; Ex[2] = C1[11]; Ex[3] = C1[15];
+                }
+            }
+            __syncthreads();   // also: every read of this step's LDS slots is done
+            if (wave == 0) {
+                C[5] = Ex[0]; C[7] = Ex[1]; C[13] = Ex[1]; C[11] = Ex[2]; C[14] = Ex[2]; C[15] = Ex[3];
+                if (divide) {
+                    ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                    divide = false;
+                }
+            }
+        }
+        if (wave == 0) {
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
+            ggp_innov v;
+            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+            cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
+            if (cl != cl) {
+                nan_row = (int)(r - r0);
+                live = false;
+            } else {
+                ggp_posterior(m, C, x0, x1, v);
+                pending = r + 1 < r1;
+                if (pending) dt = t_next - t_cur;
+                t_cur = t_next;
+                ++r;
+                live = r < r1;
+            }
+        }
+    }
+    if (tid == 0) {
+        double *st = state + (size_t)20 * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[k] = m[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+        cell_ll[c] = cl;
+        cell_nan[c] = nan_row;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // -p smoother kernels (lane schedule).  Parameters per row come from the segment table.
 // ------------------------------------------------------------------------------------------
 GGP_DEV const double *seg_params(const DevForest &F, const double *ptab, int n_seg, int64_t r)
@@ -583,6 +722,7 @@ struct ggp_forest {
     int kernel_pref = GGP_KERNEL_AUTO;
     int64_t group_max_cells = 2048;   // auto: group schedule for levels up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
+    int group_waves = 1;                          // 2: k_loglik_group2 where one cell per SIMD fits
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -639,6 +779,12 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             if (f->kernel_pref == GGP_KERNEL_AUTO) cpw = std::min(cpw, 2);
             if (f->tune_group_cpw > 0) cpw = f->tune_group_cpw;
             const int blocks = (n + cpw - 1) / cpw;
+            if (cpw == 1 && f->group_waves == 2) {
+                hipLaunchKernelGGL(k_loglik_group2, dim3(n), dim3(128), 0, f->stream, f->F, P,
+                                   f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan);
+                f->kernel_used = GGP_KERNEL_GROUP;
+                f->last_code = GGP_KERNEL_GROUP << 8 | 128;
+            } else {
             switch (cpw) {
             case 1: hipLaunchKernelGGL(k_loglik_group<64>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
                                        f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
@@ -651,6 +797,7 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             }
             f->kernel_used = GGP_KERNEL_GROUP;
             f->last_code = GGP_KERNEL_GROUP << 8 | (64 / cpw);
+            }
         } else {
             const int cpw = lane_cpw(f);
             const int blocks = (n + cpw - 1) / cpw;
@@ -789,6 +936,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
         f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_GROUP_WAVES")) f->group_waves = atoi(e) == 2 ? 2 : 1;
     int rc = GGP_OK;
     auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
     check(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? GGP_OK : GGP_EDEV);

@@ -436,7 +436,10 @@ GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const P
 }
 
 // ---- the outputs: new mean and covariance (mean_cov_model.h:73-208) -------------------
-template <class IA, class XA>
+// PART = -1 computes everything.  PART 0 / 1 compute the new mean plus one half of the
+// covariance (0: xx xg xl xq gl ll, 1: gg gq lq qq) for the two-wave group schedule, which
+// exchanges the halves through LDS; every expression is the same in all three forms.
+template <int PART = -1, class IA, class XA>
 GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
 {
     const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
@@ -461,7 +464,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     nm[3] = mq + (bq - mq) * egq;
 
     double nxg = 0, nxl = 0, nxq = 0, ngl = 0, nxx = 0, nll = 0, ngq = 0, ngg = 0, nlq = 0, nqq = 0;
-    {
+    if constexpr (PART != 1) {
     // cov_xg (mean_cov_model.h:97-115)
     nxg =
         rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + rdiv(bg * bl, ebt_gl, r_ebt_gl)
@@ -507,7 +510,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
           + S.k_xx * (2 * gl * t - 3 + 4 * egl - (egl * egl));
     nll = Cll * (egl * egl) + S.k_ll * (1 - (egl * egl));
     }
-    {
+    if constexpr (PART != 0) {
     // cov_gq (mean_cov_model.h:183-196)
     ngq =
         rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)
@@ -569,10 +572,13 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
 #undef DGL
 #undef DGQ
     m[0] = nm[0]; m[1] = nm[1]; m[2] = nm[2]; m[3] = nm[3];
-    C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
-    C[4] = nxg;  C[5] = ngg;  C[6] = ngl;  C[7] = ngq;
-    C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[11] = nlq;
-    C[12] = nxq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
+    if constexpr (PART != 1) {
+        C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
+        C[4] = nxg;  C[6] = ngl;  C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[12] = nxq;
+    }
+    if constexpr (PART != 0) {
+        C[5] = ngg;  C[7] = ngq;  C[11] = nlq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
+    }
 }
 
 // ---- lane schedule: one lane runs every task of its own cell; the task descriptors are

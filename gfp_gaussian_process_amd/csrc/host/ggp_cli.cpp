@@ -1,0 +1,697 @@
+// ggp_cli.cpp -- the command-line surface of the reference (src/main.cpp) over the MI355X
+// engine: same flags, defaults, checks, output files and formats; the likelihood and the
+// smoother run on the GPU through include/ggp.h, ingest through include/ggp_host.h.
+//
+//   -m  run_minimization      main.cpp:23-77    (minimize_wrapper[_log_params], error bars,
+//                                                final csv, generated parameter file)
+//   -s  run_bound_1dscan      main.cpp:80-114
+//   -p  run_prediction_segments main.cpp:117-146 (write_predictions_to_file)
+//   -e  additive: one total log-likelihood at the parameter files' values
+//   -j  joints (correlation_tree.h) are not built in this version: the flag is rejected.
+//
+// Output text is produced with the same iostream manipulators as the reference, so the files
+// are byte-identical given identical numbers.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <filesystem>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <map>
+#include <numeric>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ggp.h"
+#include "ggp_host.h"
+#include "ggp_nelder_mead.h"
+
+namespace {
+
+std::ofstream g_log;        // _file_log
+std::ofstream g_iter;       // _file_iteration
+int g_iteration = 0;        // _iteration
+int g_print_level = 0;      // _print_level
+bool g_save_ll = false;     // _save_ll
+
+// ---- utils.h ------------------------------------------------------------------------------
+std::vector<std::string> split_string_at(std::string s, const std::string &delimiter = ",")
+{
+    std::vector<std::string> out;
+    size_t pos;
+    while ((pos = s.find(delimiter)) != std::string::npos) {
+        out.push_back(s.substr(0, pos));
+        s.erase(0, pos + delimiter.length());
+    }
+    out.push_back(s);
+    return out;
+}
+
+std::string trim(const std::string &str, char trim_char = ' ')
+{
+    const size_t first = str.find_first_not_of(trim_char);
+    if (first == std::string::npos) return str;
+    const size_t last = str.find_last_not_of(' ');
+    return str.substr(first, last - first + 1);
+}
+
+std::string pad_str(std::string s, size_t num)
+{
+    if (num > s.size()) s.insert(s.end(), num - s.size(), ' ');
+    return s;
+}
+
+std::string pad_str(double d, size_t num)
+{
+    std::stringstream b;
+    b << d;
+    return pad_str(b.str(), num);
+}
+
+std::string file_base(const std::string &infile)
+{
+    const auto parts = split_string_at(infile, "/");
+    const auto base = split_string_at(parts.back(), ".");
+    std::string out;
+    for (size_t i = 0; i + 1 < base.size(); ++i) {
+        if (i > 0) out += '.';
+        out += base[i];
+    }
+    return out;
+}
+
+std::string default_out_dir(const std::string &infile)
+{
+    const auto parts = split_string_at(infile, "/");
+    const auto base = split_string_at(parts.back(), ".");
+    std::string out;
+    for (size_t i = 0; i + 1 < parts.size(); ++i) out += parts[i] + "/";
+    for (size_t i = 0; i + 1 < base.size(); ++i) {
+        if (i > 0) out += '.';
+        out += base[i];
+    }
+    return out + "_out/";
+}
+
+std::string out_dir(std::map<std::string, std::string> &args)
+{
+    std::string d;
+    if (!args.count("outdir")) {
+        d = default_out_dir(args["infile"]);
+    } else {
+        d = args["outdir"];
+        if (d.back() != '/') d += "/";
+    }
+    std::filesystem::create_directory(d);
+    return d;
+}
+
+std::string add_segment_to_filename(const std::string &name, int segment)
+{
+    return segment == -1 ? name : name + "_segment" + std::to_string(segment);
+}
+
+template <typename T>
+std::vector<T> arange(T start, T stop, T step)
+{
+    std::vector<T> v;
+    for (T x = start; x < stop; x += step) v.push_back(x);
+    return v;
+}
+
+// ---- Parameters.h -------------------------------------------------------------------------
+struct Params {
+    ggp_param_set p{};
+    double final_[GGP_N_PARAMS] = {};
+    bool minimized[GGP_N_PARAMS] = {};
+    bool fixed(int i) const { return p.kind[i] == 0; }
+    bool free_(int i) const { return p.kind[i] == 1; }
+    bool bound(int i) const { return p.kind[i] == 2; }
+    std::string name(int i) const { return p.name[i]; }
+    bool has_nonfixed() const
+    {
+        for (int i = 0; i < GGP_N_PARAMS; ++i)
+            if (!fixed(i)) return true;
+        return false;
+    }
+    std::vector<double> get_final() const
+    {
+        std::vector<double> v(GGP_N_PARAMS);
+        for (int i = 0; i < GGP_N_PARAMS; ++i) v[i] = minimized[i] ? final_[i] : p.init[i];
+        return v;
+    }
+    void set_final(const std::vector<double> &v)
+    {
+        for (int i = 0; i < GGP_N_PARAMS; ++i) {
+            final_[i] = v[i];
+            minimized[i] = true;
+        }
+    }
+    std::vector<int> non_fixed() const
+    {
+        std::vector<int> idx;
+        for (int i = 0; i < GGP_N_PARAMS; ++i)
+            if (!fixed(i)) idx.push_back(i);
+        return idx;
+    }
+    void to_csv(std::ostream &file) const   // Parameter_set::to_csv (Parameters.h:201-224)
+    {
+        file << "no,name,type,init,step,lower_bound,upper_bound,final\n";
+        for (int i = 0; i < GGP_N_PARAMS; ++i) {
+            file << i << ",";
+            if (fixed(i)) {
+                file << name(i) << "," << "fixed" << "," << p.init[i] << ", , , ,";
+            } else if (bound(i)) {
+                file << name(i) << "," << "bound" << "," << p.init[i] << "," << p.step[i] << "," << p.lower[i] << ","
+                     << p.upper[i] << ",";
+            } else {
+                file << name(i) << "," << "free" << "," << p.init[i] << "," << p.step[i] << ", , ,";
+            }
+            if (minimized[i]) file << final_[i];
+            file << "\n";
+        }
+    }
+    void to_csv(const std::string &outfile, std::ios_base::openmode mode = std::ios_base::out) const
+    {
+        std::ofstream f(outfile, mode);
+        to_csv(f);
+    }
+};
+
+std::ostream &operator<<(std::ostream &os, const Params &P)   // Parameters.h:300-334
+{
+    const std::vector<int> w{4, 15, 8, 20, 20, 15, 15};
+    os << pad_str("No", w[0]) << pad_str("Name", w[1]) << pad_str("Type", w[2]) << pad_str("Init", w[3])
+       << pad_str("Step", w[4]) << pad_str("Bounds", w[5]) << "\n";
+    for (int i = 0; i < std::accumulate(w.begin(), w.end(), 0); ++i) os << "_";
+    os << "\n";
+    for (int i = 0; i < GGP_N_PARAMS; ++i) {
+        os << pad_str(std::to_string(i) + ":", w[0]);
+        if (P.fixed(i)) {
+            os << pad_str(P.name(i), w[1]) << pad_str("(fixed)", w[2]) << pad_str(P.p.init[i], w[3])
+               << pad_str("", w[4] + w[5] + w[6]);
+        } else if (P.bound(i)) {
+            os << pad_str(P.name(i), w[1]) << pad_str("(bound)", w[2]) << pad_str(P.p.init[i], w[3])
+               << pad_str(P.p.step[i], w[4]) << pad_str(P.p.lower[i], w[5]) << pad_str(P.p.upper[i], w[6]);
+        } else {
+            os << pad_str(P.name(i), w[1]) << pad_str("(free)", w[2]) << pad_str(P.p.init[i], w[3])
+               << pad_str(P.p.step[i], w[4]) << pad_str("", w[5] + w[6]);
+        }
+        if (P.minimized[i] && !P.fixed(i)) os << " -> " << P.final_[i];
+        os << "\n";
+    }
+    return os;
+}
+
+std::string outfile_param_code(const Params &P)   // predictions.h:505-520
+{
+    std::string code = "_f";
+    for (int i = 0; i < GGP_N_PARAMS; ++i)
+        if (!P.bound(i) && !P.fixed(i)) code += std::to_string(i);
+    code += "_b";
+    for (int i = 0; i < GGP_N_PARAMS; ++i)
+        if (P.bound(i)) code += std::to_string(i);
+    return code;
+}
+
+// ---- the objective on the GPU (likelihood.h:125-174) --------------------------------------
+struct Objective {
+    ggp_forest *forest = nullptr;
+    ggp_host_forest *host = nullptr;
+    const ggp_forest_desc *desc = nullptr;
+};
+
+void log_iteration(const std::vector<double> &p, double tl, int iteration)
+{
+    g_iter << iteration << ",";
+    for (double v : p) g_iter << std::setprecision(20) << v << ",";
+    g_iter << std::setprecision(30) << tl << std::setprecision(15) << "\n";
+}
+
+// +ll; throws std::domain_error("Likelihood is Nan") after the reference's side effects
+double total_likelihood(const std::vector<double> &params, Objective &o)
+{
+    double ll = 0;
+    int64_t nc = -1, nr = -1;
+    const int rc = ggp_total_loglik(o.forest, params.data(), &ll, &nc, &nr);
+    if (rc == GGP_ENAN) {
+        if (g_save_ll) log_iteration(params, ll, g_iteration + 1);
+        g_log << "\n(sc_likelihood) ERROR: Log likelihood is Nan\n";
+        g_log << "____________________________________________\n";
+        if (nc >= 0) {
+            const double t = o.desc->time[o.desc->row_offset[nc] + nr];
+            g_log << "cell_id: " << ggp_host_forest_cell_id(o.host, nc) << ", at time " << t << "\n";
+        }
+        g_log << g_iteration + 1 << ": ";
+        for (double v : params) g_log << v << ", ";
+        g_log << "ll=" << std::setprecision(10) << ll << "\n";
+        g_iter.close();
+        throw std::domain_error("Likelihood is Nan");
+    }
+    if (rc != GGP_OK) throw std::runtime_error(std::string("GPU likelihood failed: ") + ggp_strerror(rc));
+    ++g_iteration;
+    if (g_save_ll) log_iteration(params, ll, g_iteration);
+    if (g_print_level > 0) {
+        std::cout << g_iteration << ": ";
+        for (double v : params) std::cout << std::setprecision(20) << v << ", ";
+        std::cout << "ll=" << std::setprecision(30) << ll << std::setprecision(15) << "\n";
+    }
+    return ll;
+}
+
+struct Forest {
+    ggp_host_forest *host = nullptr;
+    ggp_forest_desc desc{};
+    ggp_forest *gpu = nullptr;
+    ~Forest()
+    {
+        if (gpu) ggp_forest_destroy(gpu);
+        if (host) ggp_host_forest_free(host);
+    }
+};
+
+void build_forest(Forest &F, const ggp_dataset *d, int segment, const std::string &noise, const std::string &div)
+{
+    if (ggp_forest_build(d, segment, noise == "scaled", div == "binomial", &F.host) != GGP_OK)
+        throw std::invalid_argument(ggp_host_last_error());
+    ggp_host_forest_desc(F.host, &F.desc);
+    F.desc.device = 0;
+    F.desc.kernel = GGP_KERNEL_AUTO;
+    const int rc = ggp_forest_create(&F.desc, &F.gpu);
+    if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_forest_create: ") + ggp_strerror(rc));
+}
+
+// ---- -m (minimizer_nlopt.h, likelihood.h:211-350) ------------------------------------------
+double minimize(Objective &o, Params &P, double tolerance, bool log_space)
+{
+    const int n = GGP_N_PARAMS;
+    std::vector<double> lb(n), ub(n), step(n), x(n);
+    for (int i = 0; i < n; ++i) {
+        const double start = P.minimized[i] ? P.final_[i] : P.p.init[i];
+        x[i] = log_space ? std::log(start) : start;
+        if (P.fixed(i)) {
+            step[i] = 1.;
+            lb[i] = ub[i] = log_space ? std::log(P.p.init[i]) : P.p.init[i];
+        } else {
+            step[i] = log_space ? std::log(1. + P.p.step[i] / P.p.init[i]) : P.p.step[i];
+            lb[i] = log_space ? std::log(P.p.lower[i]) : P.p.lower[i];
+            ub[i] = log_space ? std::log(P.p.upper[i]) : P.p.upper[i];
+        }
+    }
+    g_save_ll = true;
+    g_log << "Optimization algorithm: Nelder-Mead simplex algorithm (local, no-derivative) Tolerance: " << tolerance
+          << "\n";
+    g_iteration = 0;
+    std::vector<double> pv(n);
+    const ggp_nm::Objective f = [&](const double *xx, double *v) {
+        for (int i = 0; i < n; ++i) pv[i] = log_space ? std::exp(xx[i]) : xx[i];
+        *v = -total_likelihood(pv, o);   // throws on NaN, unwinding the optimiser
+        return true;
+    };
+    double minf = 0;
+    ggp_nm::Stats st;
+    ggp_nm::Result r;
+    try {
+        r = ggp_nm::minimize(n, f, lb.data(), ub.data(), x.data(), step.data(), tolerance, 0, &minf, st);
+    } catch (std::exception &e) {
+        g_log << "(minimize_wrapper) ERROR: Log likelihood optimization failed (" << e.what() << ")" << std::endl;
+        throw;
+    }
+    if (r == ggp_nm::INVALID_ARGS) throw std::invalid_argument("nlopt invalid argument");
+    if (r == ggp_nm::FAILURE) throw std::runtime_error("nlopt failure");
+    g_save_ll = false;
+    g_log << "Found maximum: log likelihood = " << std::setprecision(20) << -minf << std::setprecision(10) << "\n";
+    if (log_space)
+        for (int i = 0; i < n; ++i) x[i] = std::exp(x[i]);
+    P.set_final(x);
+    g_log << P << std::endl;
+    return -minf;
+}
+
+std::vector<double> ll_error_bars(Params &P, Objective &o, double epsilon)
+{
+    const std::vector<double> x = P.get_final();
+    const std::vector<int> idx = P.non_fixed();
+    const int k = (int)idx.size();
+    std::vector<int32_t> idx32(idx.begin(), idx.end());
+    std::vector<double> H((size_t)k * k), Hi((size_t)k * k);
+    struct Ctx { Objective *o; } ctx{&o};
+    auto cb = [](const double *xx, double *v, void *data) -> int {
+        auto *c = static_cast<Ctx *>(data);
+        *v = total_likelihood(std::vector<double>(xx, xx + GGP_N_PARAMS), *c->o);
+        return 0;
+    };
+    if (ggp_num_hessian(GGP_N_PARAMS, cb, &ctx, x.data(), idx32.data(), k, epsilon, H.data()) != GGP_OK)
+        throw std::runtime_error(ggp_host_last_error());
+    ggp_inverse_pplu(k, H.data(), Hi.data());
+    std::vector<double> err;
+    for (int i = 0; i < k; ++i) err.push_back(-Hi[(size_t)i * k + i]);
+    return err;
+}
+
+void run_minimization(Objective &o, Params &P, std::map<std::string, std::string> &args, int segment, long n_rows)
+{
+    g_log << "-> Minimizaton" << "\n";
+    const std::string base = out_dir(args) + add_segment_to_filename(file_base(args["infile"]), segment) +
+                             outfile_param_code(P);
+    const std::string outfile_ll = base + "_iterations.csv";
+    g_iter = std::ofstream(outfile_ll, std::ios_base::app);
+    {   // setup_outfile_likelihood (likelihood.h:290-299)
+        P.to_csv(outfile_ll);
+        std::ofstream file(outfile_ll, std::ios_base::app);
+        file << "\nlog_likelihoods:\niteration,";
+        for (int i = 0; i < GGP_N_PARAMS; ++i) file << P.name(i) << ",";
+        file << "log_likelihood" << "\n";
+    }
+    g_log << "Outfile: " << outfile_ll << "\n";
+    const double tol = std::stod(args["tolerance_maximization"]);
+    const double ll_max = minimize(o, P, tol, args["search_space"] == "log");
+    g_iter.close();
+
+    g_log << "-> Error estimation" << "\n";
+    const std::string outfile_estim = base + "_final.csv";
+    g_log << "Outfile: " << outfile_estim << "\n";
+    P.to_csv(outfile_estim);
+    {   // save_error_bars (likelihood.h:341-368)
+        std::ofstream file(outfile_estim, std::ios_base::app);
+        file << "\nerrors^2:";
+        file << "\nepsilon";
+        const std::vector<double> eps{5e-2, 1e-2, 5e-3};
+        for (int i : P.non_fixed()) file << "," << P.name(i);
+        file << "\n";
+        for (double e : eps) {
+            const std::vector<double> error = ll_error_bars(P, o, e);
+            file << e;
+            for (double v : error) file << "," << v;
+            file << "\n";
+        }
+    }
+    {   // save_final_likelihood (likelihood.h:316-339)
+        std::ofstream file(outfile_estim, std::ios_base::app);
+        file << "\n";
+        file << "n_data_points, " << n_rows << "\n";
+        file << "total_log_likelihoood," << std::setprecision(15) << ll_max << "\n";
+        file << "norm_log_likelihoood," << std::setprecision(15) << ll_max / n_rows << "\n";
+        file << "optimization_algorithm," << "LN_NELDERMEAD" << "\n";
+        file << "tolerance," << tol << "\n";
+        file << "search_space," << args["search_space"] << "\n";
+        file << "noise_model," << args["noise_model"] << "\n";
+        file << "cell_division_model," << args["cell_division_model"] << "\n";
+        file << "version," << "0.4.2" << "\n";
+    }
+    {   // create_parameter_file (likelihood.h:371-377)
+        std::ofstream file(base + "_parameter_file.txt");
+        file << "# Generated parameter file with the final parameters that may be used for predictions\n";
+        for (int i = 0; i < GGP_N_PARAMS; ++i) file << P.name(i) << " = " << P.final_[i] << "\n";
+    }
+}
+
+// ---- -s (main.cpp:80-114) ------------------------------------------------------------------
+void run_bound_1dscan(Objective &o, const Params &P, std::map<std::string, std::string> &args, int segment)
+{
+    g_log << "-> 1d Scan" << "\n";
+    g_save_ll = true;
+    for (int i = 0; i < GGP_N_PARAMS; ++i) {
+        if (!P.bound(i)) continue;
+        std::vector<double> pv = P.get_final();
+        const std::string outfile = out_dir(args) + add_segment_to_filename(file_base(args["infile"]), segment) +
+                                    "_scan_" + P.name(i) + ".csv";
+        g_iter = std::ofstream(outfile, std::ios_base::app);
+        {
+            P.to_csv(outfile);
+            std::ofstream file(outfile, std::ios_base::app);
+            file << "\nlog_likelihoods:\niteration,";
+            for (int k = 0; k < GGP_N_PARAMS; ++k) file << P.name(k) << ",";
+            file << "log_likelihood" << "\n";
+        }
+        g_log << "Outfile: " << outfile << "\n";
+        for (double v : arange<double>(P.p.lower[i], P.p.upper[i], P.p.step[i])) {
+            pv[i] = v;
+            total_likelihood(pv, o);
+        }
+    }
+    g_save_ll = false;
+}
+
+// ---- -p (main.cpp:117-146, predictions.h:522-601) -----------------------------------------
+void output_upper_triangle(std::ostream &file, const double *C)
+{
+    for (int m = 0; m < 4; ++m)
+        for (int n = 0; n < 4; ++n)
+            if (m <= n) {
+                if (n + m > 0) file << ",";
+                file << C[4 * m + n];
+            }
+}
+
+void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::string, std::string> &args)
+{
+    g_log << "-> prediction" << "\n";
+    std::string outfile = out_dir(args) + file_base(args["infile"]);
+    for (const Params &P : plist) outfile += outfile_param_code(P);
+    outfile += "_prediction.csv";
+    Forest F;
+    build_forest(F, d, -1, args["noise_model"], args["cell_division_model"]);
+    std::vector<double> pv;
+    for (const Params &P : plist) {
+        const auto v = P.get_final();
+        pv.insert(pv.end(), v.begin(), v.end());
+    }
+    const int64_t nr = F.desc.n_rows, nc = F.desc.n_cells;
+    std::vector<double> comb((size_t)nr * 20);
+    const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, comb.data());
+    if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
+    g_log << "Outfile: " << outfile << "\n";
+    for (size_t i = 0; i < plist.size(); ++i) {
+        if (i == 0)
+            plist[i].to_csv(outfile);
+        else
+            plist[i].to_csv(outfile, std::ios_base::app);
+    }
+    std::ofstream file(outfile, std::ios_base::app);
+    file << "\ncell_id,parent_id,time,log_length,fp,";
+    file << "mean_x,mean_g,mean_l,mean_q," << "cov_xx,cov_xg,cov_xl,cov_xq," << "cov_gg,cov_gl,cov_gq,"
+         << "cov_ll,cov_lq," << "cov_qq\n";
+    for (int64_t c = 0; c < nc; ++c) {
+        for (int64_t r = F.desc.row_offset[c]; r < F.desc.row_offset[c + 1]; ++r) {
+            file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
+                 << F.desc.time[r] << "," << F.desc.log_length[r] << "," << F.desc.fp[r] << ",";
+            const double *s = &comb[(size_t)r * 20];
+            for (int k = 0; k < 4; ++k) {
+                if (k > 0) file << ",";
+                file << s[k];
+            }
+            file << ",";
+            output_upper_triangle(file, s + 4);
+            file << "\n";
+        }
+    }
+}
+
+// ---- main.cpp:148-345 arg_parser ------------------------------------------------------------
+std::map<std::string, std::string> arg_parser(int argc, char **argv)
+{
+    const std::vector<std::vector<std::string>> keys = {
+        {"-h", "--help", "this help message"},
+        {"-i", "--infile", "(required) input data file"},
+        {"-b", "--parameter_bounds", "(required) file(s) setting the type, step, bounds of the parameters"},
+        {"-c", "--csv_config", "file that sets the columns that will be used from the input file"},
+        {"-l", "--print_level", "print level {0,1,2}, default: 0"},
+        {"-o", "--outdir", "specify output direction and do not use default"},
+        {"-t", "--tolerance_maximization", "absolute tolerance of maximization between optimization steps, default: 1e-10"},
+        {"-r", "--rel_tolerance_joints", "relative tolerance of joint calculation: default 1e-10"},
+        {"-space", "--search_space", "search parameter space in {'log'|'linear'} space, default: 'log'"},
+        {"-noise", "--noise_model", "measurement noise of fp content {'scaled'|'const'} default: 'scaled'"},
+        {"-div", "--cell_division_model", "cell divison model {'binomial'|'gauss'} default: 'binomial'"},
+        {"-m", "--maximize", "run maximization"},
+        {"-s", "--scan", "run 1d parameter scan"},
+        {"-p", "--predict", "run prediction"},
+        {"-j", "--joints", "run calculation of joint probabilities"},
+        {"-e", "--evaluate", "evaluate the total log likelihood once at the parameter files' values"},
+    };
+    std::map<std::string, std::string> a;
+    a["print_level"] = "0";
+    a["tolerance_maximization"] = "1e-10";
+    a["rel_tolerance_joints"] = "1e-10";
+    a["search_space"] = "log";
+    a["noise_model"] = "scaled";
+    a["cell_division_model"] = "binomial";
+    for (size_t k = 0; k < keys.size(); ++k) {
+        for (int i = 1; i < argc; ++i) {
+            const std::string arg = argv[i];
+            if (arg != keys[k][0] && arg != keys[k][1]) continue;
+            const std::string &key = keys[k][0];
+            auto next = [&]() -> std::string {
+                if (i + 1 >= argc) throw std::invalid_argument("Invalide argument");
+                return argv[i + 1];
+            };
+            if (key == "-i") a["infile"] = next();
+            else if (key == "-b") {
+                for (int j = i + 1; j < argc; ++j) {
+                    const std::string argj = argv[j];
+                    if (argj.rfind("-", 0) == 0) break;
+                    a["parameter_bounds"] += argj + " ";
+                }
+                a["parameter_bounds"] = trim(a["parameter_bounds"]);
+            } else if (key == "-c") a["csv_config"] = next();
+            else if (key == "-l") a["print_level"] = next();
+            else if (key == "-o") a["outdir"] = next();
+            else if (key == "-t") a["tolerance_maximization"] = next();
+            else if (key == "-r") a["rel_tolerance_joints"] = next();
+            else if (key == "-space") a["search_space"] = next();
+            else if (key == "-noise") a["noise_model"] = next();
+            else if (key == "-div") a["cell_division_model"] = next();
+            else if (key == "-m") a["minimize"] = "1";
+            else if (key == "-s") a["scan"] = "1";
+            else if (key == "-p") a["predict"] = "1";
+            else if (key == "-e") a["evaluate"] = "1";
+            else if (key == "-j") {
+                a["joints"] = "1";
+                a["predict"] = "1";
+            } else if (key == "-h") {
+                a["help"] = "1";
+                std::cout << "Usage: ./gfp_gaussian [-options]\n";
+                for (const auto &kk : keys) std::cout << pad_str(kk[0] + ", " + kk[1], 35) << kk[2] << "\n";
+            }
+        }
+    }
+    if (a.count("help")) return a;
+    if (a["search_space"] != "log" && a["search_space"] != "linear") {
+        std::cout << "(arg_parser) ERROR: search_space must be either 'log' or 'linear', not " << a["search_space"];
+        throw std::invalid_argument("Invalide argument");
+    }
+    if (a["noise_model"] != "const" && a["noise_model"] != "scaled") {
+        std::cout << "(arg_parser) ERROR: noise_model must be either 'const' or 'scaled', not " << a["noise_model"];
+        throw std::invalid_argument("Invalide argument");
+    }
+    if (a["cell_division_model"] != "gauss" && a["cell_division_model"] != "binomial") {
+        std::cout << "(arg_parser) ERROR: cell_division_model must be either 'gauss' or 'binomial', not "
+                  << a["cell_division_model"];
+        throw std::invalid_argument("Invalide argument");
+    }
+    if (!a.count("infile")) {
+        std::cout << "(arg_parser) ERROR: Required infile flag not set!\n";
+        throw std::invalid_argument("Invalide argument");
+    } else if (!std::filesystem::exists(a["infile"])) {
+        std::cout << "(arg_parser) ERROR: Infile " << a["infile"] << " not found (use '-h' for help)!" << std::endl;
+        throw std::invalid_argument("Invalide argument");
+    }
+    if (!a.count("parameter_bounds")) {
+        std::cout << "(arg_parser) ERROR: Required parameter_bounds flag not set!\n";
+        throw std::invalid_argument("Invalide argument");
+    }
+    for (const auto &pf : split_string_at(a["parameter_bounds"], " ")) {
+        if (!std::filesystem::exists(pf)) {
+            std::cout << "(arg_parser) ERROR: Paramters bound file '" << pf << "' not found (use '-h' for help)!"
+                      << std::endl;
+            throw std::invalid_argument("Invalide argument");
+        }
+    }
+    if (a.count("csv_config") && !std::filesystem::exists(a["csv_config"])) {
+        std::cout << "(arg_parser) ERROR: csv_config flag set, but csv configuration file " << a["csv_config"]
+                  << " not found!" << std::endl;
+        throw std::invalid_argument("Invalide argument");
+    }
+    return a;
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    std::string outfile_log, outfile_log_success, outfile_log_error;
+    std::cout << "Running... \n";
+    ggp_dataset *data = nullptr;
+    ggp_csv_config *cfg = nullptr;
+    try {
+        auto args = arg_parser(argc, argv);
+        g_print_level = std::stoi(args["print_level"]);
+        if (args.count("help")) return EXIT_SUCCESS;
+        const std::string base = out_dir(args) + file_base(args["infile"]);
+        outfile_log = base + ".log";
+        outfile_log_success = base + "_success.log";
+        outfile_log_error = base + "_error.log";
+
+        const auto param_files = split_string_at(args["parameter_bounds"], " ");
+        std::vector<Params> plist;
+        g_log = std::ofstream(outfile_log, std::ios_base::app);
+        std::cout << "Temporary log file '" << outfile_log << "' created\n";
+        for (const auto &pf : param_files) {
+            Params P;
+            if (ggp_param_file_load(pf.c_str(), 1, &P.p) != GGP_OK) {
+                g_log << ggp_host_last_error() << "\n";
+                throw std::invalid_argument("Invalide argument");
+            }
+            g_log << P << "\n";
+            plist.push_back(P);
+        }
+        if (args.count("joints"))
+            throw std::invalid_argument("-j (joint distributions) is not built in this version");
+
+        const char *cfg_path = args.count("csv_config") ? args["csv_config"].c_str() : "";
+        if (ggp_csv_config_load(cfg_path, &cfg) != GGP_OK) throw std::invalid_argument(ggp_host_last_error());
+        g_log << "-> Reading" << "\n";
+        if (ggp_dataset_read(args["infile"].c_str(), cfg, &data) != GGP_OK)
+            throw std::invalid_argument(ggp_host_last_error());
+        int32_t nseg = 0;
+        ggp_dataset_segments(data, nullptr, 0, &nseg);
+        std::vector<int32_t> seg(nseg);
+        ggp_dataset_segments(data, seg.data(), nseg, &nseg);
+        if ((size_t)nseg != param_files.size()) {
+            g_log << "(main) ERROR: There are " << nseg << " segments, but " << param_files.size()
+                  << " parameter files!\n";
+            throw std::invalid_argument("Invalide argument");
+        }
+        auto file_number = [&](int i) { return nseg > 1 ? i : -1; };
+
+        if (args.count("evaluate")) {
+            for (int i = 0; i < nseg; ++i) {
+                Forest F;
+                build_forest(F, data, seg[i], args["noise_model"], args["cell_division_model"]);
+                Objective o{F.gpu, F.host, &F.desc};
+                const double ll = total_likelihood(plist[i].get_final(), o);
+                std::cout << "segment " << seg[i] << ": total log likelihood = " << std::setprecision(17) << ll
+                          << " (" << F.desc.n_rows << " data points)\n";
+                g_log << "total log likelihood (segment " << seg[i] << ") = " << std::setprecision(17) << ll << "\n";
+            }
+        }
+        if (args.count("minimize")) {
+            for (int i = 0; i < nseg; ++i) {
+                if (!plist[i].has_nonfixed()) continue;
+                Forest F;
+                build_forest(F, data, seg[i], args["noise_model"], args["cell_division_model"]);
+                Objective o{F.gpu, F.host, &F.desc};
+                run_minimization(o, plist[i], args, file_number(i), (long)F.desc.n_rows);
+            }
+        }
+        if (args.count("scan")) {
+            for (int i = 0; i < nseg; ++i) {
+                Forest F;
+                build_forest(F, data, seg[i], args["noise_model"], args["cell_division_model"]);
+                Objective o{F.gpu, F.host, &F.desc};
+                run_bound_1dscan(o, plist[i], args, file_number(i));
+            }
+        }
+        if (args.count("predict")) run_prediction(data, plist, args);
+
+        g_log << "Done." << std::endl;
+        std::cout << "Done. Log file: " << outfile_log_success << std::endl;
+        std::rename(outfile_log.c_str(), outfile_log_success.c_str());
+        g_log.close();
+        ggp_dataset_free(data);
+        ggp_csv_config_free(cfg);
+        return EXIT_SUCCESS;
+    } catch (std::exception &e) {
+        if (!outfile_log.empty()) std::rename(outfile_log.c_str(), outfile_log_error.c_str());
+        g_log << "Quit because of an error: " << e.what() << "\n";
+        g_log.close();
+        std::cout << "Quit because of an error: " << e.what() << "\n";
+        std::cout << "Error log file: " << outfile_log_error << std::endl;
+        if (data) ggp_dataset_free(data);
+        if (cfg) ggp_csv_config_free(cfg);
+        return EXIT_FAILURE;
+    }
+}

@@ -1,6 +1,7 @@
 // ggp_host.cpp -- host-side forest ingest with the reference's data-model semantics.
 // See include/ggp_host.h for the function <-> reference mapping.
 #include "ggp_host.h"
+#include "ggp_nelder_mead.h"
 
 #include <algorithm>
 #include <cerrno>
@@ -685,5 +686,82 @@ extern "C" int ggp_synthetic_forest(int64_t n_trees, int64_t P, uint64_t seed, i
         mean_var(g1, f->leaf_mean[1], f->leaf_var[1]);
     }
     *out = f;
+    return GGP_OK;
+}
+
+// ---- -m numerics ----------------------------------------------------------------------------
+extern "C" int ggp_nldrmd_minimize(int32_t n, ggp_objective_fn f, void *data, const double *lb, const double *ub,
+                                   double *x, const double *dx, double ftol_abs, int64_t maxeval, double *minf,
+                                   int64_t *nevals)
+{
+    if (n < 0 || !f || !lb || !ub || !x || !dx || !minf) return ggp_nm::INVALID_ARGS;
+    ggp_nm::Stats st;
+    const ggp_nm::Objective obj = [&](const double *xx, double *v) { return f(xx, v, data) == 0; };
+    const ggp_nm::Result r = ggp_nm::minimize(n, obj, lb, ub, x, dx, ftol_abs, (long)maxeval, minf, st);
+    if (nevals) *nevals = st.nevals;
+    return r;
+}
+
+extern "C" int ggp_num_hessian(int32_t n, ggp_objective_fn f, void *data, const double *x, const int32_t *idx,
+                               int32_t k, double epsilon, double *out)
+{
+    if (n <= 0 || k < 0 || !f || !x || !idx || !out) return fail(GGP_EINVAL, "ggp_num_hessian: bad arguments");
+    std::vector<double> p(x, x + n), xx;
+    auto call = [&](const std::vector<double> &v, double &val) { return f(v.data(), &val, data) == 0; };
+    for (int32_t i = 0; i < k; ++i) {
+        const int ii = idx[i];
+        for (int32_t j = 0; j < k; ++j) {
+            const int jj = idx[j];
+            const double h1 = std::max(p[ii] * epsilon, 1e-12);
+            const double h2 = std::max(p[jj] * epsilon, 1e-12);
+            double lij, li_j, l_ij, l_i_j;
+            xx = p; xx[ii] = xx[ii] + h1; xx[jj] = xx[jj] + h2;
+            if (!call(xx, lij)) return fail(GGP_ENAN, "objective stopped");
+            xx = p; xx[ii] = xx[ii] + h1; xx[jj] = xx[jj] - h2;
+            if (!call(xx, li_j)) return fail(GGP_ENAN, "objective stopped");
+            xx = p; xx[ii] = xx[ii] - h1; xx[jj] = xx[jj] + h2;
+            if (!call(xx, l_ij)) return fail(GGP_ENAN, "objective stopped");
+            xx = p; xx[ii] = xx[ii] - h1; xx[jj] = xx[jj] - h2;
+            if (!call(xx, l_i_j)) return fail(GGP_ENAN, "objective stopped");
+            out[(size_t)i * k + j] = (lij - li_j - l_ij + l_i_j) / (4 * h1 * h2);
+        }
+    }
+    return GGP_OK;
+}
+
+extern "C" int ggp_inverse_pplu(int32_t k, const double *a, double *out)
+{
+    if (k < 0 || !a || !out) return fail(GGP_EINVAL, "ggp_inverse_pplu: bad arguments");
+    std::vector<double> lu(a, a + (size_t)k * k);
+    std::vector<int> perm(k);
+    for (int i = 0; i < k; ++i) perm[i] = i;
+    for (int c = 0; c < k; ++c) {
+        int piv = c;
+        double big = std::fabs(lu[(size_t)c * k + c]);
+        for (int r = c + 1; r < k; ++r) {
+            const double v = std::fabs(lu[(size_t)r * k + c]);
+            if (v > big) { big = v; piv = r; }
+        }
+        if (piv != c) {
+            for (int j = 0; j < k; ++j) std::swap(lu[(size_t)c * k + j], lu[(size_t)piv * k + j]);
+            std::swap(perm[c], perm[piv]);
+        }
+        if (big != 0.0) {
+            for (int r = c + 1; r < k; ++r) lu[(size_t)r * k + c] /= lu[(size_t)c * k + c];
+            for (int r = c + 1; r < k; ++r)
+                for (int j = c + 1; j < k; ++j) lu[(size_t)r * k + j] -= lu[(size_t)r * k + c] * lu[(size_t)c * k + j];
+        }
+    }
+    std::vector<double> y(k);
+    for (int col = 0; col < k; ++col) {
+        for (int i = 0; i < k; ++i) y[i] = perm[i] == col ? 1.0 : 0.0;
+        for (int i = 1; i < k; ++i)
+            for (int j = 0; j < i; ++j) y[i] -= lu[(size_t)i * k + j] * y[j];
+        for (int i = k - 1; i >= 0; --i) {
+            for (int j = i + 1; j < k; ++j) y[i] -= lu[(size_t)i * k + j] * y[j];
+            y[i] /= lu[(size_t)i * k + i];
+        }
+        for (int i = 0; i < k; ++i) out[(size_t)i * k + col] = y[i];
+    }
     return GGP_OK;
 }

@@ -285,7 +285,9 @@ class HostForest:
 def kernel_name(code: int) -> str:
     """the HIP kernel symbol behind a launch-profile code (include/ggp.h)"""
     kind, lanes = code >> 8, code & 0xFF
-    return "k_loglik_level" if kind == N.KERNELS["lane"] else f"k_loglik_group<{lanes}>"
+    if kind == N.KERNELS["lane"]:
+        return "k_loglik_level"
+    return "k_loglik_group2" if lanes == 128 else f"k_loglik_group<{lanes}>"
 
 
 class Forest:

@@ -1,0 +1,143 @@
+"""The -m / -s layer over an objective: the reference's minimizer_nlopt.h and the error bars
+of likelihood.h, with the numerics in libggp_host.so (include/ggp_host.h):
+
+  nldrmd_minimize        NLopt 2.7.1 LN_NELDERMEAD (restated, csrc/host/ggp_nelder_mead.h)
+  minimize_wrapper       minimize_wrapper / minimize_wrapper_log_params  minimizer_nlopt.h:10-215
+  num_hessian            num_hessian_ll                                    likelihood.h:211-258
+  inverse_pplu           Eigen MatrixXd::inverse (partial-pivot LU)
+  ll_error_bars          ll_error_bars                                     likelihood.h:260-268
+  bound_1dscan           run_bound_1dscan                                  main.cpp:80-114
+
+The objective is any callable params(11) -> +log-likelihood that raises LikelihoodIsNan on a
+NaN -- in the product a gfp_gaussian_process_amd.Forest (GPU); in CPU tests the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+
+from . import _native as N
+from .forest import ParameterSet
+
+# nlopt_result
+FAILURE, INVALID_ARGS, FORCED_STOP = -1, -2, -5
+SUCCESS, FTOL_REACHED, XTOL_REACHED, MAXEVAL_REACHED = 1, 3, 4, 5
+
+
+class _Stop(Exception):
+    pass
+
+
+def _callback(f, n, errors: list):
+    def cb(xp, vp, _data):
+        try:
+            vp[0] = float(f(np.ctypeslib.as_array(xp, shape=(n,)).copy()))
+            return 0
+        except BaseException as e:   # re-raised by the caller after the C side unwinds
+            errors.append(e)
+            return 1
+    return N.OBJECTIVE_FN(cb)
+
+
+def nldrmd_minimize(f, x0, lb, ub, dx, ftol_abs: float, maxeval: int = 0):
+    """minimise f over the box [lb, ub] (lb == ub: a fixed dimension); returns
+    (x_best, f_best, result_code, n_evaluations).  An exception raised by f stops the run
+    and propagates (the reference's NaN path)."""
+    x = np.ascontiguousarray(x0, np.float64).copy()
+    n = x.size
+    lb, ub, dx = (np.ascontiguousarray(v, np.float64) for v in (lb, ub, dx))
+    errors: list = []
+    cb = _callback(f, n, errors)
+    minf = ctypes.c_double()
+    nev = ctypes.c_int64()
+    dp = lambda a: a.ctypes.data_as(N.c_double_p)  # noqa: E731
+    rc = N.host().ggp_nldrmd_minimize(n, cb, None, dp(lb), dp(ub), dp(x), dp(dx), ftol_abs, maxeval,
+                                      ctypes.byref(minf), ctypes.byref(nev))
+    if errors:
+        raise errors[0]
+    return x, minf.value, rc, nev.value
+
+
+def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, search_space: str = "log",
+                     start=None):
+    """maximise objective(params) over the non-fixed parameters (minimizer_nlopt.h:10-215);
+    returns (final parameter vector, maximal log-likelihood, nlopt result)"""
+    log = search_space == "log"
+    init = np.asarray(params.init, np.float64)
+    start = init if start is None else np.asarray(start, np.float64)
+    lb, ub, dx, x = (np.zeros(11) for _ in range(4))
+    ln = (lambda v: float(np.log(np.float64(v)))) if log else float   # log(0) = -inf, as in C
+    with np.errstate(divide="ignore"):
+        for i, kind in enumerate(params.kind):
+            x[i] = ln(start[i])
+            if kind == "fixed":
+                dx[i] = 1.0
+                lb[i] = ub[i] = ln(init[i])
+            else:
+                dx[i] = math.log(1.0 + params.step[i] / init[i]) if log else params.step[i]
+                lb[i] = ln(params.lower[i])
+                ub[i] = ln(params.upper[i])
+    f = (lambda v: -objective(np.exp(v))) if log else (lambda v: -objective(v))
+    xb, minf, rc, _ = nldrmd_minimize(f, x, lb, ub, dx, tolerance)
+    if rc == INVALID_ARGS:
+        raise ValueError("nlopt invalid argument")
+    if rc == FAILURE:
+        raise RuntimeError("nlopt failure")
+    return (np.exp(xb) if log else xb), -minf, rc
+
+
+def num_hessian(objective, x, idx, epsilon: float) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float64)
+    idx32 = np.ascontiguousarray(idx, np.int32)
+    k = idx32.size
+    out = np.zeros((k, k))
+    errors: list = []
+    cb = _callback(objective, x.size, errors)
+    rc = N.host().ggp_num_hessian(x.size, cb, None, x.ctypes.data_as(N.c_double_p),
+                                  idx32.ctypes.data_as(N.c_int32_p), k, epsilon,
+                                  out.ctypes.data_as(N.c_double_p))
+    if errors:
+        raise errors[0]
+    if rc != N.GGP_OK:
+        raise RuntimeError("ggp_num_hessian failed")
+    return out
+
+
+def inverse_pplu(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, np.float64)
+    out = np.zeros_like(a)
+    N.host().ggp_inverse_pplu(a.shape[0], a.ctypes.data_as(N.c_double_p), out.ctypes.data_as(N.c_double_p))
+    return out
+
+
+def ll_error_bars(objective, x_final, params: ParameterSet, epsilon: float) -> np.ndarray:
+    """squared error bars -diag(H^-1) of the non-fixed parameters (likelihood.h:260-268)"""
+    h = num_hessian(objective, x_final, params.non_fixed(), epsilon)
+    return -np.diag(inverse_pplu(h))
+
+
+def arange(start: float, stop: float, step: float) -> list:
+    """utils.h arange: accumulate value += step (not start + i*step)"""
+    out, v = [], start
+    while v < stop:
+        out.append(v)
+        v += step
+    return out
+
+
+def bound_1dscan(objective, params: ParameterSet, final=None) -> dict:
+    """run_bound_1dscan (main.cpp:80-114): for every bound parameter, evaluate the objective
+    along arange(lower, upper, step) with the others at their final (else init) values.
+    Returns {name: [(value, log_likelihood), ...]} in evaluation order."""
+    base = np.asarray(params.init if final is None else final, np.float64)
+    out = {}
+    for i in params.bound():
+        pv = base.copy()
+        rows = []
+        for v in arange(params.lower[i], params.upper[i], params.step[i]):
+            pv[i] = v
+            rows.append((v, objective(pv.copy())))
+        out[params.names[i]] = rows
+    return out

@@ -81,6 +81,29 @@ int ggp_synthetic_forest(int64_t n_trees, int64_t rows_per_tree, uint64_t seed,
                          int64_t first_tree, int32_t noise_scaled, int32_t division_binomial,
                          ggp_host_forest **out);
 
+/* ---- -m / error-bar numerics (CPU; the objective is a callback) ------------------------
+ * The objective returns 0 and writes *value, or non-zero to stop the run (the reference's
+ * objective throws std::domain_error on a NaN likelihood, likelihood.h:71-93). */
+typedef int (*ggp_objective_fn)(const double *x, double *value, void *data);
+
+/* NLopt 2.7.1 LN_NELDERMEAD as minimizer_nlopt.h:112-215 configures it (bounds, initial
+ * step, ftol_abs; maxeval <= 0: none).  Returns the nlopt_result code (3 FTOL_REACHED,
+ * 4 XTOL_REACHED, 5 MAXEVAL_REACHED, -1 FAILURE, -2 INVALID_ARGS, -5 FORCED_STOP); x is
+ * the best point seen, *minf its value.  Restatement: csrc/host/ggp_nelder_mead.h. */
+int ggp_nldrmd_minimize(int32_t n, ggp_objective_fn f, void *data, const double *lb, const double *ub,
+                        double *x, const double *dx, double ftol_abs, int64_t maxeval, double *minf,
+                        int64_t *nevals);
+
+/* num_hessian_ll (likelihood.h:211-258): central 4-point differences over the parameters
+ * idx[0..k-1] of x, h_i = max(x_i * epsilon, 1e-12), evaluated in the reference's order
+ * (i, j, then ++ +- -+ --).  out: k*k row-major.  Returns 0, or the callback's stop. */
+int ggp_num_hessian(int32_t n, ggp_objective_fn f, void *data, const double *x, const int32_t *idx, int32_t k,
+                    double epsilon, double *out);
+
+/* Eigen 3.3 MatrixXd::inverse(): partial-pivot LU (first max |a|), solved against the
+ * identity.  a, out: k*k row-major. */
+int ggp_inverse_pplu(int32_t k, const double *a, double *out);
+
 #ifdef __cplusplus
 }
 #endif

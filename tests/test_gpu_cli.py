@@ -1,0 +1,139 @@
+"""The CLI (lib/ggp, the reference's main.cpp surface) on the GPU against the CPU oracle:
+-e, -s, -p and -m on the reference's example data set.
+
+Tolerances: log-likelihood values 1e-9 relative (the north-star bar); -p values are printed
+with 6 significant digits by the reference's writer, so they are compared after parsing at
+1e-4 normalised by the standard deviations (the smoother's own tolerance is 1e-5, see
+test_gpu_parity.py).  The -m trajectory is compared with the same Nelder-Mead restatement
+driven by the oracle objective.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+CLI = os.path.join(ROOT, "gfp_gaussian_process_amd", "lib", "ggp")
+NAMES = ["mean_lambda", "gamma_lambda", "var_lambda", "mean_q", "gamma_q", "var_q", "beta",
+         "var_x", "var_g", "var_dx", "var_dg"]
+INIT = [2.31E-03, 4.36E-02, 9.75E-08, 9.03E+01, 1.60E-02, 1.94E+01, 4.95E-04, 3.35E-04, 8.26E-01,
+        1.63E-04, 7.48E-01]
+
+
+def _param_file(path, spec):
+    """spec: {index: "init, step[, lower, upper]"}; every other parameter fixed at INIT"""
+    with open(path, "w") as f:
+        for i, n in enumerate(NAMES):
+            f.write(f"{n} = {spec.get(i, repr(INIT[i]))}\n")
+    return str(path)
+
+
+def _run(args, cwd):
+    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=600, cwd=cwd)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _ll_table(path):
+    lines = open(path).read().split("log_likelihoods:\n")[1].strip().splitlines()[1:]
+    return [[float(v) for v in ln.rstrip(",").split(",")] for ln in lines]
+
+
+@pytest.fixture(scope="module")
+def oracle_example(example_paths):
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.from_csv(example_paths["csv"], example_paths["config"], -1, "scaled", "binomial")
+    return hf
+
+
+def test_cli_evaluate_matches_oracle(tmp_path, example_paths, oracle_example):
+    from oracle import oracle as O
+    pf = _param_file(tmp_path / "p.txt", {})
+    out = _run(["-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-e", "-o", str(tmp_path / "o")],
+               tmp_path)
+    ll = float(out.split("total log likelihood = ")[1].split()[0])
+    ref = O.OracleForest(oracle_example.a).total_likelihood(INIT)[0]
+    assert abs(ll - ref) / abs(ref) < 1e-9
+    assert os.path.exists(tmp_path / "o" / "input_success.log")
+
+
+def test_cli_scan_chain_matches_oracle(tmp_path, example_paths, oracle_example):
+    """-s: one bound parameter, every sample on the carried state of the previous one"""
+    from oracle import oracle as O
+    pf = _param_file(tmp_path / "p.txt", {8: "8.26E-01, 2.0E-01, 4.0E-01, 1.3E+00"})
+    _run(["-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-s", "-o", str(tmp_path / "o")],
+         tmp_path)
+    rows = _ll_table(tmp_path / "o" / "input_scan_var_g.csv")
+    of = O.OracleForest(oracle_example.a)
+    from gfp_gaussian_process_amd.optimize import arange
+    samples = arange(0.4, 1.3, 0.2)
+    assert len(rows) == len(samples)
+    for k, (row, v) in enumerate(zip(rows, samples)):
+        assert row[0] == k + 1 and row[9] == v
+        p = list(INIT)
+        p[8] = v
+        ref = of.total_likelihood(p)[0]
+        assert abs(row[-1] - ref) / abs(ref) < 1e-9, (k, row[-1], ref)
+
+
+def test_cli_predict_matches_oracle(tmp_path, example_paths, oracle_example):
+    from oracle import oracle as O
+    pf = _param_file(tmp_path / "p.txt", {})
+    _run(["-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-p", "-o", str(tmp_path / "o")],
+         tmp_path)
+    text = open(tmp_path / "o" / "input_f_b_prediction.csv").read()
+    head, body = text.split("\ncell_id,parent_id,time,log_length,fp,")
+    assert head.startswith("no,name,type,init,step,lower_bound,upper_bound,final\n0,mean_lambda,fixed,0.00231, , , ,")
+    lines = body.strip().splitlines()[1:]
+    hf = oracle_example
+    assert len(lines) == hf.n_rows
+    _, _, comb = O.OracleForest(hf.a).predict(INIT)
+    got = np.array([[float(v) for v in ln.split(",")[5:]] for ln in lines])
+    iu = np.triu_indices(4)
+    ref_m = comb[:, :4]
+    ref_c = comb[:, 4:].reshape(-1, 4, 4)
+    sd = np.sqrt(np.abs(np.einsum("nii->ni", ref_c)))
+    em = np.max(np.abs(got[:, :4] - ref_m) / (np.abs(ref_m) + sd))
+    ec = np.max(np.abs(got[:, 4:] - ref_c[:, iu[0], iu[1]]) / (sd[:, iu[0]] * sd[:, iu[1]]))
+    assert em < 1e-4 and ec < 1e-4, (em, ec)
+    ids = [ln.split(",")[0] for ln in lines]
+    assert ids[0] == hf.ids[0] and ids[-1] == hf.ids[-1]
+
+
+def test_cli_minimize_matches_oracle_trajectory(tmp_path, example_paths, oracle_example):
+    """-m, log space, two free parameters: the GPU run's iteration log follows the same
+    Nelder-Mead steps as the restatement driven by the oracle objective"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as Opt
+    from oracle import oracle as O
+    pf = _param_file(tmp_path / "p.txt", {7: "3.35E-04, 3.35E-05", 8: "8.26E-01, 8.26E-02"})
+    _run(["-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-m", "-t", "1e-4",
+          "-o", str(tmp_path / "o")], tmp_path)
+    base = tmp_path / "o" / "input_f78_b"
+    rows = _ll_table(str(base) + "_iterations.csv")
+    of = O.OracleForest(oracle_example.a)
+    seen = []
+
+    def objective(p):
+        v = of.total_likelihood(p)[0]
+        seen.append((p.copy(), v))
+        return v
+
+    P = g.ParameterSet.load(pf)
+    x, ll, rc = Opt.minimize_wrapper(objective, P, tolerance=1e-4, search_space="log")
+    assert rc == Opt.FTOL_REACHED
+    n = min(len(rows), len(seen), 25)
+    assert n >= 10
+    for k in range(n):
+        assert np.allclose(rows[k][1:12], seen[k][0], rtol=1e-9), k
+        assert abs(rows[k][12] - seen[k][1]) / abs(seen[k][1]) < 1e-9, k
+    final = open(str(base) + "_final.csv").read()
+    assert "errors^2:\nepsilon,var_x,var_g\n" in final and "n_data_points, 22065" in final
+    assert "optimization_algorithm,LN_NELDERMEAD" in final
+    fl = float(final.split("total_log_likelihoood,")[1].split()[0])
+    assert abs(fl - ll) / abs(ll) < 1e-8
+    pfile = open(str(base) + "_parameter_file.txt").read()
+    assert pfile.startswith("# Generated parameter file")
