@@ -30,6 +30,7 @@
 #include "ggp_device.h"
 #include "ggp_prop.h"
 #include "ggp_predict.h"
+#include "ggp_joints.h"
 
 #define GGP_VERSION "ggp-mi355x 0.1.0 (reference gfp_gaussian_process 0.4.2)"
 
@@ -349,145 +350,6 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 
 
 // ------------------------------------------------------------------------------------------
-// GROUP2 schedule: one cell per 128-lane workgroup.  Wave 0 owns the cell (state, step block,
-// Kalman update); both waves share the exponential / Dawson / integral tasks and split the
-// outputs (ggp::outputs<0> / <1>), exchanging wave 1's half through LDS.  Nothing is
-// computed twice, so a level of at most one cell per SIMD gets two SIMDs' issue per cell.
-// Bitwise identical to the other schedules.
-// ------------------------------------------------------------------------------------------
-constexpr int kX2 = 37, kD2 = 7, kI2 = 23;   // per-wave task counts (exp, Dawson, integral)
-static_assert(2 * kX2 >= ggp::NXT && 2 * kD2 >= ggp::ND && 2 * kI2 >= ggp::NI, "task split");
-
-__global__ __launch_bounds__(128) void k_loglik_group2(DevForest F, ggp_params P,
-                                                       const int32_t *__restrict__ cells, int n,
-                                                       double *__restrict__ state,
-                                                       double *__restrict__ cell_ll,
-                                                       int32_t *__restrict__ cell_nan)
-{
-    __shared__ double lds[kSlot + 4];
-    __shared__ double s_ou[ggp::OU_N];
-    __shared__ double s_tab[kDawsonTab];
-    __shared__ int s_flag[4];                     // [iteration parity][live, prop]
-    const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
-    for (int k = tid; k < kDawsonTab; k += 128) s_tab[k] = ggp_dawson_coef[k];
-    double *Xl = lds;
-    double *Dl = Xl + ggp::NX;
-    double *Pl = Dl + ggp::ND;
-    double *Il = Pl + ggp::NPW;
-    double *Sb = Il + ggp::NI;
-    double *Ex = lds + kSlot;
-    const int je = wave * kX2 + l, jd = wave * kD2 + l, ji = wave * kI2 + l;
-    const bool ve = l < kX2 && je < ggp::NXT, vd = l < kD2 && jd < ggp::ND, vi = l < kI2 && ji < ggp::NI;
-    const bool vp = wave == 1 && l < 3;
-    const uint32_t xd = ggp::pack_x(ggp::kXT[ve ? je : 0]);
-    const uint32_t dd = ggp::pack_d(ggp::kDT[vd ? jd : 0]);
-    const ggp::ITask cd = ggp::kIT[vi ? ji : 0];
-    const double *p = P.p;
-    if (tid == 0) {
-        ggp::store_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]), s_ou);
-        Xl[ggp::X_ONE] = 1.0;
-    }
-    const int c = cells[blockIdx.x];
-    const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
-    int64_t r = r0;
-    double m[4] = {0, 0, 0, 0}, C[16] = {0};
-    double dt = 0.0, t_cur = 0.0, cl = 0.0;
-    bool pending = false, divide = false, live = true;
-    int nan_row = kNanNone;
-    if (wave == 0) {
-        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
-        divide = pending;
-        t_cur = F.time[r0];
-    }
-    __syncthreads();   // s_tab, s_ou
-    for (int it = 0;; ++it) {
-        double y_l = 0.0, y_f = 0.0, t_next = 0.0;
-        int *fl = s_flag + 2 * (it & 1);
-        if (wave == 0) {
-            if (live) {
-                y_l = F.logl[r];
-                y_f = F.fp[r];
-                if (r + 1 < r1) t_next = F.time[r + 1];
-            }
-            const bool prop = live && pending;
-            if (tid == 0) {
-                if (prop) {
-                    ggp::Step S;
-                    ggp::step_init(S, m, C, dt, ggp::load_ou(s_ou));
-                    ggp::store_step(S, Sb);
-                }
-                fl[0] = live;
-                fl[1] = prop;
-            }
-        }
-        __syncthreads();
-        if (!fl[0]) break;
-        if (fl[1]) {
-            const ggp::StepL S(Sb);
-            const double ev = ggp::exp_body(S, ggp::unpack_x(xd));
-            const double dv = ggp::dawson_body(S, ggp::unpack_d(dd), s_tab);
-            const double pw = ggp::pow_task(S, vp ? l : 0);
-            if (ve) Xl[je] = ev;
-            if (vd) Dl[jd] = dv;
-            if (vp) {
-                Pl[l] = pw;
-                Pl[3 + l] = 1.0 / pw;
-            }
-            __syncthreads();
-            const double iv = ggp::tau_body(S, cd, Xl, Dl, Pl);
-            if (vi) Il[ji] = iv;
-            __syncthreads();
-            ggp::Step SR;
-            ggp::load_step(SR, Sb, s_ou);
-            if (wave == 0) {
-                ggp::outputs<0>(SR, Il, Xl, m, C);
-            } else {
-                double m1[4], C1[16];
-                ggp::outputs<1>(SR, Il, Xl, m1, C1);
-                if (l == 0) {
-                    Ex[0] = C1[5]; Ex[1] = C1[7]; Ex[2] = C1[11]; Ex[3] = C1[15];
-                }
-            }
-            __syncthreads();   // also: every read of this step's LDS slots is done
-            if (wave == 0) {
-                C[5] = Ex[0]; C[7] = Ex[1]; C[13] = Ex[1]; C[11] = Ex[2]; C[14] = Ex[2]; C[15] = Ex[3];
-                if (divide) {
-                    ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
-                    divide = false;
-                }
-            }
-        }
-        if (wave == 0) {
-            const double x0 = y_l - m[0];
-            const double x1 = y_f - m[1];
-            ggp_innov v;
-            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
-            cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
-            if (cl != cl) {
-                nan_row = (int)(r - r0);
-                live = false;
-            } else {
-                ggp_posterior(m, C, x0, x1, v);
-                pending = r + 1 < r1;
-                if (pending) dt = t_next - t_cur;
-                t_cur = t_next;
-                ++r;
-                live = r < r1;
-            }
-        }
-    }
-    if (tid == 0) {
-        double *st = state + (size_t)20 * c;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st[k] = m[k];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-        cell_ll[c] = cl;
-        cell_nan[c] = nan_row;
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // -p smoother kernels (lane schedule).  Parameters per row come from the segment table.
 // ------------------------------------------------------------------------------------------
 GGP_DEV const double *seg_params(const DevForest &F, const double *ptab, int n_seg, int64_t r)
@@ -646,6 +508,212 @@ __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab
 }
 
 // ------------------------------------------------------------------------------------------
+// -j kernels (ggp_joints.h).  Per-row tables: back [20] = the backward factor over the prior,
+// cond [36] = a, F, A of the step conditional, start [72] = the start joint.
+// ------------------------------------------------------------------------------------------
+constexpr int kJBack = 20, kJCond = 36, kJStart = 72;
+
+GGP_DEV void load_g4(const double *src, ggp::G4 &g)
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g.m[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) g.C[k] = src[4 + k];
+}
+
+GGP_DEV void store_a4(double *dst, const ggp::A4 &g)
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = g.a[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        dst[4 + k] = g.F[k];
+        dst[20 + k] = g.A[k];
+    }
+}
+
+GGP_DEV ggp::A4 load_a4(const double *src)
+{
+    ggp::A4 g;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g.a[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        g.F[k] = src[4 + k];
+        g.A[k] = src[20 + k];
+    }
+    return g;
+}
+
+GGP_DEV void store_g8(double *dst, const ggp::G8 &g)
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[k] = g.m[k];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) dst[8 + k] = g.C[k];
+}
+
+GGP_DEV void load_g8(const double *src, ggp::G8 &g)
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g.m[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) g.C[k] = src[8 + k];
+}
+
+__global__ __launch_bounds__(64) void k_joint_rows(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                   const int32_t *__restrict__ row_cell, int64_t n_rows,
+                                                   const double *__restrict__ fwd, const double *__restrict__ bwd,
+                                                   double *__restrict__ back, double *__restrict__ cond,
+                                                   double *__restrict__ start)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+    if (r >= n_rows) return;
+    const int c = row_cell[r];
+    const int64_t r1 = F.row_off[c + 1];
+    const double *p = seg_params(F, ptab, n_seg, r);
+    const ggp::G4 bk = ggp::backward_over_prior(bwd + (size_t)20 * r, p);
+    store20(back + (size_t)kJBack * r, bk.m, bk.C);
+    const double *ft = fwd + (size_t)20 * r;
+    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    double m2[4], C2[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m2[k] = ft[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) C2[k] = ft[4 + k];
+    ggp::G8 j;
+    ggp::A4 cd;
+    if (r + 1 < r1) {
+        // consecutive_joint / consecutive_conditional (correlation_tree.h:285-356)
+        double K[16], Kt[16];
+        ggp::propagate_lane(m2, C2, F.time[r + 1] - F.time[r], ou, s_tab, K);
+        ggp::jt<4, 4>(K, Kt);
+        ggp::join8(m2, ft, C2, K, Kt, ft + 4, j);
+        ggp::G8 jc;
+        ggp::join8(ft, m2, ft + 4, Kt, K, C2, jc);
+        ggp::G4 mg;
+        ggp::A4 sc;
+        ggp::separate(jc, mg, sc);
+        cd = ggp::a_transform(sc);
+    } else if (F.d1[c] >= 0) {
+        // consecutive_{joint,conditional}_cell_division (correlation_tree.h:158-283)
+        const double dtd = F.time[F.row_off[F.d1[c]]] - F.time[r];
+        if (F.binomial) {
+            double mb[4], Cb[16], cross[16], crossT[16];
+            ggp::propagate_lane(m2, C2, dtd, ou, s_tab);
+            ggp::division_binomial_j(p, m2, C2, ft, mb, Cb, cross);
+            ggp::jt<4, 4>(cross, crossT);
+            ggp::join8(mb, ft, Cb, cross, crossT, ft + 4, j);
+            ggp::G8 jc;
+            ggp::join8(ft, mb, ft + 4, crossT, cross, Cb, jc);
+            ggp::G4 mg;
+            ggp::A4 sc;
+            ggp::separate(jc, mg, sc);
+            cd = ggp::a_transform(sc);
+        } else {
+            ggp::G4 mg;
+            load_g4(ft, mg);
+            const ggp::A4 dv = ggp::division_affine(p);
+            j = ggp::flip_xy(ggp::to_joint(mg, dv));
+            cd = ggp::a_transform(dv);
+        }
+    } else {
+        return;   // a leaf's last row starts no walk and is never stepped from
+    }
+    store_g8(start + (size_t)kJStart * r, j);
+    store_a4(cond + (size_t)kJCond * r, cd);
+}
+
+// One lane per start row.  emit == nullptr: count the joints into counts[i]; else write them
+// from out_off[i] on (start, target, mean[8], cov[64]).  stack: depth x (cell, joint) per lane.
+__global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                   const int32_t *__restrict__ row_cell,
+                                                   const double *__restrict__ bstate,
+                                                   const double *__restrict__ back, const double *__restrict__ cond,
+                                                   const double *__restrict__ start, double tol, int64_t r_lo,
+                                                   int64_t n_starts, int depth, double *__restrict__ stack_j,
+                                                   int32_t *__restrict__ stack_c, int64_t *__restrict__ counts,
+                                                   const int64_t *__restrict__ out_off, int64_t *__restrict__ out_idx,
+                                                   double *__restrict__ out_val)
+{
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= n_starts) return;
+    const int64_t r = r_lo + i;
+    int cur = row_cell[r];
+    const int64_t rows0 = F.row_off[cur + 1] - F.row_off[cur];
+    int64_t cn = r - F.row_off[cur];
+    bool at_div = false;
+    int64_t cnt = 0;
+    int64_t out = out_off ? out_off[i] : 0;
+    if (cn == rows0 - 1) {
+        if (F.d1[cur] < 0) {
+            if (!out_off) counts[i] = 0;
+            return;
+        }
+        at_div = true;
+    }
+    ggp::G8 J;
+    load_g8(start + (size_t)kJStart * r, J);
+    double *sj = stack_j + (size_t)i * depth * kJStart;
+    int32_t *sc = stack_c + (size_t)i * depth;
+    int sp = 0;
+    for (;;) {
+        bool stop = false;
+        if (!at_div) {
+            // calc_joint_distributions (correlation_tree.h:464-524)
+            const int64_t rr0 = F.row_off[cur], rows = F.row_off[cur + 1] - rr0;
+            const double mean1 = bstate[(size_t)20 * cur + 1];   // cell.mean(1) after -p
+            const bool has_d1 = F.d1[cur] >= 0;
+            for (int64_t m = 1; cn + m < rows; ++m) {
+                const int64_t rr = rr0 + cn + m;
+                const double *p = seg_params(F, ptab, n_seg, rr);
+                const double D[4] = {p[7], 0.0, 0.0, F.scaled ? p[8] * (mean1 + F.fp_auto) : p[8]};
+                ggp::include_measurement(J, D, F.logl[rr], F.fp[rr]);
+                ggp::G4 mg, bk;
+                ggp::A4 sep;
+                ggp::separate(J, mg, sep);
+                load_g4(back + (size_t)kJBack * rr, bk);
+                const ggp::G8 comb = ggp::to_joint(ggp::g_multiply(mg, bk), sep);
+                if (ggp::cross_small(comb, tol)) {
+                    stop = true;
+                    break;
+                }
+                if (out_off) {
+                    out_idx[2 * out] = r;
+                    out_idx[2 * out + 1] = rr;
+                    store_g8(out_val + (size_t)kJStart * out, comb);
+                    ++out;
+                }
+                ++cnt;
+                if (cn + m < rows - 1 || has_d1) J = ggp::next_joint(J, load_a4(cond + (size_t)kJCond * rr));
+            }
+        }
+        if (!stop && F.d1[cur] >= 0) {   // joint_distributions_recr: daughter1, then daughter2
+            if (F.d2[cur] >= 0 && sp < depth) {
+                sc[sp] = F.d2[cur];
+                store_g8(sj + (size_t)kJStart * sp, J);
+                ++sp;
+            }
+            cur = F.d1[cur];
+            cn = -1;
+            at_div = false;
+            continue;
+        }
+        if (sp == 0) break;
+        --sp;
+        cur = sc[sp];
+        load_g8(sj + (size_t)kJStart * sp, J);
+        cn = -1;
+        at_div = false;
+    }
+    if (!out_off) counts[i] = cnt;
+}
+
+// ------------------------------------------------------------------------------------------
 // Deterministic total: sum cell_ll in DFS pre-order (the reference's accumulation order at
 // cell granularity) with a fixed-shape tree; first NaN = min over (dfs rank, row).
 // ------------------------------------------------------------------------------------------
@@ -722,7 +790,6 @@ struct ggp_forest {
     int kernel_pref = GGP_KERNEL_AUTO;
     int64_t group_max_cells = 2048;   // auto: group schedule for levels up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
-    int group_waves = 1;                          // 2: k_loglik_group2 where one cell per SIMD fits
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -732,6 +799,7 @@ struct ggp_forest {
     int32_t *d_parent = nullptr, *d_d1 = nullptr, *d_d2 = nullptr, *d_seg = nullptr;
     int32_t *d_level_cells = nullptr, *d_dfs_order = nullptr;
     int32_t *d_prior_seg = nullptr;   // -p: segment of the stationary prior per row
+    int32_t *d_row_cell = nullptr;    // -j: cell of every row
     double *d_state = nullptr, *d_cell_ll = nullptr;
     int32_t *d_cell_nan = nullptr;
     double *d_out_ll = nullptr;
@@ -779,12 +847,6 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             if (f->kernel_pref == GGP_KERNEL_AUTO) cpw = std::min(cpw, 2);
             if (f->tune_group_cpw > 0) cpw = f->tune_group_cpw;
             const int blocks = (n + cpw - 1) / cpw;
-            if (cpw == 1 && f->group_waves == 2) {
-                hipLaunchKernelGGL(k_loglik_group2, dim3(n), dim3(128), 0, f->stream, f->F, P,
-                                   f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan);
-                f->kernel_used = GGP_KERNEL_GROUP;
-                f->last_code = GGP_KERNEL_GROUP << 8 | 128;
-            } else {
             switch (cpw) {
             case 1: hipLaunchKernelGGL(k_loglik_group<64>, dim3(blocks), dim3(64), 0, f->stream, f->F, P,
                                        f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
@@ -797,7 +859,6 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             }
             f->kernel_used = GGP_KERNEL_GROUP;
             f->last_code = GGP_KERNEL_GROUP << 8 | (64 / cpw);
-            }
         } else {
             const int cpw = lane_cpw(f);
             const int blocks = (n + cpw - 1) / cpw;
@@ -820,6 +881,34 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
     HIPCHK(hipMemcpyAsync(f->h_out_ll, f->d_out_ll, sizeof(double), hipMemcpyDeviceToHost, f->stream));
     HIPCHK(hipMemcpyAsync(f->h_out_nan, f->d_out_nan, sizeof(int64_t), hipMemcpyDeviceToHost, f->stream));
     return GGP_OK;
+}
+
+// forward then backward pass of the smoother (predictions.h:93-444) into device buffers; pstate
+// is left holding every cell's backward final state (MOMAdata::mean/cov after -p)
+static hipError_t run_smoother(ggp_forest *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd,
+                               double *d_bwd)
+{
+    const int n_levels = (int)f->level_start.size() - 1;
+    hipError_t e = hipMemsetAsync(d_pstate, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream);
+    for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
+        const int64_t a = f->level_start[L];
+        const int n = (int)(f->level_start[L + 1] - a);
+        if (n <= 0) continue;
+        const int cpw = lane_cpw(f);
+        hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                           f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        e = hipGetLastError();
+    }
+    for (int L = n_levels - 1; L >= 0 && e == hipSuccess; --L) {   // backward: leaves first
+        const int64_t a = f->level_start[L];
+        const int n = (int)(f->level_start[L + 1] - a);
+        if (n <= 0) continue;
+        const int cpw = lane_cpw(f);
+        hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                           f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
+        e = hipGetLastError();
+    }
+    return e;
 }
 
 extern "C" {
@@ -853,7 +942,7 @@ void ggp_forest_destroy(ggp_forest *f)
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
                     (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
-                    (void *)f->d_level_cells, (void *)f->d_dfs_order, (void *)f->d_prior_seg, (void *)f->d_state,
+                    (void *)f->d_level_cells, (void *)f->d_dfs_order, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
                     (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_out_ll,
                     (void *)f->d_out_nan})
         if (p) (void)hipFree(p);
@@ -936,7 +1025,6 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
         f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_GROUP_WAVES")) f->group_waves = atoi(e) == 2 ? 2 : 1;
     int rc = GGP_OK;
     auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
     check(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? GGP_OK : GGP_EDEV);
@@ -976,6 +1064,10 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
             }
         }
         check(dev_upload(&f->d_prior_seg, prior.data(), nr));
+        std::vector<int32_t> row_cell(nr);
+        for (int64_t c = 0; c < nc; ++c)
+            for (int64_t r = d->row_offset[c]; r < d->row_offset[c + 1]; ++r) row_cell[r] = (int32_t)c;
+        check(dev_upload(&f->d_row_cell, row_cell.data(), nr));
     }
     check(dev_upload<double>(&f->d_state, nullptr, (size_t)nc * 20));
     check(dev_upload<double>(&f->d_cell_ll, nullptr, nc));
@@ -1009,6 +1101,96 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
             f->ev_rows[L] += d->row_offset[c + 1] - d->row_offset[c];
         }
     *out = f;
+    return GGP_OK;
+}
+
+int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
+               int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+{
+    if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
+    const int64_t nc = f->n_cells, nr = f->n_rows;
+    if (r_lo < 0) r_lo = 0;
+    if (r_hi > nr) r_hi = nr;
+    *n_out = 0;
+    if (nc == 0 || r_hi <= r_lo) return GGP_OK;
+    HIPCHK(hipSetDevice(f->device));
+    HIPCHK(hipStreamSynchronize(f->stream));
+    std::vector<void *> bufs;
+    auto alloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return p;
+    };
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(f->stream);
+        for (void *p : bufs) (void)hipFree(p);
+    };
+    const int64_t ns = r_hi - r_lo;
+    const int depth = (int)f->level_start.size();   // generations below any start, plus one
+    auto *d_ptab = (double *)alloc((size_t)n_seg * 11 * sizeof(double));
+    auto *d_pstate = (double *)alloc((size_t)nc * 20 * sizeof(double));
+    auto *d_fwd = (double *)alloc((size_t)nr * 20 * sizeof(double));
+    auto *d_bwd = (double *)alloc((size_t)nr * 20 * sizeof(double));
+    auto *d_back = (double *)alloc((size_t)nr * kJBack * sizeof(double));
+    auto *d_cond = (double *)alloc((size_t)nr * kJCond * sizeof(double));
+    auto *d_start = (double *)alloc((size_t)nr * kJStart * sizeof(double));
+    auto *d_stack_j = (double *)alloc((size_t)ns * depth * kJStart * sizeof(double));
+    auto *d_stack_c = (int32_t *)alloc((size_t)ns * depth * sizeof(int32_t));
+    auto *d_counts = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
+    for (void *p : bufs)
+        if (!p) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
+    if (bufs.size() != 10) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
+    hipError_t e = hipMemcpyAsync(d_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice, f->stream);
+    if (e == hipSuccess) e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_joint_rows, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                           f->d_row_cell, nr, d_fwd, d_bwd, d_back, d_cond, d_start);
+        e = hipGetLastError();
+    }
+    const unsigned wblocks = (unsigned)((ns + 63) / 64);
+    if (e == hipSuccess) {   // pass 1: count
+        hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_row_cell,
+                           d_pstate, d_back, d_cond, d_start, tol, r_lo, ns, depth, d_stack_j, d_stack_c, d_counts,
+                           (const int64_t *)nullptr, (int64_t *)nullptr, (double *)nullptr);
+        e = hipGetLastError();
+    }
+    std::vector<int64_t> counts(ns), off(ns);
+    if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    int64_t total = 0;
+    for (int64_t k = 0; k < ns; ++k) {
+        off[k] = total;
+        total += counts[k];
+    }
+    *n_out = total;
+    if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
+        auto *d_off = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
+        auto *d_idx = (int64_t *)alloc((size_t)total * 2 * sizeof(int64_t));
+        auto *d_val = (double *)alloc((size_t)total * kJStart * sizeof(double));
+        if (!d_off || !d_idx || !d_val) {
+            cleanup();
+            g_last_err = "ggp_joints: device allocation failed";
+            return GGP_ENOMEM;
+        }
+        e = hipMemcpyAsync(d_off, off.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_row_cell,
+                               d_pstate, d_back, d_cond, d_start, tol, r_lo, ns, depth, d_stack_j, d_stack_c, d_counts,
+                               (const int64_t *)d_off, d_idx, d_val);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    }
+    cleanup();
+    if (e != hipSuccess) {
+        g_last_err = std::string("ggp_joints: ") + hipGetErrorString(e);
+        return GGP_EDEV;
+    }
     return GGP_OK;
 }
 
@@ -1138,26 +1320,7 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
     if (rc == GGP_OK && hipMemsetAsync(d_pstate, 0, (size_t)nc * 20 * sizeof(double), f->stream) != hipSuccess)
         rc = GGP_EDEV;
     if (rc != GGP_OK) { cleanup(); return rc; }
-    const int n_levels = (int)f->level_start.size() - 1;
-    hipError_t e = hipSuccess;
-    for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
-        const int64_t a = f->level_start[L];
-        const int n = (int)(f->level_start[L + 1] - a);
-        if (n <= 0) continue;
-        const int cpw = lane_cpw(f);
-        hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                           f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
-        e = hipGetLastError();
-    }
-    for (int L = n_levels - 1; L >= 0 && e == hipSuccess; --L) {   // backward: leaves first
-        const int64_t a = f->level_start[L];
-        const int n = (int)(f->level_start[L + 1] - a);
-        if (n <= 0) continue;
-        const int cpw = lane_cpw(f);
-        hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                           f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
-        e = hipGetLastError();
-    }
+    hipError_t e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
     if (e == hipSuccess) {
         const int64_t blocks = (nr + 255) / 256;
         hipLaunchKernelGGL(k_combine, dim3((unsigned)blocks), dim3(256), 0, f->stream, d_ptab, n_seg,

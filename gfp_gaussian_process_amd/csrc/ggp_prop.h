@@ -436,10 +436,7 @@ GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const P
 }
 
 // ---- the outputs: new mean and covariance (mean_cov_model.h:73-208) -------------------
-// PART = -1 computes everything.  PART 0 / 1 compute the new mean plus one half of the
-// covariance (0: xx xg xl xq gl ll, 1: gg gq lq qq) for the two-wave group schedule, which
-// exchanges the halves through LDS; every expression is the same in all three forms.
-template <int PART = -1, class IA, class XA>
+template <class IA, class XA>
 GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
 {
     const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
@@ -464,7 +461,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     nm[3] = mq + (bq - mq) * egq;
 
     double nxg = 0, nxl = 0, nxq = 0, ngl = 0, nxx = 0, nll = 0, ngq = 0, ngg = 0, nlq = 0, nqq = 0;
-    if constexpr (PART != 1) {
+    {
     // cov_xg (mean_cov_model.h:97-115)
     nxg =
         rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + rdiv(bg * bl, ebt_gl, r_ebt_gl)
@@ -510,7 +507,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
           + S.k_xx * (2 * gl * t - 3 + 4 * egl - (egl * egl));
     nll = Cll * (egl * egl) + S.k_ll * (1 - (egl * egl));
     }
-    if constexpr (PART != 0) {
+    {
     // cov_gq (mean_cov_model.h:183-196)
     ngq =
         rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)
@@ -572,13 +569,47 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
 #undef DGL
 #undef DGQ
     m[0] = nm[0]; m[1] = nm[1]; m[2] = nm[2]; m[3] = nm[3];
-    if constexpr (PART != 1) {
-        C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
-        C[4] = nxg;  C[6] = ngl;  C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[12] = nxq;
-    }
-    if constexpr (PART != 0) {
-        C[5] = ngg;  C[7] = ngq;  C[11] = nlq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
-    }
+    C[0] = nxx;  C[1] = nxg;  C[2] = nxl;  C[3] = nxq;
+    C[4] = nxg;  C[5] = ngg;  C[6] = ngl;  C[7] = ngq;
+    C[8] = nxl;  C[9] = ngl;  C[10] = nll; C[11] = nlq;
+    C[12] = nxq; C[13] = ngq; C[14] = nlq; C[15] = nqq;
+}
+
+// ---- cross_cov_model (mean_cov_model.h:380-432): K_{n+1,n} from the same step's integrals
+// (its I0/I1/I2 calls are the O_1A, O_2A, T_2A, Z_1A, Z_2A integrals of mean_cov_model) ----
+template <class IA, class XA>
+GGP_DEV void cross_outputs(const Step &S, const IA &I, const XA &X, double *K)
+{
+    const double bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
+    const double Cxx = S.Cxx, Cxg = S.Cxg, Cxl = S.Cxl, Cxq = S.Cxq, Cgg = S.Cgg, Cgl = S.Cgl;
+    const double Cgq = S.Cgq, Cll = S.Cll, Clq = S.Clq, Cqq = S.Cqq;
+    const double gl = S.gl, mq = S.mq, rgl = S.r_gl;
+    const double ebt = X[XS_bt], egl = X[XS_gl], egq = X[XS_gq];
+    const double r_ebt = 1.0 / ebt;
+    // nm(1): mean_g at the end of the step, the same expression as outputs()
+    const double nm1 = rdiv(bg, ebt, r_ebt) + Clq * I[O_2A] + mq * I[Z_1A] + (bq + Cxq - mq) * I[Z_2A];
+    K[0] = Cxx + rdiv(Cxl * (1 - egl), gl, rgl);
+    K[1] = Cxg + rdiv(Cgl * (1 - egl), gl, rgl);
+    K[2] = Cxl + rdiv(Cll * (1 - egl), gl, rgl);
+    K[3] = Cxq + rdiv(Clq * (1 - egl), gl, rgl);
+    K[4] = rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + Cxl * mq * I[O_1A]
+           + (bx * Clq + bq * Cxl + Cxl * Cxq + Clq * Cxx - Cxl * mq) * I[O_2A] + Clq * Cxl * I[T_2A]
+           + (bx * mq + Cxx * mq) * I[Z_1A]
+           + (bq * bx + Cxq + bx * Cxq + bq * Cxx + Cxq * Cxx - bx * mq - Cxx * mq) * I[Z_2A] - nm1 * bx;
+    K[5] = rdiv(bg * bg, ebt, r_ebt) + rdiv(Cgg, ebt, r_ebt) + Cgl * mq * I[O_1A]
+           + (bq * Cgl + bg * Clq + Clq * Cxg + Cgl * Cxq - Cgl * mq) * I[O_2A] + Cgl * Clq * I[T_2A]
+           + (bg * mq + Cxg * mq) * I[Z_1A]
+           + (bg * bq + Cgq + bq * Cxg + bg * Cxq + Cxg * Cxq - bg * mq - Cxg * mq) * I[Z_2A] - nm1 * bg;
+    K[6] = rdiv(bg * bl, ebt, r_ebt) + rdiv(Cgl, ebt, r_ebt) + Cll * mq * I[O_1A]
+           + (bq * Cll + bl * Clq + Clq * Cxl + Cll * Cxq - Cll * mq) * I[O_2A] + Cll * Clq * I[T_2A]
+           + (bl * mq + Cxl * mq) * I[Z_1A]
+           + (bl * bq + Clq + bq * Cxl + bl * Cxq + Cxl * Cxq - bl * mq - Cxl * mq) * I[Z_2A] - nm1 * bl;
+    K[7] = rdiv(bg * bq, ebt, r_ebt) + rdiv(Cgq, ebt, r_ebt) + Clq * mq * I[O_1A]
+           + (2 * bq * Clq + 2 * Clq * Cxq - Clq * mq) * I[O_2A] + (Clq * Clq) * I[T_2A]
+           + (bq * mq + Cxq * mq) * I[Z_1A]
+           + ((bq * bq) + Cqq + 2 * bq * Cxq + (Cxq * Cxq) - bq * mq - Cxq * mq) * I[Z_2A] - nm1 * bq;
+    K[8] = Cxl * egl;  K[9] = Cgl * egl;  K[10] = Cll * egl; K[11] = Clq * egl;
+    K[12] = Cxq * egq; K[13] = Cgq * egq; K[14] = Clq * egq; K[15] = Cqq * egq;
 }
 
 // ---- lane schedule: one lane runs every task of its own cell; the task descriptors are
@@ -608,7 +639,8 @@ GGP_DEV void lane_taus(const Step &S, const XA &X, const DA &Dw, const PA &PW, d
 }
 
 // ---- lane schedule: one lane runs every task of its own cell
-GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, const double *tab)
+// K (optional, 16): cross_cov_model of the same step (the -j path)
+GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, const double *tab, double *K = nullptr)
 {
     Step S;
     step_init(S, m, C, t, P);
@@ -625,6 +657,7 @@ GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, c
     }
     double I[NI];
     lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
+    if (K) cross_outputs(S, I, X, K);
     outputs(S, I, X, m, C);
 }
 

@@ -285,9 +285,7 @@ class HostForest:
 def kernel_name(code: int) -> str:
     """the HIP kernel symbol behind a launch-profile code (include/ggp.h)"""
     kind, lanes = code >> 8, code & 0xFF
-    if kind == N.KERNELS["lane"]:
-        return "k_loglik_level"
-    return "k_loglik_group2" if lanes == 128 else f"k_loglik_group<{lanes}>"
+    return "k_loglik_level" if kind == N.KERNELS["lane"] else f"k_loglik_group<{lanes}>"
 
 
 class Forest:
@@ -351,6 +349,21 @@ class Forest:
         self._check(self._lib.ggp_predict(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0],
                                           *(o.ctypes.data_as(N.c_double_p) for o in out)))
         return tuple(out)
+
+    def joints(self, params_per_segment, tol: float = 1e-10, r_lo: int = 0, r_hi=None, cap: int = 1 << 22):
+        """-j compute for start rows [r_lo, r_hi) (ggp_joints): (idx [k, 2] = (start, target) rows,
+        val [k, 72] = mean[8], row-major cov[64]) in the reference's add order"""
+        p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
+        r_hi = self.n_rows if r_hi is None else r_hi
+        n = ctypes.c_int64()
+        idx = np.zeros((cap, 2), np.int64)
+        val = np.zeros((cap, 72))
+        self._check(self._lib.ggp_joints(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0], tol, r_lo, r_hi, cap,
+                                         idx.ctypes.data_as(N.c_int64_p), val.ctypes.data_as(N.c_double_p),
+                                         ctypes.byref(n)))
+        if n.value > cap:
+            raise GGPError(f"{n.value} joints exceed cap {cap}: use a larger cap or a smaller row range")
+        return idx[: n.value], val[: n.value]
 
     def enable_profile(self) -> None:
         n = ctypes.c_int32()

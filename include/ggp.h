@@ -10,6 +10,7 @@
  *                                total_likelihood_log_params         likelihood.h:161-167:
  *                                the caller negates / exponentiates)
  *                               incl. likelihood_recr / sc_likelihood likelihood.h:36-122
+ *   ggp_joints        replaces  collect_joint_distributions (compute) correlation_tree.h:464-651
  *   ggp_predict       replaces  prediction_forward                   predictions.h:166-173
  *                               prediction_backward                  predictions.h:438-444
  *                               combine_predictions                  predictions.h:466-499
@@ -96,6 +97,15 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
  * normal (un-reversed) coordinates as stored in MOMAdata::mean_backward. */
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd,
                 double *out_bwd, double *out_comb);
+
+/* -j compute: collect_joint_distributions (correlation_tree.h:464-651).  Runs the smoother,
+ * then for every start row r in [r_lo, r_hi) (input order) the joints P(z_target, z_r | D)
+ * the reference adds to its Joint_vector, in the order it adds them: out_idx[2k] = r,
+ * out_idx[2k+1] = target row, out_val[72k..] = mean[8] then cov[64] row-major.  *n_out is the
+ * number of joints; they are stored only when *n_out <= cap (else call again with a larger
+ * cap or a smaller row range). */
+int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo,
+               int64_t r_hi, int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out);
 
 /* carried state: zero it (fresh cells), or read it back ([n_cells*20]) */
 int ggp_reset_state(ggp_forest *f);

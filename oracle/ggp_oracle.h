@@ -71,6 +71,16 @@ double ora_total_loglik(const ora_forest *f, const double *params, double *state
 int ora_predict(const ora_forest *f, const double *params, int n_seg, double *state,
                 double *fwd, double *bwd, double *comb);
 
+/* -j: collect_joint_distributions (correlation_tree.h:464-651), compute only.  For every
+ * start row r in [r_lo, r_hi) (input order) the joints P(z_target, z_r | D) the reference
+ * adds to its Joint_vector, in the order it adds them: out_idx[2k] = start row,
+ * out_idx[2k+1] = target row, out_val[72k..] = mean[8], cov[64] (row-major).  fwd/bwd are
+ * ora_predict's outputs and bstate the state buffer it leaves (MOMAdata::mean/cov after -p).
+ * Returns the number of joints (only the first cap are stored). */
+int64_t ora_joints(const ora_forest *f, const double *params, int n_seg, const double *fwd,
+                   const double *bwd, const double *bstate, double tol, int64_t r_lo,
+                   int64_t r_hi, int64_t cap, int64_t *out_idx, double *out_val);
+
 #ifdef ORA_EXPERIMENT
 /* sensitivity experiments only: replace exp() on the propagator path */
 extern double (*ora_exp_hook)(double);

@@ -55,6 +55,10 @@ def lib():
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), dp]
         L.ora_predict.restype = ctypes.c_int
         L.ora_predict.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, dp]
+        L.ora_joints.restype = ctypes.c_int64
+        L.ora_joints.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, ctypes.c_double,
+                                 ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                 ctypes.POINTER(ctypes.c_int64), dp]
         _lib = L
     return _lib
 
@@ -112,7 +116,21 @@ class OracleForest:
         st = np.zeros((self.f.n_cells, 20))
         out = [np.zeros((self.f.n_rows, 20)) for _ in range(3)]
         lib().ora_predict(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(st), *(_dp(o) for o in out))
+        self.after_predict = st          # MOMAdata::mean/cov after -p (the backward final states)
         return tuple(out)
+
+    def joints(self, params_per_segment, tol=1e-10, r_lo=0, r_hi=None, cap=1 << 20):
+        """-j for start rows [r_lo, r_hi): (idx [k, 2] = (start, target), val [k, 72])"""
+        p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
+        fwd, bwd, _ = self.predict(p)
+        r_hi = self.f.n_rows if r_hi is None else r_hi
+        idx = np.zeros((cap, 2), np.int64)
+        val = np.zeros((cap, 72))
+        n = lib().ora_joints(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(fwd), _dp(bwd), _dp(self.after_predict),
+                             tol, r_lo, r_hi, cap, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _dp(val))
+        if n > cap:
+            raise ValueError(f"{n} joints > cap {cap}")
+        return idx[:n], val[:n]
 
 
 def dawson(x: float) -> float:

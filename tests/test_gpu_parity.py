@@ -223,17 +223,9 @@ def test_lane_and_group_schedules_bitwise_equal(example_forests, which):
           "ragged": _ragged_roots}[which]()
     P = CONFIGS[0][2]
     lane, group = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel="group")
-    os.environ["GGP_GROUP_WAVES"] = "2"          # read at forest creation: the two-wave kernel
-    try:
-        group2 = g.Forest(hf, kernel="group")
-    finally:
-        del os.environ["GGP_GROUP_WAVES"]
     for _ in range(3):
-        v = lane.total_likelihood(P)
-        assert group.total_likelihood(P) == v
-        assert group2.total_likelihood(P) == v
+        assert lane.total_likelihood(P) == group.total_likelihood(P)
     assert np.array_equal(lane.state(), group.state())
-    assert np.array_equal(lane.state(), group2.state())
 
 
 # ------------------------------------------------------------------------------------------
