@@ -15,6 +15,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
+LIB_SENS = os.path.join(HERE, "liboracle_sens.so")
 REF_FADDEEVA = os.path.join(HERE, "_ref", "libfaddeeva_ref.so")
 
 
@@ -29,38 +30,51 @@ class OraForest(ctypes.Structure):
 
 
 _lib = None
+_libs = {}
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib():
+def lib(sens: bool = False):
+    """the oracle library; sens=True: the build with the exp-ulp conditioning probe"""
     global _lib
+    if sens:
+        if "sens" not in _libs:
+            if not os.path.exists(LIB_SENS):
+                build()
+            _libs["sens"] = _bind(ctypes.CDLL(LIB_SENS))
+            _libs["sens"].ora_set_exp_ulp_noise.argtypes = [ctypes.c_uint64]
+            _libs["sens"].ora_set_exp_ulp_noise.restype = None
+        return _libs["sens"]
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        L = ctypes.CDLL(LIB)
-        dp = ctypes.POINTER(ctypes.c_double)
-        L.ora_dawson.restype = ctypes.c_double
-        L.ora_dawson.argtypes = [ctypes.c_double]
-        L.ora_tauint.restype = ctypes.c_double
-        L.ora_tauint.argtypes = [ctypes.c_int] + [ctypes.c_double] * 5
-        L.ora_mean_cov_model.restype = None
-        L.ora_mean_cov_model.argtypes = [dp, dp, ctypes.c_double, dp]
-        L.ora_cross_cov_model.restype = None
-        L.ora_cross_cov_model.argtypes = [dp, dp, ctypes.c_double, dp, dp]
-        L.ora_total_loglik.restype = ctypes.c_double
-        L.ora_total_loglik.argtypes = [ctypes.POINTER(OraForest), dp, dp,
-                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), dp]
-        L.ora_predict.restype = ctypes.c_int
-        L.ora_predict.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, dp]
-        L.ora_joints.restype = ctypes.c_int64
-        L.ora_joints.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, ctypes.c_double,
-                                 ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                                 ctypes.POINTER(ctypes.c_int64), dp]
-        _lib = L
+        _lib = _bind(ctypes.CDLL(LIB))
     return _lib
+
+
+def _bind(L):
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.ora_dawson.restype = ctypes.c_double
+    L.ora_dawson.argtypes = [ctypes.c_double]
+    L.ora_tauint.restype = ctypes.c_double
+    L.ora_tauint.argtypes = [ctypes.c_int] + [ctypes.c_double] * 5
+    L.ora_mean_cov_model.restype = None
+    L.ora_mean_cov_model.argtypes = [dp, dp, ctypes.c_double, dp]
+    L.ora_cross_cov_model.restype = None
+    L.ora_cross_cov_model.argtypes = [dp, dp, ctypes.c_double, dp, dp]
+    L.ora_total_loglik.restype = ctypes.c_double
+    L.ora_total_loglik.argtypes = [ctypes.POINTER(OraForest), dp, dp,
+                                   ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), dp]
+    L.ora_predict.restype = ctypes.c_int
+    L.ora_predict.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, dp]
+    L.ora_joints.restype = ctypes.c_int64
+    L.ora_joints.argtypes = [ctypes.POINTER(OraForest), dp, ctypes.c_int, dp, dp, dp, ctypes.c_double,
+                             ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                             ctypes.POINTER(ctypes.c_int64), dp]
+    return L
 
 
 def _dp(a):
@@ -96,15 +110,25 @@ def make_forest(a: dict) -> OraForest:
 class OracleForest:
     """CPU oracle over the same arrays, with its own carried state."""
 
-    def __init__(self, arrays: dict):
+    def __init__(self, arrays: dict, exp_ulp_noise: int = 0):
+        """exp_ulp_noise != 0: run on the conditioning-probe build with exp() moved +-1 ulp at
+        random (seeded) -- tells a test which outputs rounding alone can move"""
         self.f = make_forest(arrays)
+        self._noise = int(exp_ulp_noise)
         self.state = np.zeros((self.f.n_cells, 20))
         self.cell_ll = np.zeros(self.f.n_cells)
+
+    def _L(self):
+        if not self._noise:
+            return lib()
+        L = lib(sens=True)
+        L.ora_set_exp_ulp_noise(self._noise)    # re-seeded per call: deterministic
+        return L
 
     def total_likelihood(self, params):
         p = np.ascontiguousarray(params, np.float64)
         nc, nr = ctypes.c_int64(), ctypes.c_int64()
-        v = lib().ora_total_loglik(ctypes.byref(self.f), _dp(p), _dp(self.state), ctypes.byref(nc),
+        v = self._L().ora_total_loglik(ctypes.byref(self.f), _dp(p), _dp(self.state), ctypes.byref(nc),
                                    ctypes.byref(nr), _dp(self.cell_ll))
         return v, nc.value, nr.value
 
@@ -115,7 +139,7 @@ class OracleForest:
         p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
         st = np.zeros((self.f.n_cells, 20))
         out = [np.zeros((self.f.n_rows, 20)) for _ in range(3)]
-        lib().ora_predict(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(st), *(_dp(o) for o in out))
+        self._L().ora_predict(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(st), *(_dp(o) for o in out))
         self.after_predict = st          # MOMAdata::mean/cov after -p (the backward final states)
         return tuple(out)
 
@@ -126,7 +150,7 @@ class OracleForest:
         r_hi = self.f.n_rows if r_hi is None else r_hi
         idx = np.zeros((cap, 2), np.int64)
         val = np.zeros((cap, 72))
-        n = lib().ora_joints(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(fwd), _dp(bwd), _dp(self.after_predict),
+        n = self._L().ora_joints(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(fwd), _dp(bwd), _dp(self.after_predict),
                              tol, r_lo, r_hi, cap, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _dp(val))
         if n > cap:
             raise ValueError(f"{n} joints > cap {cap}")
