@@ -8,7 +8,7 @@ total-log-likelihood evaluation (likelihood.h:125-174 semantics, carried root st
 the inputs resident in HBM, plus -- for N > 1 -- the one all_gather of the per-rank
 partial (RCCL over xGMI).  Weak scaling: rank r evaluates trees [r*T, (r+1)*T).
 
-  python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group]
+  python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group|wave]
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the one with the
 largest share of the evaluation), timed with HIP events on the engine's own stream; `cpu_baseline` is the CPU oracle
@@ -66,7 +66,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--trees", type=int, default=1000, help="trees per GPU")
     ap.add_argument("--rows", type=int, default=200, help="rows per tree")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group", "wave"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--large-trees", type=int, default=12500,

@@ -11,16 +11,26 @@
 // the library is built with -ffp-contract=off).  Transcendental libm differences (ocml vs
 // glibc, <= 1 ulp) move the total log-likelihood by ~1e-11 relative (measured).
 #pragma once
-#include <hip/hip_runtime.h>
 #include <math.h>
 
+#ifdef GGP_HOST_SIM
+// host simulation of the device math (tools/hostsim.cpp, g++): the same source, glibc libm.
+// Diagnostic builds only; the shipped library is always the gfx950 code object.
+#include <algorithm>
+#include <cstdint>
+using std::min;
+#define GGP_DEV inline
+#define GGP_DAWSON_TABLE_QUALIFIER static const
+#include "dawson_table.inc"
+#else
+#include <hip/hip_runtime.h>
 #ifndef GGP_DEVICE_TABLE_DEFINED
 #define GGP_DEVICE_TABLE_DEFINED
 #define GGP_DAWSON_TABLE_QUALIFIER static __constant__ const
 #include "dawson_table.inc"
 #endif
-
 #define GGP_DEV __device__ __forceinline__
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Dawson: w_im on y = 1/(1+|x|) with 97 polynomial pieces (degree 6..8, zero-padded to 9),

@@ -29,6 +29,7 @@
 #include "ggp.h"
 #include "ggp_device.h"
 #include "ggp_prop.h"
+#include "ggp_outtab.h"
 #include "ggp_predict.h"
 #include "ggp_joints.h"
 
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
 // the shipped library never does).
 #ifdef GGP_STAMPS
 __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + stage]
-#define GGP_STAMP_DECL unsigned long long st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, st_now = 0; int st_steps = 0
+#define GGP_STAMP_DECL unsigned long long st_acc[15] = {0}, st_prev = 0, st_now = 0; int st_steps = 0
 #define GGP_STAMP(k)                                                                       \
     do {                                                                                   \
         __builtin_amdgcn_sched_barrier(0);                                                 \
@@ -173,7 +174,7 @@ __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + sta
     do {                                                                                   \
         if (threadIdx.x == 0) {                                                            \
             const int o_ = 16 * (CPW == 1 ? 0 : CPW == 2 ? 1 : CPW == 4 ? 2 : 3);          \
-            for (int k_ = 0; k_ < 9; ++k_) atomicAdd(&g_stamp[o_ + k_], st_acc[k_]);       \
+            for (int k_ = 0; k_ < 15; ++k_) atomicAdd(&g_stamp[o_ + k_], st_acc[k_]);      \
             atomicAdd(&g_stamp[o_ + 15], (unsigned long long)st_steps);                    \
         }                                                                                  \
     } while (0)
@@ -338,6 +339,246 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
     }
     GGP_STAMP_FLUSH();
     if (valid && lg == 0) {
+        double *st = state + (size_t)20 * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[k] = m[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+        cell_ll[c] = cl;
+        cell_nan[c] = nan_row;
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// WAVE schedule: one 64-lane wave per cell with every stage of the step spread over the
+// lanes -- the 74 exponentials + 14 Dawson values + 3 powers, the 45 integrals in one
+// branch-free form (ggp::tau_unified) + the 18 exp-derived basis values on the spare lanes,
+// the outputs as the sparse trilinear form of ggp_outtab.h (59 lanes x 4 terms, summed by a
+// DPP butterfly inside power-of-two lane blocks and broadcast by readlane) -- and the Kalman
+// update redundantly in all lanes (the state stays in registers).  The log of the ll term is
+// off the critical path: det and the quadratic form go to an LDS ring, and every 64 rows (or
+// at the cell's end) 64 lanes take the logs at once and one lane adds the terms in row order
+// (the reference's summation order; the first NaN row is found there).
+// The outputs are the same polynomial as ggp::outputs summed in another order, so results
+// agree with the lane/group schedules to ~1e-10 relative on the total, not bitwise
+// (DESIGN.md "Parity").
+// ------------------------------------------------------------------------------------------
+constexpr int kWaveSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::BV_N + ggp::V_N + ggp::SB_N;
+
+template <int CTRL>
+GGP_DEV double dpp_f64(const double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <int LANE>
+GGP_DEV double readlane_f64(const double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), LANE);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), LANE);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <size_t... K>
+GGP_DEV void wave_outputs(const double v, double *o, std::index_sequence<K...>)
+{
+    ((o[K] = readlane_f64<ggp::kOutLead[K]>(v)), ...);
+}
+
+// ll terms of rows [base, base + n) from the LDS ring into cl, in row order; false at the
+// first NaN (nan_row set)
+GGP_DEV bool wave_flush_ll(const double *ring_q, const double *ring_det, double *ring_t, const int n,
+                           const int64_t base, const double two_log_2pi, const int lane, double &cl, int &nan_row)
+{
+    __syncthreads();
+    if (lane < n) ring_t[lane] = ring_q[lane] - 0.5 * log(ring_det[lane]) - two_log_2pi;
+    __syncthreads();
+    bool ok = true;
+    if (lane == 0) {
+        for (int k = 0; k < n; ++k) {
+            cl += ring_t[k];
+            if (cl != cl) {
+                nan_row = (int)(base + k);
+                ok = false;
+                break;
+            }
+        }
+    }
+    // every lane returns lane 0's verdict
+    return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+}
+
+__global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
+                                                    int n, double *__restrict__ state,
+                                                    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
+{
+    constexpr int G = 64;
+    constexpr int CPW = 8;   // stamp slot 3 (GGP_STAMPS builds only)
+    constexpr int NXB = (ggp::NXT + G - 1) / G;
+    __shared__ double lds[kWaveSlot];
+    __shared__ double s_ou[ggp::OU_N];
+    __shared__ double s_tab[kDawsonTab];
+    __shared__ double ring_q[64], ring_det[64], ring_t[64];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    const int i = blockIdx.x;
+    double *Xl = lds;
+    double *Dl = Xl + ggp::NX;
+    double *Pl = Dl + ggp::ND;
+    double *Bv = Pl + ggp::NPW;       // [1, I(45), derived(18)]
+    double *Il = Bv + ggp::BV_I;
+    double *Vl = Bv + ggp::BV_N;      // [1, bx, bg, bl - ml, bq - mq, Cxx .. Cqq, t]
+    double *Sb = Vl + ggp::V_N;       // the step block (ggp_prop.h)
+    // this lane's task descriptors (registers for the whole launch)
+    uint32_t xd[NXB];
+#pragma unroll
+    for (int q = 0; q < NXB; ++q) {
+        const int j = lane + q * G;
+        xd[q] = ggp::pack_x(ggp::kXT[j < ggp::NXT ? j : 0]);
+    }
+    const uint32_t dd = ggp::pack_d(ggp::kDT[lane < ggp::ND ? lane : 0]);
+    const ggp::ITask cd = ggp::kIT[lane < ggp::NI ? lane : 0];
+    const ggp::DTaskB dbt = ggp::kDerived[lane >= ggp::NI && lane < ggp::NI + ggp::kNDerived ? lane - ggp::NI : 0];
+    const double *p = P.p;
+    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    double kap[ggp::kOutL];
+    ggp::OutTerm tt[ggp::kOutL];
+#pragma unroll
+    for (int q = 0; q < ggp::kOutL; ++q) {
+        tt[q] = ggp::kOutTerm[lane][q];
+        kap[q] = ggp::out_kappa(ou, tt[q].kap);
+    }
+    const int bs = ggp::kOutBlock[lane];
+    if (lane == 0) ggp::store_ou(ou, s_ou);
+    double m[4] = {0, 0, 0, 0}, C[16] = {0};
+    int c = 0;
+    int64_t r = 0, r1 = 0, r0 = 0;
+    double dt = 0.0, t_cur = 0.0;
+    bool pending = false, divide = false;
+    const bool valid = i < n;
+    if (valid) {
+        c = cells[i];
+        r0 = F.row_off[c];
+        r1 = F.row_off[c + 1];
+        r = r0;
+        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        divide = pending;
+        t_cur = F.time[r0];
+    }
+    if (lane == 0) {
+        Xl[ggp::X_ONE] = 1.0;
+        Bv[ggp::BV_ONE] = 1.0;
+        Vl[ggp::V_ONE] = 1.0;
+    }
+    __syncthreads();
+    double cl = 0.0;
+    int nan_row = kNanNone;
+    int slot = 0;                     // rows in the ll ring
+    bool live = valid;
+    GGP_STAMP_DECL;
+    while (live) {   // the whole workgroup is one cell: uniform
+        GGP_STAMP(0);
+        GGP_STAMP_STEP();
+        const double y_l = F.logl[r], y_f = F.fp[r];
+        const double t_next = r + 1 < r1 ? F.time[r + 1] : 0.0;
+        if (pending) {
+            if (lane == 0) {
+                ggp::Step S;
+                ggp::step_init(S, m, C, dt, ou);
+                ggp::store_step(S, Sb);
+                const double v[ggp::V_N - 1] = {S.bx, S.bg, S.bl - S.ml, S.bq - S.mq, S.Cxx, S.Cxg, S.Cxl, S.Cxq,
+                                                S.Cgg, S.Cgl, S.Cgq, S.Cll, S.Clq, S.Cqq, S.t};
+#pragma unroll
+                for (int k = 0; k < ggp::V_N - 1; ++k) Vl[1 + k] = v[k];
+            }
+            GGP_STAMP(1);
+            __syncthreads();
+            GGP_STAMP(2);
+            const ggp::StepL S(Sb);
+            {   // exponentials, Dawson values, powers
+                double ev[NXB];
+#pragma unroll
+                for (int q = 0; q < NXB; ++q) ev[q] = ggp::exp_body(S, ggp::unpack_x(xd[q]));
+                const double dv = ggp::dawson_body(S, ggp::unpack_d(dd), s_tab);
+                const double pw = ggp::pow_task(S, lane < 3 ? lane : 0);
+#pragma unroll
+                for (int q = 0; q < NXB; ++q)
+                    if (lane + q * G < ggp::NXT) Xl[lane + q * G] = ev[q];
+                if (lane < ggp::ND) Dl[lane] = dv;
+                if (lane < 3) {
+                    Pl[lane] = pw;
+                    Pl[3 + lane] = 1.0 / pw;
+                }
+            }
+            GGP_STAMP(3);
+            __syncthreads();
+            GGP_STAMP(4);
+            if (lane < ggp::NI) {   // the integrals
+                Il[lane] = ggp::tau_unified(S, cd, Xl, Dl, Pl);
+            } else if (lane < ggp::NI + ggp::kNDerived) {   // the exp-derived basis values
+                Bv[ggp::BV_R_EBT + lane - ggp::NI] = ggp::derived_generic(dbt, Xl, ou.gl, S.t);
+            }
+            GGP_STAMP(5);
+            __syncthreads();
+            GGP_STAMP(6);
+            double acc = 0.0;   // this lane's output terms
+#pragma unroll
+            for (int q = 0; q < ggp::kOutL; ++q)
+                acc = acc + (((kap[q] * Vl[tt[q].v1]) * Vl[tt[q].v2]) * Vl[tt[q].v3]) * Bv[tt[q].basis];
+            GGP_STAMP(7);
+            {   // block sums: DPP butterfly (ggp::out_partner)
+                double w;
+                w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
+                w = dpp_f64<0x4E>(acc);  acc = bs > 2 ? acc + w : acc;
+                w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
+                w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
+            }
+            GGP_STAMP(8);
+            double o[ggp::kOutN];
+            wave_outputs(acc, o, std::make_index_sequence<ggp::kOutN>{});
+            ggp::out_finish([&](int k) { return o[k]; }, o);
+            ggp::out_store(o, m, C);
+            if (divide) {
+                ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                divide = false;
+            }
+            GGP_STAMP(9);
+        }
+        const double x0 = y_l - m[0];
+        const double x1 = y_f - m[1];
+        ggp_innov v;
+        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+        {   // the ll term without its log (ggp_ll_term), into the ring
+            const double h0 = -0.5 * x0, h1 = -0.5 * x1;
+            const double q = (h0 * v.si00 + h1 * v.si10) * x0 + (h0 * v.si01 + h1 * v.si11) * x1;
+            if (lane == 0) {
+                ring_q[slot] = q;
+                ring_det[slot] = ggp_det_pplu(v.S00, v.S01, v.S10, v.S11);
+            }
+        }
+        ++slot;
+        ggp_posterior(m, C, x0, x1, v);
+        pending = r + 1 < r1;
+        if (pending) dt = t_next - t_cur;
+        t_cur = t_next;
+        ++r;
+        live = r < r1;
+        GGP_STAMP(10);
+        if (slot == 64 || !live) {
+            if (!wave_flush_ll(ring_q, ring_det, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
+                break;
+            slot = 0;
+        }
+        __syncthreads();   // LDS slots are rewritten by the next step
+        GGP_STAMP(11);
+    }
+    GGP_STAMP_FLUSH();
+    if (valid && lane == 0) {
         double *st = state + (size_t)20 * c;
 #pragma unroll
         for (int k = 0; k < 4; ++k) st[k] = m[k];
@@ -839,7 +1080,12 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
         const int64_t n_simd = (int64_t)f->n_cu * 4;
         const bool group = f->kernel_pref == GGP_KERNEL_GROUP ||
                            (f->kernel_pref == GGP_KERNEL_AUTO && n <= f->group_max_cells);
-        if (group) {
+        if (f->kernel_pref == GGP_KERNEL_WAVE) {
+            hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                               f->d_state, f->d_cell_ll, f->d_cell_nan);
+            f->kernel_used = GGP_KERNEL_WAVE;
+            f->last_code = GGP_KERNEL_WAVE << 8 | 64;
+        } else if (group) {
             // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
             int cpw = 1;
@@ -1005,6 +1251,10 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
                     g_last_err = "daughter/parent pointers disagree";
                     return GGP_EINVAL;
                 }
+    }
+    if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_WAVE) {
+        g_last_err = "ggp_forest_create: unknown kernel policy";
+        return GGP_EINVAL;
     }
     auto *f = new ggp_forest();
     f->device = d->device;

@@ -429,6 +429,34 @@ GGP_DEV double tau_body(const ST &S, const ITask T, const XA &X, const DA &Dw, c
     return rdiv(x, PW[2], PW[5]);
 }
 
+// One expression for all four tauint kinds (the wave schedule: no divergence between k):
+//   x = S1 * ec * (ea0 P(t0) - ea1 P(t1)) + Q (E0 D0 - E1 D1),  I = x / den_k
+//   k=0: S1 = 0, Q = -2, den = 2 sqrt a   (E = Z slots)   == 2 (-Z0 D0 + Z1 D1) bitwise
+//   k=1: S1 = -2 sqrt a, P = 1, Q = 2 B                  == tau_body bitwise
+//   k=2: S1 = 2 sqrt a, P = B - 2a t, Q = 2 (2a - B^2)   (E-term grouping differs: ulps)
+//   k=3: S1 = -2 sqrt a, P = B^2 - 4a - 2aB t + 4a^2 t^2, Q = 2 B (B^2 - 6a)  (ulps)
+template <class ST, class XA, class DA, class PA>
+GGP_DEV double tau_unified(const ST &S, const ITask T, const XA &X, const DA &Dw, const PA &PW)
+{
+    const double D0 = Dw[T.d0], D1 = Dw[T.d1];
+    const double E0 = X[T.x0], E1 = X[T.x1];
+    const double B = S.Bv(T.iB);
+    const double t0 = S.Tv(T.it0), t1 = S.Tv(T.it1);
+    const int k = T.k;
+    const double BB = B * B;
+    const double al = k == 1 ? 1.0 : k == 2 ? B : BB - 2. * S.two_a;
+    const double be = k == 1 ? 0.0 : k == 2 ? -S.two_a : -S.two_a * B;
+    const double ga = k == 3 ? S.four_aa : 0.0;
+    const double P0 = al + t0 * (be + ga * t0), P1 = al + t1 * (be + ga * t1);
+    const double Q = k == 0 ? -2.0 : k == 1 ? B * 2. : k == 2 ? (S.two_a - BB) * 2. : B * (-6. * S.a + BB) * 2.;
+    const double S1 = k == 2 ? S.two_sa : S.m2sa;
+    const double ec = X[T.xc], ea0 = X[T.xa0], ea1 = X[T.xa1];
+    const double dterm = Q * (E0 * D0 - E1 * D1);
+    const double x = k == 0 ? dterm : S1 * ec * (ea0 * P0 - ea1 * P1) + dterm;
+    const double den = k == 0 ? S.two_sa : PW[k - 1], rden = k == 0 ? S.r_two_sa : PW[k + 2];
+    return rdiv(x, den, rden);
+}
+
 template <class XA, class DA, class PA>
 GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const PA &PW)
 {

@@ -285,7 +285,11 @@ class HostForest:
 def kernel_name(code: int) -> str:
     """the HIP kernel symbol behind a launch-profile code (include/ggp.h)"""
     kind, lanes = code >> 8, code & 0xFF
-    return "k_loglik_level" if kind == N.KERNELS["lane"] else f"k_loglik_group<{lanes}>"
+    if kind == N.KERNELS["lane"]:
+        return "k_loglik_level"
+    if kind == N.KERNELS["wave"]:
+        return "k_loglik_wave"
+    return f"k_loglik_group<{lanes}>"
 
 
 class Forest:

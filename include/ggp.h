@@ -77,6 +77,8 @@ typedef struct {
 #define GGP_KERNEL_AUTO 0     /* pick by occupancy                                   */
 #define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
 #define GGP_KERNEL_GROUP 2    /* one workgroup per cell (latency)                    */
+#define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);
+                                 agrees with LANE/GROUP to ~1e-10, not bitwise        */
 
 int ggp_forest_create(const ggp_forest_desc *desc, ggp_forest **out);
 void ggp_forest_destroy(ggp_forest *f);

@@ -19,6 +19,7 @@
 #ifdef ORA_EXPERIMENT
 double (*ora_exp_hook)(double) = exp;
 double (*ora_dawson_hook)(double) = 0;
+void (*ora_mcm_hook)(double *, double *, double, const double *) = 0;
 #define EXP(v) (ora_exp_hook(v))
 #else
 #define EXP(v) exp(v)
@@ -312,6 +313,12 @@ static void load_prop(prop_in *s, const double *m, const double *C, double t, co
 
 void ora_mean_cov_model(double *m, double *C, double t, const double *p)
 {   /* mean_cov_model.h:211-274 */
+#ifdef ORA_EXPERIMENT
+    if (ora_mcm_hook) {
+        ora_mcm_hook(m, C, t, p);
+        return;
+    }
+#endif
     prop_in s;
     double nm[4], nC[16];
     load_prop(&s, m, C, t, p);

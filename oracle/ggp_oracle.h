@@ -85,6 +85,7 @@ int64_t ora_joints(const ora_forest *f, const double *params, int n_seg, const d
 /* sensitivity experiments only: replace exp() on the propagator path */
 extern double (*ora_exp_hook)(double);
 extern double (*ora_dawson_hook)(double);
+extern void (*ora_mcm_hook)(double *, double *, double, const double *);
 #endif
 
 #ifdef __cplusplus

@@ -28,3 +28,10 @@ void ora_set_exp_ulp_noise(uint64_t seed)
     g_state = seed ? seed : 0;
     ora_exp_hook = seed ? exp_ulp_noise : exp;
 }
+
+/* replace mean_cov_model by an external propagator (tools/hostsim.cpp: the device algorithm
+ * compiled for the host), to measure what a reformulation of it does to the total */
+void ora_set_mcm_hook(void (*fn)(double *, double *, double, const double *))
+{
+    ora_mcm_hook = fn;
+}

@@ -1,0 +1,84 @@
+// hostsim.cpp -- diagnostic only (never shipped): the device propagator compiled for the host
+// (GGP_HOST_SIM: same source, glibc libm), exported for numerical experiments against the
+// oracle (oracle/liboracle_sens.so ora_set_mcm_hook).  Build:
+//   g++ -O2 -std=c++17 -ffp-contract=off -fPIC -shared -I gfp_gaussian_process_amd/csrc \
+//       -o tools/libhostsim.so tools/hostsim.cpp
+#define GGP_HOST_SIM
+#include "ggp_outtab.h"
+#include <cstring>
+
+extern "C" {
+// mean_cov_model through the lane schedule's expressions (ggp::propagate_lane)
+void hs_mcm_lane(double *m, double *C, double t, const double *p)
+{
+    const ggp::OU P = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    ggp::propagate_lane(m, C, t, P, ggp_dawson_coef);
+}
+// the same with the wave schedule's table-driven outputs (ggp_outtab.h)
+void hs_mcm_tab(double *m, double *C, double t, const double *p)
+{
+    const ggp::OU P = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    ggp::propagate_tab(m, C, t, P, ggp_dawson_coef);
+}
+}
+
+extern "C" {
+// both output forms on one (m, C): out_lane/out_tab = m[4] then C[16]
+void hs_compare(const double *m, const double *C, double t, const double *p, double *out_lane, double *out_tab)
+{
+    for (int k = 0; k < 4; ++k) out_lane[k] = out_tab[k] = m[k];
+    for (int k = 0; k < 16; ++k) out_lane[4 + k] = out_tab[4 + k] = C[k];
+    hs_mcm_lane(out_lane, out_lane + 4, t, p);
+    hs_mcm_tab(out_tab, out_tab + 4, t, p);
+}
+}
+
+extern "C" {
+// per-term values of the table form at (m, C): terms[64 * kOutL]
+void hs_terms(const double *m, const double *C, double t, const double *p, double *terms)
+{
+    using namespace ggp;
+    const OU P = make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    Step S;
+    step_init(S, m, C, t, P);
+    double X[NX];
+    lane_exps(S, X, std::make_index_sequence<NXT>{});
+    X[X_ONE] = 1.0;
+    double Dw[ND];
+    lane_dawsons(S, Dw, ggp_dawson_coef, std::make_index_sequence<ND>{});
+    double PW[NPW];
+    for (int q = 0; q < 3; ++q) { PW[q] = pow_task(S, q); PW[3 + q] = 1.0 / PW[q]; }
+    double I[NI];
+    lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
+    double V[V_N] = {1.0, S.bx, S.bg, S.bl - S.ml, S.bq - S.mq, S.Cxx, S.Cxg, S.Cxl, S.Cxq, S.Cgg, S.Cgl, S.Cgq, S.Cll,
+                     S.Clq, S.Cqq, S.t};
+    double Bv[BV_N];
+    Bv[BV_ONE] = 1.0;
+    for (int j = 0; j < NI; ++j) Bv[BV_I + j] = I[j];
+    for (int j = 0; j < kNDerived; ++j) Bv[BV_R_EBT + j] = derived_basis(j, X, P.gl, S.t);
+    for (int l = 0; l < 64; ++l)
+        for (int q = 0; q < kOutL; ++q) {
+            const OutTerm T = kOutTerm[l][q];
+            terms[l * kOutL + q] = (((out_kappa(P, T.kap) * V[T.v1]) * V[T.v2]) * V[T.v3]) * Bv[T.basis];
+        }
+}
+}
+
+extern "C" {
+// derived_generic (device form) against derived_basis (reference order): number of mismatching bits
+int hs_check_derived(void)
+{
+    using namespace ggp;
+    int bad = 0;
+    for (int trial = 0; trial < 1000; ++trial) {
+        double X[NX];
+        for (int k = 0; k < NX; ++k) X[k] = exp(-0.001 * (trial % 97) - 0.01 * k);
+        const double gl = 0.01 + 1e-4 * trial, t = 0.5 + 0.01 * (trial % 13);
+        for (int j = 0; j < kNDerived; ++j) {
+            const double a = derived_basis(j, X, gl, t), b = derived_generic(kDerived[j], X, gl, t);
+            if (memcmp(&a, &b, 8)) ++bad;
+        }
+    }
+    return bad;
+}
+}
