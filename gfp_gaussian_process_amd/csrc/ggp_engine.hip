@@ -30,6 +30,7 @@
 #include "ggp_device.h"
 #include "ggp_prop.h"
 #include "ggp_outtab.h"
+#include "ggp_wave.h"
 #include "ggp_predict.h"
 #include "ggp_joints.h"
 
@@ -351,21 +352,21 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 
 
 // ------------------------------------------------------------------------------------------
-// WAVE schedule: one 64-lane wave per cell with every stage of the step spread over the
-// lanes -- the 74 exponentials + 14 Dawson values + 3 powers, the 45 integrals in one
-// branch-free form (ggp::tau_unified) + the 18 exp-derived basis values on the spare lanes,
-// the outputs as the sparse trilinear form of ggp_outtab.h (59 lanes x 4 terms, summed by a
-// DPP butterfly inside power-of-two lane blocks and broadcast by readlane) -- and the Kalman
-// update redundantly in all lanes (the state stays in registers).  The log of the ll term is
-// off the critical path: det and the quadratic form go to an LDS ring, and every 64 rows (or
-// at the cell's end) 64 lanes take the logs at once and one lane adds the terms in row order
+// WAVE schedule: one 64-lane wave per cell, every stage of a step spread over the lanes
+// (ggp_wave.h): one exponential, one Dawson value and one power per lane, then one integral
+// per lane, then the outputs as the sparse trilinear form of ggp_outtab.h (59 lanes x 4
+// terms, summed by a DPP butterfly inside power-of-two lane blocks and broadcast through
+// LDS); the Kalman update runs redundantly in all lanes (the state stays in registers).
+// Every stage is straight-line code (ggp_wave.h says why).  What depends on the parameters
+// and dt only -- exp(s t) and the 18 exp-derived basis values of the outputs -- is formed
+// when dt changes and kept in LDS.  The determinant and log of the ll term are off the
+// critical path: q and S go to an LDS ring, and every 64 rows (or at the cell's end) 64
+// lanes take the determinants and logs at once and one lane adds the terms in row order
 // (the reference's summation order; the first NaN row is found there).
-// The outputs are the same polynomial as ggp::outputs summed in another order, so results
-// agree with the lane/group schedules to ~1e-10 relative on the total, not bitwise
-// (DESIGN.md "Parity").
+// The outputs are the same polynomial as ggp::outputs summed in another order, and four
+// exp(c) are products of exponentials, so results agree with the lane/group schedules to
+// ~1e-10 relative on the total, not bitwise (DESIGN.md "Parity").
 // ------------------------------------------------------------------------------------------
-constexpr int kWaveSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::BV_N + ggp::V_N + ggp::SB_N;
-
 template <int CTRL>
 GGP_DEV double dpp_f64(const double v)
 {
@@ -384,19 +385,16 @@ GGP_DEV double readlane_f64(const double v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-template <size_t... K>
-GGP_DEV void wave_outputs(const double v, double *o, std::index_sequence<K...>)
-{
-    ((o[K] = readlane_f64<ggp::kOutLead[K]>(v)), ...);
-}
-
-// ll terms of rows [base, base + n) from the LDS ring into cl, in row order; false at the
-// first NaN (nan_row set)
-GGP_DEV bool wave_flush_ll(const double *ring_q, const double *ring_det, double *ring_t, const int n,
+// ll terms of rows [base, base + n) from the LDS ring into cl, in row order (ggp_ll_term:
+// q - 0.5 log(det S) - 2 log(2 pi)); false at the first NaN (nan_row set)
+GGP_DEV bool wave_flush_ll(const double *ring_q, const double (*ring_s)[64], double *ring_t, const int n,
                            const int64_t base, const double two_log_2pi, const int lane, double &cl, int &nan_row)
 {
     __syncthreads();
-    if (lane < n) ring_t[lane] = ring_q[lane] - 0.5 * log(ring_det[lane]) - two_log_2pi;
+    if (lane < n)
+        ring_t[lane] = ring_q[lane] -
+                       0.5 * log(ggp_det_pplu(ring_s[0][lane], ring_s[1][lane], ring_s[2][lane], ring_s[3][lane])) -
+                       two_log_2pi;
     __syncthreads();
     bool ok = true;
     if (lane == 0) {
@@ -413,39 +411,25 @@ GGP_DEV bool wave_flush_ll(const double *ring_q, const double *ring_det, double 
     return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
 }
 
-__global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
                                                     int n, double *__restrict__ state,
                                                     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
 {
-    constexpr int G = 64;
+    namespace W = ggp::wave;
     constexpr int CPW = 8;   // stamp slot 3 (GGP_STAMPS builds only)
-    constexpr int NXB = (ggp::NXT + G - 1) / G;
-    __shared__ double lds[kWaveSlot];
-    __shared__ double s_ou[ggp::OU_N];
+    __shared__ double lds[W::kLds];
     __shared__ double s_tab[kDawsonTab];
-    __shared__ double ring_q[64], ring_det[64], ring_t[64];
+    __shared__ double ring_q[64], ring_s[4][64], ring_t[64];
+    __shared__ double row_l[64], row_f[64], row_t[65];   // this 64-row chunk's data (+ next time)
     const int lane = threadIdx.x;
     load_dawson_table(s_tab, lane);
     const int i = blockIdx.x;
-    double *Xl = lds;
-    double *Dl = Xl + ggp::NX;
-    double *Pl = Dl + ggp::ND;
-    double *Bv = Pl + ggp::NPW;       // [1, I(45), derived(18)]
-    double *Il = Bv + ggp::BV_I;
-    double *Vl = Bv + ggp::BV_N;      // [1, bx, bg, bl - ml, bq - mq, Cxx .. Cqq, t]
-    double *Sb = Vl + ggp::V_N;       // the step block (ggp_prop.h)
-    // this lane's task descriptors (registers for the whole launch)
-    uint32_t xd[NXB];
-#pragma unroll
-    for (int q = 0; q < NXB; ++q) {
-        const int j = lane + q * G;
-        xd[q] = ggp::pack_x(ggp::kXT[j < ggp::NXT ? j : 0]);
-    }
-    const uint32_t dd = ggp::pack_d(ggp::kDT[lane < ggp::ND ? lane : 0]);
-    const ggp::ITask cd = ggp::kIT[lane < ggp::NI ? lane : 0];
-    const ggp::DTaskB dbt = ggp::kDerived[lane >= ggp::NI && lane < ggp::NI + ggp::kNDerived ? lane - ggp::NI : 0];
+    double *Xl = lds + W::L_X, *Dl = lds + W::L_D, *Pl = lds + W::L_P;
+    double *Bv = lds + W::L_BV, *Vl = lds + W::L_V;
+    const W::LaneTasks T = W::lane_tasks(lane);   // this lane's tasks, registers for the launch
     const double *p = P.p;
-    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    const ggp::OU ou = W::pin_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
+    const double var_x = W::pin(p[7]), var_g = W::pin(p[8]), var_dx = W::pin(p[9]), var_dg = W::pin(p[10]);
     double kap[ggp::kOutL];
     ggp::OutTerm tt[ggp::kOutL];
 #pragma unroll
@@ -454,7 +438,6 @@ __global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, c
         kap[q] = ggp::out_kappa(ou, tt[q].kap);
     }
     const int bs = ggp::kOutBlock[lane];
-    if (lane == 0) ggp::store_ou(ou, s_ou);
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
     int c = 0;
     int64_t r = 0, r1 = 0, r0 = 0;
@@ -470,6 +453,22 @@ __global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, c
         divide = pending;
         t_cur = F.time[r0];
     }
+    // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane), so
+    // the step loop issues no global loads and never waits on one
+    auto load_chunk = [&](const int64_t base) {
+        const int64_t rr = base + lane;
+        double a = 0.0, b = 0.0, t = 0.0;
+        if (rr < r1) {
+            a = F.logl[rr];
+            b = F.fp[rr];
+            t = F.time[rr];
+        }
+        row_l[lane] = a;
+        row_f[lane] = b;
+        row_t[lane] = t;
+        if (lane == 0) row_t[64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
+    };
+    if (valid) load_chunk(r0);
     if (lane == 0) {
         Xl[ggp::X_ONE] = 1.0;
         Bv[ggp::BV_ONE] = 1.0;
@@ -478,59 +477,51 @@ __global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, c
     __syncthreads();
     double cl = 0.0;
     int nan_row = kNanNone;
-    int slot = 0;                     // rows in the ll ring
+    int slot = 0;                                                   // rows in the ll ring = row - chunk base
+    double dt_cached = __longlong_as_double(0x7ff8000000000000LL);  // NaN: nothing cached yet
     bool live = valid;
     GGP_STAMP_DECL;
     while (live) {   // the whole workgroup is one cell: uniform
         GGP_STAMP(0);
         GGP_STAMP_STEP();
-        const double y_l = F.logl[r], y_f = F.fp[r];
-        const double t_next = r + 1 < r1 ? F.time[r + 1] : 0.0;
+        const double y_l = row_l[slot], y_f = row_f[slot];
+        const double t_next = r + 1 < r1 ? row_t[slot + 1] : 0.0;
         if (pending) {
-            if (lane == 0) {
-                ggp::Step S;
-                ggp::step_init(S, m, C, dt, ou);
-                ggp::store_step(S, Sb);
-                const double v[ggp::V_N - 1] = {S.bx, S.bg, S.bl - S.ml, S.bq - S.mq, S.Cxx, S.Cxg, S.Cxl, S.Cxq,
-                                                S.Cgg, S.Cgl, S.Cgq, S.Cll, S.Clq, S.Cqq, S.t};
-#pragma unroll
-                for (int k = 0; k < ggp::V_N - 1; ++k) Vl[1 + k] = v[k];
+            ggp::Step S;
+            ggp::step_init(S, m, C, dt, ou);   // every lane: the same step scalars, in registers
+            if (lane == 0) W::store_v(S, Vl);
+            if (__builtin_amdgcn_readfirstlane(dt == dt_cached ? 0 : 1)) {
+                // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
+                lds[T.xs_dst] = exp(ggp::pickSV(S, T.sv) * S.t);
+                __syncthreads();
+                lds[T.dv_dst] = ggp::derived_generic(T.dv, Xl, ou.gl, S.t);
+                __syncthreads();
+                dt_cached = dt;
             }
             GGP_STAMP(1);
-            __syncthreads();
+            {   // stage B: one exponential, one Dawson value, one power per lane
+                const double ev = exp(W::exp_arg(S, T));
+                const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
+                const double pw = W::pow_bf(S, T.p);
+                const double rpw = 1.0 / pw;
+                lds[T.x_dst] = ev;
+                lds[T.d_dst] = dv;
+                lds[T.p_dst0] = pw;
+                lds[T.p_dst1] = rpw;
+                lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
+            }
             GGP_STAMP(2);
-            const ggp::StepL S(Sb);
-            {   // exponentials, Dawson values, powers
-                double ev[NXB];
-#pragma unroll
-                for (int q = 0; q < NXB; ++q) ev[q] = ggp::exp_body(S, ggp::unpack_x(xd[q]));
-                const double dv = ggp::dawson_body(S, ggp::unpack_d(dd), s_tab);
-                const double pw = ggp::pow_task(S, lane < 3 ? lane : 0);
-#pragma unroll
-                for (int q = 0; q < NXB; ++q)
-                    if (lane + q * G < ggp::NXT) Xl[lane + q * G] = ev[q];
-                if (lane < ggp::ND) Dl[lane] = dv;
-                if (lane < 3) {
-                    Pl[lane] = pw;
-                    Pl[3 + lane] = 1.0 / pw;
-                }
-            }
+            __syncthreads();
             GGP_STAMP(3);
-            __syncthreads();
+            lds[T.i_dst] = W::tau_bf(S, T.it, T.i_km, T.i_ks, Xl, Dl, Pl);   // stage C: one integral per lane
             GGP_STAMP(4);
-            if (lane < ggp::NI) {   // the integrals
-                Il[lane] = ggp::tau_unified(S, cd, Xl, Dl, Pl);
-            } else if (lane < ggp::NI + ggp::kNDerived) {   // the exp-derived basis values
-                Bv[ggp::BV_R_EBT + lane - ggp::NI] = ggp::derived_generic(dbt, Xl, ou.gl, S.t);
-            }
-            GGP_STAMP(5);
             __syncthreads();
-            GGP_STAMP(6);
-            double acc = 0.0;   // this lane's output terms
+            GGP_STAMP(5);
+            double acc = 0.0;   // stage D: this lane's output terms
 #pragma unroll
             for (int q = 0; q < ggp::kOutL; ++q)
                 acc = acc + (((kap[q] * Vl[tt[q].v1]) * Vl[tt[q].v2]) * Vl[tt[q].v3]) * Bv[tt[q].basis];
-            GGP_STAMP(7);
+            GGP_STAMP(6);
             {   // block sums: DPP butterfly (ggp::out_partner)
                 double w;
                 w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
@@ -538,27 +529,33 @@ __global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, c
                 w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
                 w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
             }
-            GGP_STAMP(8);
+            lds[T.out_dst] = acc;   // block sums to LDS, read back by every lane
+            GGP_STAMP(7);
+            __syncthreads();
             double o[ggp::kOutN];
-            wave_outputs(acc, o, std::make_index_sequence<ggp::kOutN>{});
+#pragma unroll
+            for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
             ggp::out_finish([&](int k) { return o[k]; }, o);
             ggp::out_store(o, m, C);
             if (divide) {
-                ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
                 divide = false;
             }
-            GGP_STAMP(9);
+            GGP_STAMP(8);
         }
         const double x0 = y_l - m[0];
         const double x1 = y_f - m[1];
         ggp_innov v;
-        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
-        {   // the ll term without its log (ggp_ll_term), into the ring
+        ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
+        {   // the ll term without its determinant and log (ggp_ll_term), into the ring
             const double h0 = -0.5 * x0, h1 = -0.5 * x1;
             const double q = (h0 * v.si00 + h1 * v.si10) * x0 + (h0 * v.si01 + h1 * v.si11) * x1;
             if (lane == 0) {
                 ring_q[slot] = q;
-                ring_det[slot] = ggp_det_pplu(v.S00, v.S01, v.S10, v.S11);
+                ring_s[0][slot] = v.S00;
+                ring_s[1][slot] = v.S01;
+                ring_s[2][slot] = v.S10;
+                ring_s[3][slot] = v.S11;
             }
         }
         ++slot;
@@ -568,14 +565,15 @@ __global__ __launch_bounds__(64) void k_loglik_wave(DevForest F, ggp_params P, c
         t_cur = t_next;
         ++r;
         live = r < r1;
-        GGP_STAMP(10);
+        GGP_STAMP(9);
         if (slot == 64 || !live) {
-            if (!wave_flush_ll(ring_q, ring_det, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
+            if (!wave_flush_ll(ring_q, ring_s, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
                 break;
             slot = 0;
+            if (live) load_chunk(r);
         }
         __syncthreads();   // LDS slots are rewritten by the next step
-        GGP_STAMP(11);
+        GGP_STAMP(10);
     }
     GGP_STAMP_FLUSH();
     if (valid && lane == 0) {
@@ -1029,6 +1027,7 @@ struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0;
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
+    int auto_small = GGP_KERNEL_WAVE;   // auto's schedule for small levels
     int64_t group_max_cells = 2048;   // auto: group schedule for levels up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int kernel_used = GGP_KERNEL_LANE;
@@ -1078,9 +1077,14 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof], f->stream));
         }
         const int64_t n_simd = (int64_t)f->n_cu * 4;
-        const bool group = f->kernel_pref == GGP_KERNEL_GROUP ||
-                           (f->kernel_pref == GGP_KERNEL_AUTO && n <= f->group_max_cells);
-        if (f->kernel_pref == GGP_KERNEL_WAVE) {
+        // auto: levels of at most two cells per SIMD take the latency schedule (wave by
+        // default, GGP_AUTO_SMALL=group for the bitwise-lane-equal one), larger levels the lane
+        // schedule (measured crossover)
+        const int kind = f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
+                         : n <= f->group_max_cells         ? f->auto_small
+                                                           : GGP_KERNEL_LANE;
+        const bool group = kind == GGP_KERNEL_GROUP;
+        if (kind == GGP_KERNEL_WAVE) {
             hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
                                f->d_state, f->d_cell_ll, f->d_cell_nan);
             f->kernel_used = GGP_KERNEL_WAVE;
@@ -1275,6 +1279,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
         f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     int rc = GGP_OK;
     auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
     check(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? GGP_OK : GGP_EDEV);

@@ -71,12 +71,12 @@ typedef struct {
     int32_t division_binomial;   /* 1 = "binomial" (default), 0 = "gauss"            */
     double fp_auto;              /* CSVconfig::fp_auto                               */
     int32_t device;              /* HIP device ordinal                               */
-    int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (results identical) */
+    int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
 } ggp_forest_desc;
 
-#define GGP_KERNEL_AUTO 0     /* pick by occupancy                                   */
+#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 2 cells per SIMD, else LANE   */
 #define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
-#define GGP_KERNEL_GROUP 2    /* one workgroup per cell (latency)                    */
+#define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
 #define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);
                                  agrees with LANE/GROUP to ~1e-10, not bitwise        */
 

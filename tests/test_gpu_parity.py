@@ -33,13 +33,19 @@ def example_forests(example_paths):
     return out
 
 
+# every schedule against the oracle: lane (throughput), group (latency, bitwise = lane), wave
+# (latency; outputs summed in another order and four exp(c) formed as products, ~1e-10)
+KERNELS = ["lane", "group", "wave"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("noise,div,params", CONFIGS, ids=[f"{a}-{b}" for a, b, _ in CONFIGS])
-def test_example_carried_state_chain(example_forests, noise, div, params):
+def test_example_carried_state_chain(example_forests, noise, div, params, kernel):
     """fresh call + two calls on carried root state (predictions.h:63-78), vs the oracle"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = example_forests[(noise, div)]
-    fg = g.Forest(hf)
+    fg = g.Forest(hf, kernel=kernel)
     of = O.OracleForest(hf.a)
     for call in range(3):
         vg = fg.total_likelihood(params)
@@ -48,12 +54,13 @@ def test_example_carried_state_chain(example_forests, noise, div, params):
         assert _rel(vg, vo) < REL, (call, vg, vo)
 
 
-def test_example_state_matches_oracle(example_forests):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_example_state_matches_oracle(example_forests, kernel):
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = example_forests[("scaled", "binomial")]
     P = CONFIGS[0][2]
-    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
     for _ in range(2):
         fg.total_likelihood(P)
         of.total_likelihood(P)
@@ -83,7 +90,8 @@ def test_reset_state_and_determinism(example_forests):
     assert a.total_likelihood(P) == second
 
 
-def test_nan_reported_like_reference(example_forests):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_nan_reported_like_reference(example_forests, kernel):
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = example_forests[("scaled", "binomial")]
@@ -91,18 +99,20 @@ def test_nan_reported_like_reference(example_forests):
     P[2] = -1.0                                       # var_lambda < 0: sqrt(a<0) in the propagator
     _, oc, orow = O.OracleForest(hf.a).total_likelihood(P)
     with pytest.raises(g.LikelihoodIsNan) as e:
-        g.Forest(hf).total_likelihood(P)
+        g.Forest(hf, kernel=kernel).total_likelihood(P)
     assert (e.value.cell, e.value.row) == (oc, orow)
     assert e.value.cell_id == hf.ids[oc]
 
 
-@pytest.mark.parametrize("n_trees,rows", [(1000, 200), (37, 4), (5, 9)])
-def test_synthetic_forest_vs_oracle(n_trees, rows):
+@pytest.mark.parametrize("kernel", ["auto"] + KERNELS)
+@pytest.mark.parametrize("n_trees,rows", [(1000, 200), (37, 4), (5, 9), (3, 300)])
+def test_synthetic_forest_vs_oracle(n_trees, rows, kernel):
+    """(3, 300): 150-row roots cross the wave schedule's 64-row chunks and ll ring twice"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = g.HostForest.synthetic(n_trees, rows)
     P = CONFIGS[0][2]
-    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
     for _ in range(2):
         vg = fg.total_likelihood(P)
         vo = of.total_likelihood(P)[0]
@@ -132,19 +142,22 @@ def _ragged_roots(n_cells=40, seed=3):
     return g.HostForest(a)
 
 
-def test_single_cells_and_ragged_rows():
-    """1-row cells (no propagation) and dt = 2 steps (t != 1 exercises every t-power term)"""
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_single_cells_and_ragged_rows(kernel):
+    """1-row cells (no propagation) and dt = 2 steps (t != 1 exercises every t-power term and
+    the wave schedule's per-dt cache)"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = _ragged_roots()
     assert np.any(np.diff(hf.a["time"]) == 2.0) and np.any(np.diff(hf.a["row_offset"]) == 1)
     P = CONFIGS[0][2]
-    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
     for _ in range(2):
         assert _rel(fg.total_likelihood(P), of.total_likelihood(P)[0]) < REL
 
 
-def test_rescaled_time_units():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_rescaled_time_units(kernel):
     """time in hours (rescale_time = 60): dt = 1/60, a non-integer step"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
@@ -155,7 +168,7 @@ def test_rescaled_time_units():
         P[i] *= 60.0 if i in (0, 1, 4, 6) else 1.0
     P[2] *= 60.0 ** 3
     P[5] *= 60.0
-    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
     vg, vo = fg.total_likelihood(P), of.total_likelihood(P)[0]
     assert math.isfinite(vo) and _rel(vg, vo) < REL
 
