@@ -7,10 +7,13 @@
 //   -s  run_bound_1dscan      main.cpp:80-114
 //   -p  run_prediction_segments main.cpp:117-146 (write_predictions_to_file)
 //   -e  additive: one total log-likelihood at the parameter files' values
-//   -j  joints (correlation_tree.h) are not built in this version: the flag is rejected.
+//   -j  run_joint_distribution  main.cpp:150-186 (collect_joint_distributions' dense joint
+//                                matrix, correlation_tree.h:9-23, 96-126, 588-648, 786-791);
+//                                as in the reference, -j implies -p (main.cpp:265-268)
 //
 // Output text is produced with the same iostream manipulators as the reference, so the files
 // are byte-identical given identical numbers.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -23,6 +26,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ggp.h"
@@ -491,6 +495,147 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     }
 }
 
+// ---- -j (main.cpp:150-186; correlation_tree.h:9-23, 96-126, 588-648, 786-791) -------------
+// The reference writes one dense line per start row (cells in input order, rows in time
+// order): for every row of the forest -- a column, labelled cell_id_time -- either the joint
+// P(z_column, z_start | D) as 8 means and the 36-entry upper triangle of its covariance, or
+// 44 empty fields.  Joint_vector::add stores a joint in every column whose (cell_id, time)
+// equals the target's, the last add winning.  The joints come from the GPU (ggp_joints) in
+// the reference's add order, a bounded range of start rows per call.
+void output_values(std::ostream &file, const double *v, int n)   // output_vector (predictions.h:553-560)
+{
+    for (int k = 0; k < n; ++k) {
+        if (k > 0) file << ",";
+        file << v[k];
+    }
+}
+
+void output_upper(std::ostream &file, const double *C, int n)    // output_upper_triangle (predictions.h:540-551)
+{
+    for (int m = 0; m < n; ++m)
+        for (int k = m; k < n; ++k) {
+            if (k + m > 0) file << ",";
+            file << C[n * m + k];
+        }
+}
+
+void write_commas(std::ostream &file, int64_t count)
+{
+    static const std::string block(44 * 1024, ',');
+    while (count > 0) {
+        const int64_t k = std::min<int64_t>(count, (int64_t)block.size());
+        file.write(block.data(), (std::streamsize)k);
+        count -= k;
+    }
+}
+
+void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::string, std::string> &args)
+{
+    g_log << "-> joint posteriors" << "\n";
+    std::string outfile = out_dir(args) + file_base(args["infile"]);
+    for (const Params &P : plist) outfile += outfile_param_code(P);
+    outfile += "_joints.csv";
+    Forest F;
+    build_forest(F, d, -1, args["noise_model"], args["cell_division_model"]);
+    std::vector<double> pv;
+    for (const Params &P : plist) {
+        const auto v = P.get_final();
+        pv.insert(pv.end(), v.begin(), v.end());
+    }
+    const double tol = std::stod(args["rel_tolerance_joints"]);
+    const int64_t nr = F.desc.n_rows, nc = F.desc.n_cells;
+    const double *time = F.desc.time;
+    std::vector<int64_t> row_cell((size_t)nr);
+    for (int64_t c = 0; c < nc; ++c)
+        for (int64_t r = F.desc.row_offset[c]; r < F.desc.row_offset[c + 1]; ++r) row_cell[(size_t)r] = c;
+    // columns sharing a (cell_id, time) key: get_column_indices + Joint_vector::add
+    std::vector<int32_t> dup((size_t)nr, -1);
+    std::vector<std::vector<int64_t>> groups;
+    {
+        std::unordered_map<std::string, int64_t> first;
+        first.reserve((size_t)nr);
+        for (int64_t r = 0; r < nr; ++r) {
+            const double t = time[r] + 0.0;   // -0 == +0, as the reference's double == compares
+            std::string key = ggp_host_forest_cell_id(F.host, row_cell[(size_t)r]);
+            key.push_back('\0');
+            key.append(reinterpret_cast<const char *>(&t), sizeof t);
+            const auto ins = first.emplace(std::move(key), r);
+            if (ins.second) continue;
+            const int64_t f0 = ins.first->second;
+            if (dup[(size_t)f0] < 0) {
+                dup[(size_t)f0] = (int32_t)groups.size();
+                groups.push_back({f0});
+            }
+            dup[(size_t)r] = dup[(size_t)f0];
+            groups[(size_t)dup[(size_t)f0]].push_back(r);
+        }
+    }
+    g_log << "Outfile: " << outfile << "\n";
+    std::ofstream file(outfile);
+    for (const Params &P : plist) P.to_csv(file);   // setup_outfile_joints
+    file << "\ncell_id,parent_id,time";
+    file << ",";                                     // write_column_indices
+    for (int64_t r = 0; r < nr; ++r) {
+        file << ggp_host_forest_cell_id(F.host, row_cell[(size_t)r]) << '_' << time[r];
+        write_commas(file, r == nr - 1 ? 43 : 44);
+    }
+    file << "\n";
+    const int64_t max_cap = (int64_t)1 << 21;        // joints per call (72 doubles each)
+    int64_t cap = (int64_t)1 << 14, chunk = 4096;
+    std::vector<int64_t> idx((size_t)(2 * cap));
+    std::vector<double> val((size_t)(72 * cap));
+    std::map<int64_t, int64_t> cols;                 // column -> joint, the last add wins
+    int64_t logged = -1;
+    for (int64_t lo = 0; lo < nr;) {
+        const int64_t hi = std::min(nr, lo + chunk);
+        int64_t n_out = 0;
+        const int rc = ggp_joints(F.gpu, pv.data(), (int32_t)plist.size(), tol, lo, hi, cap, idx.data(), val.data(),
+                                  &n_out);
+        if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_joints: ") + ggp_strerror(rc));
+        if (n_out > cap) {   // buffers too small: split the range, or grow them
+            if (n_out > max_cap && hi - lo > 1) {
+                chunk = std::max<int64_t>(1, (hi - lo) / 2);
+            } else {
+                cap = n_out;
+                idx.resize((size_t)(2 * cap));
+                val.resize((size_t)(72 * cap));
+            }
+            continue;
+        }
+        int64_t k = 0;
+        for (int64_t s = lo; s < hi; ++s) {          // sc_joint_distributions: one line per start row
+            const int64_t c = row_cell[(size_t)s];
+            if (c != logged) {
+                g_log << "-> cell: " << c << "\n";
+                logged = c;
+            }
+            cols.clear();
+            for (; k < n_out && idx[(size_t)(2 * k)] == s; ++k) {
+                const int64_t tgt = idx[(size_t)(2 * k + 1)];
+                if (dup[(size_t)tgt] < 0)
+                    cols[tgt] = k;
+                else
+                    for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) cols[col] = k;
+            }
+            file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
+                 << time[s];
+            int64_t prev = 0;
+            for (const auto &e : cols) {             // Joint_vector::write
+                write_commas(file, 44 * (e.first - prev));
+                const double *j = &val[(size_t)(72 * e.second)];
+                file << ",";
+                output_values(file, j, 8);
+                file << ",";
+                output_upper(file, j + 8, 8);
+                prev = e.first + 1;
+            }
+            write_commas(file, 44 * (nr - prev));
+            file << "\n";
+        }
+        lo = hi;
+    }
+}
+
 // ---- main.cpp:148-345 arg_parser ------------------------------------------------------------
 std::map<std::string, std::string> arg_parser(int argc, char **argv)
 {
@@ -628,8 +773,6 @@ int main(int argc, char **argv)
             g_log << P << "\n";
             plist.push_back(P);
         }
-        if (args.count("joints"))
-            throw std::invalid_argument("-j (joint distributions) is not built in this version");
 
         const char *cfg_path = args.count("csv_config") ? args["csv_config"].c_str() : "";
         if (ggp_csv_config_load(cfg_path, &cfg) != GGP_OK) throw std::invalid_argument(ggp_host_last_error());
@@ -676,6 +819,7 @@ int main(int argc, char **argv)
             }
         }
         if (args.count("predict")) run_prediction(data, plist, args);
+        if (args.count("joints")) run_joints(data, plist, args);   // after -p (main.cpp:440-443)
 
         g_log << "Done." << std::endl;
         std::cout << "Done. Log file: " << outfile_log_success << std::endl;

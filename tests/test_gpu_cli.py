@@ -1,5 +1,5 @@
 """The CLI (lib/ggp, the reference's main.cpp surface) on the GPU against the CPU oracle:
--e, -s, -p and -m on the reference's example data set.
+-e, -s, -p and -m on the reference's example data set, -j on a small synthetic forest.
 
 Tolerances: log-likelihood values 1e-9 relative (the north-star bar); -p values are printed
 with 6 significant digits by the reference's writer, so they are compared after parsing at
@@ -137,3 +137,71 @@ def test_cli_minimize_matches_oracle_trajectory(tmp_path, example_paths, oracle_
     assert abs(fl - ll) / abs(ll) < 1e-8
     pfile = open(str(base) + "_parameter_file.txt").read()
     assert pfile.startswith("# Generated parameter file")
+
+
+def _small_csv(path, n_trees=2, rows=40):
+    """a small synthetic forest in the example's column layout (lane 1, integer cell ids)"""
+    import math
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(n_trees, rows)
+    a = hf.a
+    ro, par = a["row_offset"], a["parent"]
+    with open(path, "w") as f:
+        f.write(",cell_id,time_min,parent_id,lane,length,gfp\n")
+        k = 0
+        for c in range(hf.n_cells):
+            pid = int(par[c]) + 11 if par[c] >= 0 else 7       # roots: parent 7 is not in the data
+            for r in range(ro[c], ro[c + 1]):
+                t, ln, fp = float(a["time"][r]), math.exp(float(a["log_length"][r])), float(a["fp"][r])
+                f.write(f"{k},{c + 11},{t!r},{pid},1,{ln!r},{fp!r}\n")
+                k += 1
+    return str(path)
+
+
+def test_cli_joints_dense_matrix(tmp_path, example_paths):
+    """-j (implies -p): the reference's dense joint matrix (correlation_tree.h:96-126,
+    588-648) against the engine's joints (ggp_joints, checked against the oracle in
+    test_gpu_joints.py): column labels, one line per start row, 44 fields per column, the
+    joint's 8 means and upper triangle where the walk reached the column, empty elsewhere.
+    Values are printed with 6 significant digits (default stream precision)."""
+    import gfp_gaussian_process_amd as g
+    csv = _small_csv(tmp_path / "small.csv")
+    pf = _param_file(tmp_path / "p.txt", {})
+    out = tmp_path / "o"
+    _run(["-i", csv, "-b", pf, "-c", example_paths["config"], "-j", "-o", str(out)], tmp_path)
+    assert (out / "small_f_b_prediction.csv").exists()
+    text = (out / "small_f_b_joints.csv").read_text()
+    head, body = text.split("\ncell_id,parent_id,time,", 1)
+    assert head.startswith("no,name,type,init,step,lower_bound,upper_bound,final\n0,mean_lambda,fixed,")
+    lines = body.split("\n")
+    assert lines[-1] == ""
+    hdr, rows = lines[0].split(","), lines[1:-1]
+    hf = g.HostForest.from_csv(csv, example_paths["config"])
+    n = hf.n_rows
+    cell = np.repeat(np.arange(hf.n_cells), np.diff(hf.a["row_offset"]))
+    assert len(hdr) == 44 * n and len(rows) == n
+    assert hdr[::44] == [f"{hf.ids[cell[r]]}_{hf.a['time'][r]:g}" for r in range(n)]
+    assert all(x == "" for k, x in enumerate(hdr) if k % 44)
+    ig, vg = g.Forest(hf).joints(INIT, 1e-10)
+    want = {}
+    for (s, t), v in zip(ig.tolist(), vg):
+        want.setdefault(s, {})[t] = v
+    assert len(want) > n // 2
+    iu = np.triu_indices(8)
+    for s, line in enumerate(rows):
+        f = line.split(",")
+        assert len(f) == 3 + 44 * n, s
+        assert f[0] == hf.ids[cell[s]] and f[1] == hf.parent_ids[cell[s]]
+        assert float(f[2]) == pytest.approx(hf.a["time"][s], rel=1e-5)
+        got = {}
+        for col in range(n):
+            blk = f[3 + 44 * col: 3 + 44 * (col + 1)]
+            if blk[0] == "":
+                assert all(x == "" for x in blk), (s, col)
+                continue
+            got[col] = np.array([float(x) for x in blk])
+        exp = want.get(s, {})
+        assert set(got) == set(exp), s
+        for col, v in got.items():
+            ref = np.concatenate([exp[col][:8], exp[col][8:].reshape(8, 8)[iu]])
+            assert np.allclose(v, ref, rtol=1e-5, atol=0), (s, col)
