@@ -1028,7 +1028,8 @@ struct ggp_forest {
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
     int auto_small = GGP_KERNEL_WAVE;   // auto's schedule for small levels
-    int64_t group_max_cells = 2048;   // auto: group schedule for levels up to this size
+    int64_t wave_max_cells = 3072;    // auto: wave schedule for levels up to this size
+    int64_t group_max_cells = 8192;   // auto: group schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
@@ -1077,11 +1078,12 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof], f->stream));
         }
         const int64_t n_simd = (int64_t)f->n_cu * 4;
-        // auto: levels of at most two cells per SIMD take the latency schedule (wave by
-        // default, GGP_AUTO_SMALL=group for the bitwise-lane-equal one), larger levels the lane
-        // schedule (measured crossover)
+        // auto (measured, profiles/r04_schedule_scan.txt): up to 3 cells per SIMD the wave
+        // schedule (GGP_AUTO_SMALL=group: the bitwise-lane-equal one), up to 8 per SIMD the
+        // group schedule with 1-8 cells per wave, above that the lane schedule
         const int kind = f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
-                         : n <= f->group_max_cells         ? f->auto_small
+                         : n <= f->wave_max_cells          ? f->auto_small
+                         : n <= f->group_max_cells         ? GGP_KERNEL_GROUP
                                                            : GGP_KERNEL_LANE;
         const bool group = kind == GGP_KERNEL_GROUP;
         if (kind == GGP_KERNEL_WAVE) {
@@ -1094,7 +1096,6 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
             int cpw = 1;
             while (cpw < 8 && (n + cpw - 1) / cpw > n_simd) cpw *= 2;
-            if (f->kernel_pref == GGP_KERNEL_AUTO) cpw = std::min(cpw, 2);
             if (f->tune_group_cpw > 0) cpw = f->tune_group_cpw;
             const int blocks = (n + cpw - 1) / cpw;
             switch (cpw) {
@@ -1272,7 +1273,9 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess) f->n_cu = prop.multiProcessorCount;
-    f->group_max_cells = (int64_t)f->n_cu * 4 * 2;
+    f->wave_max_cells = (int64_t)f->n_cu * 4 * 3;
+    f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
+    if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
     if (const char *e = getenv("GGP_GROUP_CPW")) {
         const int v = atoi(e);

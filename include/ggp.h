@@ -74,7 +74,8 @@ typedef struct {
     int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
 } ggp_forest_desc;
 
-#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 2 cells per SIMD, else LANE   */
+#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 3 cells per SIMD, GROUP up to
+                                 8, LANE above (measured crossovers)       */
 #define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
 #define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
 #define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);

@@ -16,4 +16,4 @@ python3 tools/pmc_traffic.py gpurun_out/pmcf_${TAG} gpurun_out/pmcw_${TAG} gpuru
 mkdir -p profiles && cp gpurun_out/traffic_${TAG}.json profiles/traffic.json
 timeout -k 10 300 python bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; cat gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
-find gpurun_out/prof_${TAG} -name "*stats*" | head
+find gpurun_out/prof_${TAG} -name "*stats*"

@@ -26,7 +26,7 @@ def per_kernel(d, counter):
 def short(name):
     if "k_loglik_group<" in name:
         return "k_loglik_group<" + name.split("k_loglik_group<")[1].split(">")[0] + ">"
-    for k in ("k_loglik_level", "k_reduce", "k_fwd_level", "k_bwd_level", "k_combine"):
+    for k in ("k_loglik_wave", "k_loglik_level", "k_reduce", "k_fwd_level", "k_bwd_level", "k_combine"):
         if k in name:
             return k
     return name[:40]
