@@ -9,6 +9,10 @@ partials are summed in rank order so the result is bitwise reproducible run to r
 The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
 Scan samples and optimiser steps stay sequential (carried state), only the forest is
 parallel.
+
+-p shards the same way (ShardedPredictor): the smoother has no term across trees either,
+so every rank smooths its own trees with no collective on the data path; one gather at
+the end assembles the rows in input order on one rank (or each rank writes its own rows).
 """
 from __future__ import annotations
 
@@ -116,3 +120,67 @@ class ShardedObjective:
             raise err if (err is not None and nan_rank == self.dist.get_rank(self.group)) else \
                 LikelihoodIsNan(-1, -1, f"rank {nan_rank}")
         return total
+
+
+def shard_rows(hf: HostForest, rank: int, world: int):
+    """rank's whole-tree sub-forest and the input-order index of each of its rows"""
+    sub = shard(hf, rank, world)
+    return sub, sub.rows
+
+
+class ShardedPredictor:
+    """-p over a forest sharded by whole trees.
+
+    prediction_forward / prediction_backward / combine_predictions (predictions.h:166-173,
+    438-444, 466-499) run cell by cell, parent to daughter and back; no term crosses a tree.
+    So every rank runs the smoother over its own trees on its own GPU (no collective on the
+    data path) and predict() returns this rank's rows; gather() assembles [n_rows, 20] in
+    input order on rank `dst` with one gather of per-rank blocks (padded to the largest).
+
+    predictor: this rank's Forest (or any object with .predict(params_per_segment)).
+    rows: input-order index of each local row (HostForest.rows of the shard).
+    """
+
+    def __init__(self, predictor, rows, n_rows: int, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.p = predictor
+        self.rows = np.asarray(rows, np.int64)
+        self.n_rows = int(n_rows)
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        self.dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                                      if backend == "nccl" else torch.device("cpu"))
+
+    def predict(self, params_per_segment):
+        """this rank's (forward, backward, combined) rows, [len(rows), 20] each"""
+        return self.p.predict(params_per_segment)
+
+    def gather(self, local, dst: int = 0):
+        """assemble one [len(rows), 20] block per rank into input order on rank dst (None elsewhere)"""
+        import torch
+        local = np.asarray(local, np.float64)
+        if self.world == 1:
+            out = np.empty((self.n_rows, local.shape[1]))
+            out[self.rows] = local
+            return out
+        n = torch.tensor([len(self.rows)], dtype=torch.int64, device=self.dev)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(x.item()) for x in sizes]
+        mx = max(sizes)
+        buf = torch.zeros((mx, 1 + local.shape[1]), dtype=torch.float64, device=self.dev)
+        buf[: len(self.rows), 0] = torch.from_numpy(self.rows.astype(np.float64))   # exact below 2**53
+        buf[: len(self.rows), 1:] = torch.from_numpy(local)
+        rank = self.dist.get_rank(self.group)
+        parts = [torch.empty_like(buf) for _ in range(self.world)] if rank == dst else None
+        self.dist.gather(buf, parts, dst=dst, group=self.group)
+        if rank != dst:
+            return None
+        out = np.empty((self.n_rows, local.shape[1]))
+        for k, part in zip(sizes, parts):
+            a = part[:k].cpu().numpy()
+            out[a[:, 0].astype(np.int64)] = a[:, 1:]
+        return out

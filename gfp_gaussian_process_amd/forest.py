@@ -148,10 +148,11 @@ class HostForest:
     """A flattened forest: the reference's std::vector<MOMAdata> after genealogy + init_cells,
     as structure-of-arrays (cells in input order, rows cell-major)."""
 
-    def __init__(self, arrays: dict, ids=None, parent_ids=None):
+    def __init__(self, arrays: dict, ids=None, parent_ids=None, rows=None):
         self.a = arrays
         self.ids = ids
         self.parent_ids = parent_ids
+        self.rows = rows          # subset_trees: each row's index in the full forest
 
     # -- constructors --
     @classmethod
@@ -250,7 +251,7 @@ class HostForest:
             a[k] = self.a[k][rows]
         ids = [self.ids[i] for i in idx] if self.ids else None
         pids = [self.parent_ids[i] for i in idx] if self.parent_ids else None
-        return HostForest(a, ids, pids)
+        return HostForest(a, ids, pids, rows=np.asarray(rows, np.int64))
 
     def desc(self, device: int = 0, kernel: str = "auto") -> N.ForestDesc:
         a = self.a

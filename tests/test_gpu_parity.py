@@ -207,6 +207,27 @@ def test_shards_on_one_device_sum_to_whole():
         assert _rel(s, w) < 1e-12
 
 
+def test_sharded_predict_on_one_device_equals_whole():
+    """-p sharded by whole trees (distributed.ShardedPredictor), 3 shards on cuda:0 assembled
+    in input order: bitwise equal to the unsharded smoother (same per-cell kernels)"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedPredictor, shard_rows
+    full = g.HostForest.synthetic(300, 60)
+    P = CONFIGS[0][2]
+    want = g.Forest(full).predict(P)
+    got = [np.empty_like(w) for w in want]
+    n = 0
+    for r in range(3):
+        sub, rows = shard_rows(full, r, 3)
+        sp = ShardedPredictor(g.Forest(sub), rows, full.n_rows)
+        for k, part in enumerate(sp.predict(P)):
+            got[k][rows] = part
+        n += len(rows)
+    assert n == full.n_rows
+    for w, x in zip(want, got):
+        assert np.array_equal(w, x)
+
+
 def test_baseline_size_properties():
     """BASELINE C2 / C3 sizes: oracle agreement on C2, additivity + finiteness on C3"""
     import gfp_gaussian_process_amd as g
