@@ -42,6 +42,7 @@ struct DevForest {
     const double *time, *logl, *fp;
     const int64_t *row_off;
     const int32_t *parent, *d1, *d2, *seg;
+    const int32_t *dfs_rank;   // cell -> its position in the DFS order (the reduction's order)
     double root_mean0, root_mean1, root_var0, root_var1;
     double leaf_mean0, leaf_var0, leaf_mean1, leaf_var1;
     double fp_auto, two_log_2pi, log2;
@@ -146,8 +147,8 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
     for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
     for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-    cell_ll[c] = cl;
-    cell_nan[c] = nan_row;
+    cell_ll[F.dfs_rank[c]] = cl;
+    cell_nan[F.dfs_rank[c]] = nan_row;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -345,8 +346,8 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
         for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-        cell_ll[c] = cl;
-        cell_nan[c] = nan_row;
+        cell_ll[F.dfs_rank[c]] = cl;
+        cell_nan[F.dfs_rank[c]] = nan_row;
     }
 }
 
@@ -513,14 +514,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             GGP_STAMP(2);
             __syncthreads();
             GGP_STAMP(3);
+            // stage D's state monomials kappa V1 V2 V3 need no stage-C value: their 12 LDS reads
+            // are issued here, beside stage C, and the products formed after it
+            double vv[ggp::kOutL][3];
+#pragma unroll
+            for (int q = 0; q < ggp::kOutL; ++q) {
+                vv[q][0] = Vl[tt[q].v1];
+                vv[q][1] = Vl[tt[q].v2];
+                vv[q][2] = Vl[tt[q].v3];
+            }
             lds[T.i_dst] = W::tau_bf(S, T.it, T.i_km, T.i_ks, Xl, Dl, Pl);   // stage C: one integral per lane
+            double kv[ggp::kOutL];
+#pragma unroll
+            for (int q = 0; q < ggp::kOutL; ++q) kv[q] = ((kap[q] * vv[q][0]) * vv[q][1]) * vv[q][2];
             GGP_STAMP(4);
             __syncthreads();
             GGP_STAMP(5);
-            double acc = 0.0;   // stage D: this lane's output terms
+            double bv[ggp::kOutL];   // stage D: this lane's output terms; the four reads issue together
 #pragma unroll
-            for (int q = 0; q < ggp::kOutL; ++q)
-                acc = acc + (((kap[q] * Vl[tt[q].v1]) * Vl[tt[q].v2]) * Vl[tt[q].v3]) * Bv[tt[q].basis];
+            for (int q = 0; q < ggp::kOutL; ++q) bv[q] = Bv[tt[q].basis];
+            asm volatile("" ::"v"(bv[0]), "v"(bv[1]), "v"(bv[2]), "v"(bv[3]));
+            static_assert(ggp::kOutL == 4, "stage D issues kOutL reads together");
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < ggp::kOutL; ++q) acc = acc + kv[q] * bv[q];
             GGP_STAMP(6);
             {   // block sums: DPP butterfly (ggp::out_partner)
                 double w;
@@ -582,8 +599,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
         for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-        cell_ll[c] = cl;
-        cell_nan[c] = nan_row;
+        cell_ll[F.dfs_rank[c]] = cl;
+        cell_nan[F.dfs_rank[c]] = nan_row;
     }
 }
 
@@ -958,12 +975,13 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
 // ------------------------------------------------------------------------------------------
 constexpr int kRedThreads = 1024;
 
-__global__ __launch_bounds__(kRedThreads) void k_reduce(const int32_t *__restrict__ dfs_order, int64_t n,
-                                                         const double *__restrict__ cell_ll,
+__global__ __launch_bounds__(kRedThreads) void k_reduce(int64_t n, const double *__restrict__ cell_ll,
                                                          const int32_t *__restrict__ cell_nan,
                                                          double *__restrict__ out_ll,
                                                          int64_t *__restrict__ out_nan)
 {
+    // cell_ll / cell_nan are stored in DFS order (F.dfs_rank): each thread adds a contiguous
+    // chunk in that order, then a fixed pairwise tree over the threads (deterministic)
     __shared__ double s_sum[kRedThreads];
     __shared__ long long s_nan[kRedThreads];
     const int tid = threadIdx.x;
@@ -971,9 +989,8 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(const int32_t *__restric
     double acc = 0.0;
     long long first = 0x7fffffffffffffffLL;
     for (int64_t i = lo; i < hi; ++i) {
-        const int c = dfs_order[i];
-        acc += cell_ll[c];
-        const int nr = cell_nan[c];
+        acc += cell_ll[i];
+        const int nr = cell_nan[i];
         if (nr != kNanNone && first == 0x7fffffffffffffffLL) first = (i << 24) | (long long)nr;
     }
     s_sum[tid] = acc;
@@ -986,7 +1003,7 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(const int32_t *__restric
         }
         __syncthreads();
     }
-    if (tid == 0) {
+    if (tid == 0) {   // straight into mapped host memory (read after the stream synchronises)
         out_ll[0] = s_sum[0];
         out_nan[0] = s_nan[0];
     }
@@ -1038,16 +1055,16 @@ struct ggp_forest {
     double *d_time = nullptr, *d_logl = nullptr, *d_fp = nullptr;
     int64_t *d_row_off = nullptr;
     int32_t *d_parent = nullptr, *d_d1 = nullptr, *d_d2 = nullptr, *d_seg = nullptr;
-    int32_t *d_level_cells = nullptr, *d_dfs_order = nullptr;
+    int32_t *d_level_cells = nullptr, *d_dfs_rank = nullptr;
     int32_t *d_prior_seg = nullptr;   // -p: segment of the stationary prior per row
     int32_t *d_row_cell = nullptr;    // -j: cell of every row
     double *d_state = nullptr, *d_cell_ll = nullptr;
     int32_t *d_cell_nan = nullptr;
-    double *d_out_ll = nullptr;
-    int64_t *d_out_nan = nullptr;
-    // pinned host result
+    // the result: pinned, mapped host memory that k_reduce writes directly (no copy back)
     double *h_out_ll = nullptr;
     int64_t *h_out_nan = nullptr;
+    double *m_out_ll = nullptr;       // device views of the two
+    int64_t *m_out_nan = nullptr;
     // schedule
     std::vector<int64_t> level_start;       // [n_levels+1] into level_cells
     std::vector<int32_t> h_dfs_order;
@@ -1126,11 +1143,8 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             f->n_prof++;
         }
     }
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kRedThreads), 0, f->stream, f->d_dfs_order,
-                       f->n_cells, f->d_cell_ll, f->d_cell_nan, f->d_out_ll, f->d_out_nan);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kRedThreads), 0, f->stream, f->n_cells, f->d_cell_ll, f->d_cell_nan, f->m_out_ll, f->m_out_nan);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(f->h_out_ll, f->d_out_ll, sizeof(double), hipMemcpyDeviceToHost, f->stream));
-    HIPCHK(hipMemcpyAsync(f->h_out_nan, f->d_out_nan, sizeof(int64_t), hipMemcpyDeviceToHost, f->stream));
     return GGP_OK;
 }
 
@@ -1193,12 +1207,10 @@ void ggp_forest_destroy(ggp_forest *f)
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
                     (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
-                    (void *)f->d_level_cells, (void *)f->d_dfs_order, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
-                    (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_out_ll,
-                    (void *)f->d_out_nan})
+                    (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
+                    (void *)f->d_cell_ll, (void *)f->d_cell_nan})
         if (p) (void)hipFree(p);
-    if (f->h_out_ll) (void)hipHostFree(f->h_out_ll);
-    if (f->h_out_nan) (void)hipHostFree(f->h_out_nan);
+    if (f->h_out_ll) (void)hipHostFree(f->h_out_ll);   // one allocation: ll, then the NaN code
     for (auto &e : f->ev) (void)hipEventDestroy(e);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
@@ -1309,7 +1321,11 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     check(dev_upload(&f->d_d2, d->daughter2, nc));
     if (d->segment) check(dev_upload(&f->d_seg, d->segment, nr));
     check(dev_upload(&f->d_level_cells, level_cells.data(), nc));
-    check(dev_upload(&f->d_dfs_order, dfs.data(), nc));
+    {
+        std::vector<int32_t> rank(nc);
+        for (int64_t k = 0; k < nc; ++k) rank[dfs[k]] = (int32_t)k;
+        check(dev_upload(&f->d_dfs_rank, rank.data(), nc));
+    }
     {
         // combine_predictions' prior (predictions.h:475-490): a cell's first row divides by the
         // parameters that initialised it (its own for a root, the parent's last row otherwise)
@@ -1330,11 +1346,19 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     check(dev_upload<double>(&f->d_state, nullptr, (size_t)nc * 20));
     check(dev_upload<double>(&f->d_cell_ll, nullptr, nc));
     check(dev_upload<int32_t>(&f->d_cell_nan, nullptr, nc));
-    check(dev_upload<double>(&f->d_out_ll, nullptr, 1));
-    check(dev_upload<int64_t>(&f->d_out_nan, nullptr, 1));
     if (rc == GGP_OK && nc > 0 && hipMemset(f->d_state, 0, (size_t)nc * 20 * sizeof(double)) != hipSuccess) rc = GGP_EDEV;
-    if (rc == GGP_OK && hipHostMalloc((void **)&f->h_out_ll, sizeof(double)) != hipSuccess) rc = GGP_ENOMEM;
-    if (rc == GGP_OK && hipHostMalloc((void **)&f->h_out_nan, sizeof(int64_t)) != hipSuccess) rc = GGP_ENOMEM;
+    if (rc == GGP_OK) {   // the result slot: 16 B of pinned host memory the reduction writes over the bus
+        void *h = nullptr, *m = nullptr;
+        if (hipHostMalloc(&h, 2 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            rc = GGP_ENOMEM;
+        } else {
+            f->h_out_ll = (double *)h;
+            f->h_out_nan = (int64_t *)((char *)h + sizeof(double));
+            if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) rc = GGP_EDEV;
+            f->m_out_ll = (double *)m;
+            f->m_out_nan = (int64_t *)((char *)m + sizeof(double));
+        }
+    }
     if (rc != GGP_OK) {
         ggp_forest_destroy(f);
         return rc;
@@ -1342,6 +1366,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     DevForest &F = f->F;
     F.time = f->d_time; F.logl = f->d_logl; F.fp = f->d_fp;
     F.row_off = f->d_row_off; F.parent = f->d_parent; F.d1 = f->d_d1; F.d2 = f->d_d2; F.seg = f->d_seg;
+    F.dfs_rank = f->d_dfs_rank;
     F.root_mean0 = d->root_mean_xg[0]; F.root_mean1 = d->root_mean_xg[1];
     F.root_var0 = d->root_var_xg[0]; F.root_var1 = d->root_var_xg[1];
     F.leaf_mean0 = d->leaf_mean_xg[0]; F.leaf_mean1 = d->leaf_mean_xg[1];

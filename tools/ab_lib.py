@@ -1,0 +1,35 @@
+"""A/B timing of engine builds (diagnostic): python tools/ab_lib.py LIB_DIR [kernel] [trees]
+loads libggp.so from LIB_DIR instead of the package's lib/ and prints ms per evaluation of
+C2-shaped forests and the per-level kernel times; run it alternately for two builds."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gfp_gaussian_process_amd import _native  # noqa: E402
+
+_native.LIB_DIR = os.path.abspath(sys.argv[1])
+import gfp_gaussian_process_amd as g  # noqa: E402
+
+kern = sys.argv[2] if len(sys.argv) > 2 else "auto"
+trees = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+P = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]
+hf = g.HostForest.synthetic(trees, 200)
+f = g.Forest(hf, kernel=kern)
+for _ in range(3):
+    v = f.total_likelihood(P)
+reps = 40
+t0 = time.perf_counter()
+for _ in range(reps):
+    f.total_likelihood(P)
+dt = (time.perf_counter() - t0) / reps
+f.enable_profile()
+lv = []
+for _ in range(5):
+    f.total_likelihood(P)
+    lv.append(f.launch_profile()[0])
+import numpy as np
+ms = np.median(np.array(lv), axis=0)
+print(f"{sys.argv[1]} {kern} trees={trees}: {1e3 * dt:.4f} ms/eval  levels " + " ".join(f"{m:.4f}" for m in ms)
+      + f"  ll={v!r}", flush=True)
