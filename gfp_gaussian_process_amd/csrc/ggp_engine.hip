@@ -372,8 +372,9 @@ template <int CTRL>
 GGP_DEV double dpp_f64(const double v)
 {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    // every lane is written (full row/bank masks, in-row patterns): no old value to initialise
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
@@ -504,7 +505,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 const double ev = exp(W::exp_arg(S, T));
                 const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
                 const double pw = W::pow_bf(S, T.p);
-                const double rpw = 1.0 / pw;
+                const double rpw = W::rpow_bf(S, T.p);
                 lds[T.x_dst] = ev;
                 lds[T.d_dst] = dv;
                 lds[T.p_dst0] = pw;
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             }
         }
         ++slot;
-        ggp_posterior(m, C, x0, x1, v);
+        W::posterior(m, C, x0, x1, v, r + 1 == r1);   // lower triangle only on the cell's last row
         pending = r + 1 < r1;
         if (pending) dt = t_next - t_cur;
         t_cur = t_next;

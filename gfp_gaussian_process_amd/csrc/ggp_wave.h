@@ -203,14 +203,22 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     const double t = 2.0 * y100 - (double)(2 * k + 1);
     const double poly =
         pin(c[0] + (c[1] + (c[2] + (c[3] + (c[4] + (c[5] + (c[6] + (c[7] + c[8] * t) * t) * t) * t) * t) * t) * t) * t);
-    const double x2 = ax * ax;
-    const double *tc = ggp_dawson_taylor;
-    const double taylor = pin(ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4])))));
-    const bool far = ax > 5e7;
-    const double num = far ? GGP_ISPI : pin(GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2));
-    const double den = far ? ax : pin(ax * ((ax * ax) * (ax * ax - 5) + 3.75));
-    const double cf = pin(num / den);
-    const double w = ax > 45.0 ? cf : (y100 >= (double)GGP_DAWSON_NINT ? taylor : poly);
+    // the Taylor and continued-fraction branches are rare (|x| < ~0.03, |x| > 45): formed only
+    // when some lane of the wave needs them (a wave-uniform branch; NaN takes neither)
+    const bool use_taylor = y100 >= (double)GGP_DAWSON_NINT, use_cf = ax > 45.0;
+    double taylor = 0.0, cf = 0.0;
+    if (__builtin_amdgcn_ballot_w64(use_taylor)) {
+        const double x2 = ax * ax;
+        const double *tc = ggp_dawson_taylor;
+        taylor = pin(ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4])))));
+    }
+    if (__builtin_amdgcn_ballot_w64(use_cf)) {
+        const bool far = ax > 5e7;
+        const double num = far ? GGP_ISPI : pin(GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2));
+        const double den = far ? ax : pin(ax * ((ax * ax) * (ax * ax - 5) + 3.75));
+        cf = pin(num / den);
+    }
+    const double w = use_cf ? cf : (use_taylor ? taylor : poly);
     return GGP_SPI2 * (x < 0.0 ? -w : w);
 }
 
@@ -220,6 +228,18 @@ GGP_DEV double pow_bf(const Step &S, const int p)
     const double sa = S.two_sa * 0.5, a = S.a;
     const double p0 = pin(4. * (a * sa)), p1 = pin(8. * ((a * a) * sa)), p2 = pin(16. * (((a * a) * a) * sa));
     return p == 0 ? p0 : p == 1 ? p1 : p2;
+}
+
+// reciprocals of the powers from the step's 1/(4a) and 1/(2 sqrt a): 1/(4 a^1.5) =
+// 2 r4a r2sa, then each next power one factor 2 r4a = 1/(2a) more.  They only seed rdiv
+// (q = x r, then one residual correction against the exact divisor), whose quotient does not
+// depend on a few ulp in r: one division per step less than 1.0 / pow.
+GGP_DEV double rpow_bf(const Step &S, const int p)
+{
+    const double r0 = pin(2. * (S.r_four_a * S.r_two_sa));
+    const double r1 = pin(2. * (S.r_four_a * r0));
+    const double r2 = pin(2. * (S.r_four_a * r1));
+    return p == 0 ? r0 : p == 1 ? r1 : r2;
 }
 
 // tau_unified without branches (X, Dw, PW: the LDS arrays)
@@ -249,6 +269,34 @@ GGP_DEV double tau_bf(const Step &S, const ITask T, const double km, const doubl
     const double x = k == 0 ? dterm : xfull;
     const double den = k == 0 ? S.two_sa : pd, rden = k == 0 ? S.r_two_sa : pr;
     return rdiv(x, den, rden);
+}
+
+// ggp_posterior with the lower triangle of C formed only on the cell's last row: on every
+// other row the next propagation reads the upper triangle (step_init) and then overwrites
+// all of C (out_store), so those six entries are dead.  Same expressions, same bits.
+GGP_DEV void posterior(double *m, double *C, const double x0, const double x1, const ggp_innov &v, const bool last)
+{
+    double K[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) K[i] = C[i];
+    double KS0[4], KS1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        KS0[i] = K[i] * v.si00 + K[4 + i] * v.si10;
+        KS1[i] = K[i] * v.si01 + K[4 + i] * v.si11;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = m[i] + (KS0[i] * x0 + KS1[i] * x1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j) C[4 * i + j] = C[4 * i + j] - (KS0[i] * K[j] + KS1[i] * K[4 + j]);
+    if (last) {   // wave-uniform (one cell per wave)
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) C[4 * i + j] = C[4 * i + j] - (KS0[i] * K[j] + KS1[i] * K[4 + j]);
+    }
 }
 
 // the outputs' variables V (ggp_outtab.h): lane 0 stores them, stage D reads them
