@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
+COMBINE_BYTES_PER_ROW = 484   # k_combine: fwd + bwd rows (2 x 160 B) + prior segment (4 B) read, 160 B written
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
              3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
 SEED = 20261015
@@ -71,6 +72,9 @@ def main() -> int:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--large-trees", type=int, default=12500,
                     help="also time a C4-shard-sized forest (0 = skip)")
+    ap.add_argument("--predict-trees", type=int, default=125000,
+                    help="also time the -p smoother on a C5-shard forest: trees per GPU (0 = skip)")
+    ap.add_argument("--predict-rows", type=int, default=500, help="rows per tree of the -p forest")
     args = ap.parse_args()
 
     import torch
@@ -153,6 +157,39 @@ def main() -> int:
                  "note": "same path, per-GPU shard of BASELINE configs[3] (C4); not the headline value"}
         fl.close()
 
+    # ---- the -p smoother on a per-GPU shard of BASELINE configs[4] (C5: 1M trees x 500 tp over
+    # 8 GPUs = 125k trees per GPU): forward + backward levels and k_combine, device-resident
+    # (outputs stay in HBM; the host copies are the CLI's I/O, not the smoother) ----
+    pred = None
+    if args.predict_trees > 0:
+        hp = g.HostForest.synthetic(args.predict_trees, args.predict_rows, seed=SEED,
+                                    first_tree=world * (args.trees + args.large_trees) + rank * args.predict_trees)
+        fp_ = g.Forest(hp, device=local)
+        fp_.predict(P_EXAMPLE, outputs=(False, False, False))        # warm-up + workspace
+        barrier()
+        t1 = time.perf_counter()
+        reps, sm, cb = 3, 0.0, 0.0
+        for _ in range(reps):
+            fp_.predict(P_EXAMPLE, outputs=(False, False, False))
+            a_, b_ = fp_.predict_profile()
+            sm += a_
+            cb += b_
+        barrier()
+        pel = (time.perf_counter() - t1) / reps
+        if world > 1:
+            t = torch.tensor([pel], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pel = float(t.item())
+        nr = hp.n_rows
+        cb_ms = cb / reps
+        pred = {"trees_per_gpu": args.predict_trees, "rows_per_gpu": nr, "ms_per_predict": 1e3 * pel,
+                "rows_per_s": nr * world / pel, "smooth_ms": sm / reps, "combine_ms": cb_ms,
+                "combine_bytes_per_row": COMBINE_BYTES_PER_ROW,
+                "combine_gbs": COMBINE_BYTES_PER_ROW * nr / (cb_ms * 1e-3) / 1e9 if cb_ms > 0 else 0.0,
+                "note": "-p forward+backward+combine per GPU shard of BASELINE configs[4] (C5), outputs "
+                        "resident in HBM; rows_per_s is whole-job; not the headline value"}
+        fp_.close()
+
     result = None
     if rank == 0:
         result = {
@@ -193,6 +230,8 @@ def main() -> int:
         }
         if large is not None:
             result["large_forest"] = large
+        if pred is not None:
+            result["predict"] = pred
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

@@ -57,6 +57,8 @@ ENGINE_SYMBOLS = {
     "ggp_loglik_result": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_int64_p, c_int64_p]),
     "ggp_predict": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, c_double_p,
                                    c_double_p, c_double_p]),
+    "ggp_predict_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                           ctypes.POINTER(ctypes.c_float)]),
     "ggp_joints": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, ctypes.c_double, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int64, c_int64_p, c_double_p, c_int64_p]),
     "ggp_reset_state": (ctypes.c_int, [ctypes.c_void_p]),

@@ -1076,6 +1076,13 @@ struct ggp_forest {
     std::vector<int32_t> ev_kernel;   // per profiled launch: kind << 8 | lanes per cell
     std::vector<int64_t> ev_rows_launch;
     int n_prof = 0;
+    // -p workspace, allocated on the first ggp_predict and kept for the handle's lifetime (a
+    // scan of predictions or a bench loop then pays no hipMalloc/hipFree per call)
+    double *d_sm_ptab = nullptr, *d_sm_pstate = nullptr, *d_sm_fwd = nullptr, *d_sm_bwd = nullptr,
+           *d_sm_comb = nullptr;
+    int32_t sm_ptab_cap = 0;   // segments d_sm_ptab holds
+    hipEvent_t ev_pred[3] = {nullptr, nullptr, nullptr};   // start, after fwd+bwd, after combine
+    bool pred_timed = false;
 };
 
 // Lane schedule: a wave's cost per step does not depend on how many of its lanes hold a
@@ -1209,8 +1216,11 @@ void ggp_forest_destroy(ggp_forest *f)
     for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
                     (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
                     (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
-                    (void *)f->d_cell_ll, (void *)f->d_cell_nan})
+                    (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_sm_ptab, (void *)f->d_sm_pstate,
+                    (void *)f->d_sm_fwd, (void *)f->d_sm_bwd, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
+    for (auto &e : f->ev_pred)
+        if (e) (void)hipEventDestroy(e);
     if (f->h_out_ll) (void)hipHostFree(f->h_out_ll);   // one allocation: ll, then the NaN code
     for (auto &e : f->ev) (void)hipEventDestroy(e);
     if (f->stream) (void)hipStreamDestroy(f->stream);
@@ -1579,6 +1589,18 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, 
     return GGP_OK;
 }
 
+int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine)
+{
+    if (!f || !f->pred_timed) { g_last_err = "ggp_predict_profile: no completed ggp_predict"; return GGP_EINVAL; }
+    HIPCHK(hipSetDevice(f->device));
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, f->ev_pred[0], f->ev_pred[1]));
+    HIPCHK(hipEventElapsedTime(&b, f->ev_pred[1], f->ev_pred[2]));
+    if (ms_smooth) *ms_smooth = a;
+    if (ms_combine) *ms_combine = b;
+    return GGP_OK;
+}
+
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd, double *out_bwd,
                 double *out_comb)
 {
@@ -1587,36 +1609,53 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
     HIPCHK(hipStreamSynchronize(f->stream));
     const int64_t nc = f->n_cells, nr = f->n_rows;
     if (nc == 0) return GGP_OK;
-    // fresh cells (main.cpp:434-438): the smoother never touches the likelihood's carried state
-    double *d_ptab = nullptr, *d_pstate = nullptr, *d_fwd = nullptr, *d_bwd = nullptr, *d_comb = nullptr;
-    int rc = GGP_OK;
-    auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
-    check(dev_upload(&d_ptab, params, (size_t)n_seg * 11));
-    check(dev_upload<double>(&d_pstate, nullptr, (size_t)nc * 20));
-    check(dev_upload<double>(&d_fwd, nullptr, (size_t)nr * 20));
-    check(dev_upload<double>(&d_bwd, nullptr, (size_t)nr * 20));
-    check(dev_upload<double>(&d_comb, nullptr, (size_t)nr * 20));
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(f->stream);
-        for (double *p : {d_ptab, d_pstate, d_fwd, d_bwd, d_comb})
-            if (p) (void)hipFree(p);
-    };
-    if (rc == GGP_OK && hipMemsetAsync(d_pstate, 0, (size_t)nc * 20 * sizeof(double), f->stream) != hipSuccess)
-        rc = GGP_EDEV;
-    if (rc != GGP_OK) { cleanup(); return rc; }
-    hipError_t e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
+    // fresh cells (main.cpp:434-438): the smoother never touches the likelihood's carried state.
+    // The workspace (per-cell state + three [n_rows x 20] row buffers) lives in the handle.
+    if (!f->d_sm_pstate) {
+        int rc = GGP_OK;
+        auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+        check(dev_upload<double>(&f->d_sm_pstate, nullptr, (size_t)nc * 20));
+        check(dev_upload<double>(&f->d_sm_fwd, nullptr, (size_t)nr * 20));
+        check(dev_upload<double>(&f->d_sm_bwd, nullptr, (size_t)nr * 20));
+        check(dev_upload<double>(&f->d_sm_comb, nullptr, (size_t)nr * 20));
+        for (auto &ev : f->ev_pred)
+            if (rc == GGP_OK && hipEventCreate(&ev) != hipSuccess) rc = GGP_EDEV;
+        if (rc != GGP_OK) {
+            for (double **p : {&f->d_sm_pstate, &f->d_sm_fwd, &f->d_sm_bwd, &f->d_sm_comb}) {
+                if (*p) (void)hipFree(*p);
+                *p = nullptr;
+            }
+            return rc;
+        }
+    }
+    if (n_seg > f->sm_ptab_cap) {
+        if (f->d_sm_ptab) (void)hipFree(f->d_sm_ptab);
+        f->d_sm_ptab = nullptr;
+        f->sm_ptab_cap = 0;
+        const int rc = dev_upload<double>(&f->d_sm_ptab, nullptr, (size_t)n_seg * 11);
+        if (rc != GGP_OK) return rc;
+        f->sm_ptab_cap = n_seg;
+    }
+    double *d_ptab = f->d_sm_ptab, *d_pstate = f->d_sm_pstate, *d_fwd = f->d_sm_fwd, *d_bwd = f->d_sm_bwd,
+           *d_comb = f->d_sm_comb;
+    f->pred_timed = false;
+    hipError_t e = hipMemcpyAsync(d_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice, f->stream);
+    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[0], f->stream);
+    if (e == hipSuccess) e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
+    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[1], f->stream);
     if (e == hipSuccess) {
         const int64_t blocks = (nr + 255) / 256;
         hipLaunchKernelGGL(k_combine, dim3((unsigned)blocks), dim3(256), 0, f->stream, d_ptab, n_seg,
                            f->d_prior_seg, nr, d_fwd, d_bwd, d_comb);
         e = hipGetLastError();
     }
+    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[2], f->stream);
     const size_t bytes = (size_t)nr * 20 * sizeof(double);
     if (e == hipSuccess && out_fwd) e = hipMemcpyAsync(out_fwd, d_fwd, bytes, hipMemcpyDeviceToHost, f->stream);
     if (e == hipSuccess && out_bwd) e = hipMemcpyAsync(out_bwd, d_bwd, bytes, hipMemcpyDeviceToHost, f->stream);
     if (e == hipSuccess && out_comb) e = hipMemcpyAsync(out_comb, d_comb, bytes, hipMemcpyDeviceToHost, f->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
-    cleanup();
+    f->pred_timed = e == hipSuccess;
     if (e != hipSuccess) {
         g_last_err = std::string("ggp_predict: ") + hipGetErrorString(e);
         return GGP_EDEV;

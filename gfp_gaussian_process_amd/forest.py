@@ -348,12 +348,21 @@ class Forest:
         self._check(self._lib.ggp_get_state(self._h, out.ctypes.data_as(N.c_double_p)))
         return out
 
-    def predict(self, params_per_segment):
+    def predict(self, params_per_segment, outputs=(True, True, True)):
+        """-p smoother (ggp_predict): (forward, backward, combined) [n_rows, 20] arrays; an output
+        whose flag in `outputs` is False is not copied back and comes back as None"""
         p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
-        out = [np.zeros((self.n_rows, N.STATE)) for _ in range(3)]
+        out = [np.zeros((self.n_rows, N.STATE)) if want else None for want in outputs]
         self._check(self._lib.ggp_predict(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0],
-                                          *(o.ctypes.data_as(N.c_double_p) for o in out)))
+                                          *(o.ctypes.data_as(N.c_double_p) if o is not None else None
+                                            for o in out)))
         return tuple(out)
+
+    def predict_profile(self):
+        """device ms of the last predict: (forward + backward levels, k_combine)"""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self._lib.ggp_predict_profile(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def joints(self, params_per_segment, tol: float = 1e-10, r_lo: int = 0, r_hi=None, cap: int = 1 << 22):
         """-j compute for start rows [r_lo, r_hi) (ggp_joints): (idx [k, 2] = (start, target) rows,

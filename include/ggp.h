@@ -101,6 +101,11 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd,
                 double *out_bwd, double *out_comb);
 
+/* measurement hook (bench.py): HIP-event device time of the last completed ggp_predict on
+ * the handle's stream -- the forward + backward level launches, and k_combine.  The copies
+ * back to the host are excluded. */
+int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine);
+
 /* -j compute: collect_joint_distributions (correlation_tree.h:464-651).  Runs the smoother,
  * then for every start row r in [r_lo, r_hi) (input order) the joints P(z_target, z_r | D)
  * the reference adds to its Joint_vector, in the order it adds them: out_idx[2k] = r,

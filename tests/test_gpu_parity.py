@@ -326,3 +326,26 @@ def test_predict_leaves_carried_state_alone(example_forests):
     b.total_likelihood(P)
     a.predict(P)
     assert a.total_likelihood(P) == b.total_likelihood(P)
+
+
+def test_predict_workspace_reuse_and_partial_outputs():
+    """the handle keeps the -p workspace across calls (ggp_predict): a second predict with other
+    segments, then a repeat of the first, give bitwise the first results; outputs that are not
+    requested come back as None and the rest are unchanged; the profile hook reports device time"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(30, 40)
+    P0 = np.array(CONFIGS[0][2])
+    P1 = P0.copy()
+    P1[0] *= 1.1
+    f = g.Forest(hf)
+    first = f.predict(P0)
+    f.predict(np.stack([P0, P1]))
+    again = f.predict(P0)
+    for x, y in zip(first, again):
+        assert np.array_equal(x, y)
+    part = f.predict(P0, outputs=(False, False, True))
+    assert part[0] is None and part[1] is None
+    assert np.array_equal(part[2], first[2])
+    sm, cb = f.predict_profile()
+    assert sm > 0.0 and cb > 0.0
+    f.close()
