@@ -74,6 +74,7 @@ def main() -> int:
                     help="also time a C4-shard-sized forest (0 = skip)")
     ap.add_argument("--predict-trees", type=int, default=125000,
                     help="also time the -p smoother on a C5-shard forest: trees per GPU (0 = skip)")
+    ap.add_argument("--hessian", type=int, default=1, help="also time the batched 11-parameter Hessian (0 = skip)")
     ap.add_argument("--predict-rows", type=int, default=500, help="rows per tree of the -p forest")
     args = ap.parse_args()
 
@@ -157,6 +158,25 @@ def main() -> int:
                  "note": "same path, per-GPU shard of BASELINE configs[3] (C4); not the headline value"}
         fl.close()
 
+    # ---- opt-in batched objective on the C2 forest: the 4 k^2 = 484 points of an 11-parameter
+    # Hessian (likelihood.h:211-258) in one ggp_total_loglik_batch call ----
+    hess = None
+    if args.hessian:
+        from gfp_gaussian_process_amd import optimize as opt
+        pts, _ = opt.hessian_points(P_EXAMPLE, list(range(11)), 1e-2)
+        fg.total_likelihood_batch(pts)                     # warm-up + workspace
+        barrier()
+        t1 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            fg.total_likelihood_batch(pts)
+        barrier()
+        hel = (time.perf_counter() - t1) / reps
+        hess = {"points": len(pts), "rows_per_point": rows_rank, "ms_per_batch": 1e3 * hel,
+                "updates_per_s_per_gpu": len(pts) * rows_rank / hel,
+                "sequential_ms_estimate": len(pts) * 1e3 * el / args.steps,
+                "note": "batched objective (opt-in, points independent) on the C2 forest; not the headline value"}
+
     # ---- the -p smoother on a per-GPU shard of BASELINE configs[4] (C5: 1M trees x 500 tp over
     # 8 GPUs = 125k trees per GPU): forward + backward levels and k_combine, device-resident
     # (outputs stay in HBM; the host copies are the CLI's I/O, not the smoother) ----
@@ -232,6 +252,8 @@ def main() -> int:
             result["large_forest"] = large
         if pred is not None:
             result["predict"] = pred
+        if hess is not None:
+            result["hessian_batch"] = hess
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

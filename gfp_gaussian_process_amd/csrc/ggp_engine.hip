@@ -98,21 +98,15 @@ GGP_DEV bool cell_prologue(const DevForest &F, const double *p, const double *st
 // one generation depth.  `cpw` cells per 64-lane wave: < 64 spreads a small level over
 // more SIMDs (latency), 64 packs waves (throughput); results do not depend on it.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
-                                                      const int32_t *__restrict__ cells, int n,
-                                                      int cpw, double *__restrict__ state,
-                                                      double *__restrict__ cell_ll,
-                                                      int32_t *__restrict__ cell_nan)
+GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t *__restrict__ cells,
+                              const int n, const int cpw, double *__restrict__ state,
+                              double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan,
+                              const double *s_tab, const int lane)
 {
-    __shared__ double s_tab[kDawsonTab];
-    const int lane = threadIdx.x;
-    load_dawson_table(s_tab, lane);
-    __syncthreads();
     if (lane >= cpw) return;
     const int i = blockIdx.x * cpw + lane;
     if (i >= n) return;
     const int c = cells[i];
-    const double *p = P.p;
     const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
     double m[4], C[16];
     const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
@@ -149,6 +143,47 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
     for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
     cell_ll[F.dfs_rank[c]] = cl;
     cell_nan[F.dfs_rank[c]] = nan_row;
+}
+
+__global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
+                                                      const int32_t *__restrict__ cells, int n,
+                                                      int cpw, double *__restrict__ state,
+                                                      double *__restrict__ cell_ll,
+                                                      int32_t *__restrict__ cell_nan)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    loglik_lane_cell(F, P.p, cells, n, cpw, state, cell_ll, cell_nan, s_tab, lane);
+}
+
+// Batched objective (ggp_total_loglik_batch): blockIdx.y = parameter point.  Each point has
+// its own parameter row, state slice [n_cells x 20] and per-cell ll / NaN slices; the cell
+// body is the lane schedule's, so a point's result is bitwise that of a single lane-schedule
+// evaluation from the same starting state.
+__global__ __launch_bounds__(64) void k_loglik_level_batch(DevForest F, const double *__restrict__ ptab,
+                                                            const int32_t *__restrict__ cells, int n, int cpw,
+                                                            int64_t n_cells, double *__restrict__ state,
+                                                            double *__restrict__ cell_ll,
+                                                            int32_t *__restrict__ cell_nan)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    const int64_t pt = blockIdx.y;
+    loglik_lane_cell(F, ptab + 11 * pt, cells, n, cpw, state + pt * n_cells * 20, cell_ll + pt * n_cells,
+                     cell_nan + pt * n_cells, s_tab, lane);
+}
+
+// every batch point starts from the handle's carried state: dst[pt] = src, for pt < n_pts
+__global__ __launch_bounds__(256) void k_replicate(const double *__restrict__ src, int64_t n,
+                                                   double *__restrict__ dst, int64_t n_pts)
+{
+    const int64_t total = n * n_pts;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i % n];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -986,6 +1021,10 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(int64_t n, const double 
     __shared__ double s_sum[kRedThreads];
     __shared__ long long s_nan[kRedThreads];
     const int tid = threadIdx.x;
+    cell_ll += (int64_t)blockIdx.x * n;   // one block per parameter point (a single evaluation: 1)
+    cell_nan += (int64_t)blockIdx.x * n;
+    out_ll += blockIdx.x;
+    out_nan += blockIdx.x;
     const int64_t lo = n * tid / kRedThreads, hi = n * (tid + 1) / kRedThreads;
     double acc = 0.0;
     long long first = 0x7fffffffffffffffLL;
@@ -1083,6 +1122,11 @@ struct ggp_forest {
     int32_t sm_ptab_cap = 0;   // segments d_sm_ptab holds
     hipEvent_t ev_pred[3] = {nullptr, nullptr, nullptr};   // start, after fwd+bwd, after combine
     bool pred_timed = false;
+    // batched-objective workspace (ggp_total_loglik_batch), grown on demand
+    double *d_b_ptab = nullptr, *d_b_state = nullptr, *d_b_ll = nullptr, *d_b_out_ll = nullptr;
+    int32_t *d_b_nan = nullptr;
+    int64_t *d_b_out_nan = nullptr;
+    int64_t b_cap = 0;   // points the workspace holds
 };
 
 // Lane schedule: a wave's cost per step does not depend on how many of its lanes hold a
@@ -1217,7 +1261,9 @@ void ggp_forest_destroy(ggp_forest *f)
                     (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
                     (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
                     (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_sm_ptab, (void *)f->d_sm_pstate,
-                    (void *)f->d_sm_fwd, (void *)f->d_sm_bwd, (void *)f->d_sm_comb})
+                    (void *)f->d_sm_fwd, (void *)f->d_sm_bwd, (void *)f->d_sm_comb, (void *)f->d_b_ptab,
+                    (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_out_ll, (void *)f->d_b_nan,
+                    (void *)f->d_b_out_nan})
         if (p) (void)hipFree(p);
     for (auto &e : f->ev_pred)
         if (e) (void)hipEventDestroy(e);
@@ -1548,6 +1594,87 @@ int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *n
     int rc = ggp_total_loglik_async(f, params);
     if (rc != GGP_OK) return rc;
     return ggp_loglik_result(f, ll, nan_cell, nan_row);
+}
+
+// Batched objective: n_pts parameter points, each evaluated from the handle's carried state as
+// it is at the call (the carried state itself is left unchanged).  Points run in chunks that
+// keep the per-point state slices under kBatchBytes; every level of a chunk is one launch of
+// the lane schedule with blockIdx.y = point, then one k_reduce block per point.
+static constexpr int64_t kBatchBytes = int64_t(4) << 30;
+
+static void batch_free(ggp_forest *f)
+{
+    for (void *p : {(void *)f->d_b_ptab, (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_out_ll,
+                    (void *)f->d_b_nan, (void *)f->d_b_out_nan})
+        if (p) (void)hipFree(p);
+    f->d_b_ptab = f->d_b_state = f->d_b_ll = f->d_b_out_ll = nullptr;
+    f->d_b_nan = nullptr;
+    f->d_b_out_nan = nullptr;
+    f->b_cap = 0;
+}
+
+int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *status)
+{
+    if (!f || n_pts < 0 || (n_pts > 0 && (!params || !ll || !status))) {
+        g_last_err = "ggp_total_loglik_batch: bad arguments";
+        return GGP_EINVAL;
+    }
+    if (n_pts == 0) return GGP_OK;
+    HIPCHK(hipSetDevice(f->device));
+    const int64_t nc = f->n_cells;
+    if (nc == 0) {
+        for (int32_t i = 0; i < n_pts; ++i) { ll[i] = 0.0; status[i] = GGP_OK; }
+        return GGP_OK;
+    }
+    const int64_t per_pt = nc * (20 * 8 + 8 + 4);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({(int64_t)n_pts, kBatchBytes / per_pt, 65535}));
+    if (chunk > f->b_cap) {
+        HIPCHK(hipStreamSynchronize(f->stream));
+        batch_free(f);
+        int rc = GGP_OK;
+        auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+        check(dev_upload<double>(&f->d_b_ptab, nullptr, (size_t)chunk * 11));
+        check(dev_upload<double>(&f->d_b_state, nullptr, (size_t)chunk * nc * 20));
+        check(dev_upload<double>(&f->d_b_ll, nullptr, (size_t)chunk * nc));
+        check(dev_upload<int32_t>(&f->d_b_nan, nullptr, (size_t)chunk * nc));
+        check(dev_upload<double>(&f->d_b_out_ll, nullptr, (size_t)chunk));
+        check(dev_upload<int64_t>(&f->d_b_out_nan, nullptr, (size_t)chunk));
+        if (rc != GGP_OK) { batch_free(f); return rc; }
+        f->b_cap = chunk;
+    }
+    const int n_levels = (int)f->level_start.size() - 1;
+    const int cpw = lane_cpw(f);
+    std::vector<int64_t> nan_code((size_t)chunk);
+    for (int64_t p0 = 0; p0 < n_pts; p0 += chunk) {
+        const int64_t np = std::min<int64_t>(chunk, n_pts - p0);
+        HIPCHK(hipMemcpyAsync(f->d_b_ptab, params + 11 * p0, (size_t)np * 11 * sizeof(double), hipMemcpyHostToDevice,
+                              f->stream));
+        const int64_t total = nc * 20 * np;
+        const int rblocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_replicate, dim3(rblocks), dim3(256), 0, f->stream, f->d_state, nc * 20, f->d_b_state, np);
+        HIPCHK(hipGetLastError());
+        for (int L = 0; L < n_levels; ++L) {
+            const int64_t a = f->level_start[L];
+            const int n = (int)(f->level_start[L + 1] - a);
+            if (n <= 0) continue;
+            hipLaunchKernelGGL(k_loglik_level_batch, dim3((n + cpw - 1) / cpw, (unsigned)np), dim3(64), 0, f->stream,
+                               f->F, f->d_b_ptab, f->d_level_cells + a, n, cpw, nc, f->d_b_state, f->d_b_ll, f->d_b_nan);
+            HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_reduce, dim3((unsigned)np), dim3(kRedThreads), 0, f->stream, nc, f->d_b_ll, f->d_b_nan,
+                           f->d_b_out_ll, f->d_b_out_nan);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(ll + p0, f->d_b_out_ll, (size_t)np * sizeof(double), hipMemcpyDeviceToHost, f->stream));
+        HIPCHK(hipMemcpyAsync(nan_code.data(), f->d_b_out_nan, (size_t)np * sizeof(int64_t), hipMemcpyDeviceToHost,
+                              f->stream));
+        HIPCHK(hipStreamSynchronize(f->stream));
+        for (int64_t i = 0; i < np; ++i) {
+            const bool bad = nan_code[(size_t)i] != 0x7fffffffffffffffLL || std::isnan(ll[p0 + i]);
+            status[p0 + i] = bad ? GGP_ENAN : GGP_OK;
+            if (bad) ll[p0 + i] = std::nan("");
+        }
+    }
+    return GGP_OK;
 }
 
 int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)

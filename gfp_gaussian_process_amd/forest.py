@@ -340,6 +340,20 @@ class Forest:
         self._check(rc)
         return ll.value
 
+    def total_likelihood_batch(self, params_points):
+        """+ll of every parameter point (rows of an [n, 11] array), each from the carried state as
+        it is now; the carried state is left unchanged (ggp_total_loglik_batch).  Returns
+        (ll [n], nan [n] bool); a NaN point has ll = nan instead of raising."""
+        p = np.ascontiguousarray(np.atleast_2d(params_points), np.float64)
+        if p.shape[1] != N.N_PARAMS:
+            raise ValueError(f"expected [n, {N.N_PARAMS}] parameter points, got {p.shape}")
+        ll = np.zeros(p.shape[0])
+        st = np.zeros(p.shape[0], np.int32)
+        self._check(self._lib.ggp_total_loglik_batch(self._h, p.shape[0], p.ctypes.data_as(N.c_double_p),
+                                                     ll.ctypes.data_as(N.c_double_p),
+                                                     st.ctypes.data_as(N.c_int32_p)))
+        return ll, st == N.GGP_ENAN
+
     def reset_state(self) -> None:
         self._check(self._lib.ggp_reset_state(self._h))
 

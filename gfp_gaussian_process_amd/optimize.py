@@ -4,6 +4,7 @@ of likelihood.h, with the numerics in libggp_host.so (include/ggp_host.h):
   nldrmd_minimize        NLopt 2.7.1 LN_NELDERMEAD (restated, csrc/host/ggp_nelder_mead.h)
   minimize_wrapper       minimize_wrapper / minimize_wrapper_log_params  minimizer_nlopt.h:10-215
   num_hessian            num_hessian_ll                                    likelihood.h:211-258
+  num_hessian_batched    the same points in one ggp_total_loglik_batch call (opt-in, unchained)
   inverse_pplu           Eigen MatrixXd::inverse (partial-pivot LU)
   ll_error_bars          ll_error_bars                                     likelihood.h:260-268
   bound_1dscan           run_bound_1dscan                                  main.cpp:80-114
@@ -105,6 +106,43 @@ def num_hessian(objective, x, idx, epsilon: float) -> np.ndarray:
     return out
 
 
+def hessian_points(x, idx, epsilon: float):
+    """the 4 k^2 parameter points num_hessian_ll visits (likelihood.h:211-258), in its order
+    (i, j, then ++, +-, -+, --), with its steps h = max(x epsilon, 1e-12); returns (points
+    [4 k^2, n], h [k])"""
+    x = np.asarray(x, np.float64)
+    idx = [int(i) for i in idx]
+    h = np.array([max(x[i] * epsilon, 1e-12) for i in idx])
+    pts = []
+    for a, ii in enumerate(idx):
+        for b, jj in enumerate(idx):
+            for s1, s2 in ((1, 1), (1, -1), (-1, 1), (-1, -1)):
+                xx = x.copy()
+                xx[ii] = xx[ii] + h[a] if s1 > 0 else xx[ii] - h[a]
+                xx[jj] = xx[jj] + h[b] if s2 > 0 else xx[jj] - h[b]
+                pts.append(xx)
+    return np.array(pts), h
+
+
+def num_hessian_batched(forest, x, idx, epsilon: float) -> np.ndarray:
+    """opt-in batched num_hessian_ll: the 4 k^2 points in ONE ggp_total_loglik_batch call, each
+    from the carried state as it is now (the reference chains the state from call to call, so
+    its values differ by that carried state).  Same steps and the same
+    (l++ - l+- - l-+ + l--) / (4 h1 h2) expression as num_hessian."""
+    from .forest import LikelihoodIsNan
+    pts, h = hessian_points(x, idx, epsilon)
+    ll, nan = forest.total_likelihood_batch(pts)
+    if nan.any():
+        raise LikelihoodIsNan(-1, -1)
+    k = len(h)
+    q = ll.reshape(k, k, 4)
+    out = np.zeros((k, k))
+    for i in range(k):
+        for j in range(k):
+            out[i, j] = (q[i, j, 0] - q[i, j, 1] - q[i, j, 2] + q[i, j, 3]) / (4 * h[i] * h[j])
+    return out
+
+
 def inverse_pplu(a) -> np.ndarray:
     a = np.ascontiguousarray(a, np.float64)
     out = np.zeros_like(a)
@@ -112,9 +150,13 @@ def inverse_pplu(a) -> np.ndarray:
     return out
 
 
-def ll_error_bars(objective, x_final, params: ParameterSet, epsilon: float) -> np.ndarray:
-    """squared error bars -diag(H^-1) of the non-fixed parameters (likelihood.h:260-268)"""
-    h = num_hessian(objective, x_final, params.non_fixed(), epsilon)
+def ll_error_bars(objective, x_final, params: ParameterSet, epsilon: float, batched: bool = False) -> np.ndarray:
+    """squared error bars -diag(H^-1) of the non-fixed parameters (likelihood.h:260-268);
+    batched=True evaluates the Hessian's points in one batch (objective: a Forest)"""
+    if batched:
+        h = num_hessian_batched(objective, x_final, params.non_fixed(), epsilon)
+    else:
+        h = num_hessian(objective, x_final, params.non_fixed(), epsilon)
     return -np.diag(inverse_pplu(h))
 
 

@@ -10,6 +10,8 @@
  *                                total_likelihood_log_params         likelihood.h:161-167:
  *                                the caller negates / exponentiates)
  *                               incl. likelihood_recr / sc_likelihood likelihood.h:36-122
+ *   ggp_total_loglik_batch  the 4k^2 objective calls of num_hessian_ll   likelihood.h:211-258
+ *                               (opt-in: points independent, not chained)
  *   ggp_joints        replaces  collect_joint_distributions (compute) correlation_tree.h:464-651
  *   ggp_predict       replaces  prediction_forward                   predictions.h:166-173
  *                               prediction_backward                  predictions.h:438-444
@@ -89,6 +91,16 @@ void ggp_forest_destroy(ggp_forest *f);
  * row within the cell) or -1.  Returns GGP_OK, GGP_ENAN, GGP_EDEV. */
 int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *nan_cell,
                      int64_t *nan_row);
+
+/* Batched objective (opt-in; SURVEY.md §8(f) 2 -- the Hessian of likelihood.h:211-258 needs 4k^2
+ * independent points): params is n_pts*11 doubles; ll[i] receives point i's +ll and status[i]
+ * GGP_OK or GGP_ENAN (ll[i] = NaN).  Every point starts from the carried state as it is at the
+ * call, and the carried state is left unchanged -- the reference instead chains each call's
+ * state into the next (this is the documented difference of the batched mode).  A point's value
+ * is bitwise that of ggp_total_loglik with GGP_KERNEL_LANE from the same state.  Returns GGP_OK,
+ * GGP_EINVAL, GGP_ENOMEM or GGP_EDEV. */
+int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll,
+                           int32_t *status);
 
 /* Asynchronous form for drivers that pipeline: enqueue one evaluation on the handle's
  * stream; ggp_loglik_result() waits and returns what ggp_total_loglik would have. */

@@ -349,3 +349,82 @@ def test_predict_workspace_reuse_and_partial_outputs():
     sm, cb = f.predict_profile()
     assert sm > 0.0 and cb > 0.0
     f.close()
+
+
+def _points(P, n, seed=11):
+    rng = np.random.default_rng(seed)
+    base = np.asarray(P, np.float64)
+    return np.stack([base * (1.0 + 0.02 * rng.standard_normal(base.size)) for _ in range(n)])
+
+
+def test_batch_bitwise_equals_lane_evaluations(example_forests):
+    """ggp_total_loglik_batch: every point from the same carried state, bitwise a lane-schedule
+    ggp_total_loglik from that state; the handle's carried state is left unchanged"""
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P0 = CONFIGS[0][2]
+    pts = _points(P0, 6)
+    a = g.Forest(hf, kernel="lane")
+    a.total_likelihood(P0)                            # carried state after one call
+    ll, nan = a.total_likelihood_batch(pts)
+    assert not nan.any()
+    for k, pt in enumerate(pts):
+        b = g.Forest(hf, kernel="lane")
+        b.total_likelihood(P0)
+        assert b.total_likelihood(pt) == ll[k], k
+        b.close()
+    c = g.Forest(hf, kernel="lane")
+    c.total_likelihood(P0)
+    assert a.total_likelihood(P0) == c.total_likelihood(P0)   # batch did not touch the state
+
+
+@pytest.mark.parametrize("n_trees,rows", [(40, 40), (3, 300)])
+def test_batch_vs_oracle_fresh(n_trees, rows):
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(n_trees, rows)
+    pts = _points(CONFIGS[0][2], 5, seed=n_trees)
+    ll, nan = g.Forest(hf).total_likelihood_batch(pts)
+    assert not nan.any()
+    for k, pt in enumerate(pts):
+        vo = O.OracleForest(hf.a).total_likelihood(pt)[0]
+        assert _rel(ll[k], vo) < REL, k
+
+
+def test_batch_nan_point_and_chunking(example_forests):
+    """a NaN point is flagged without disturbing the others; many points (chunks of the lane
+    schedule's grid.y) agree with the few-point call"""
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P0 = CONFIGS[0][2]
+    pts = _points(P0, 3)
+    bad = pts.copy()
+    bad[1, 2] = -1.0                                  # var_lambda < 0 (as test_nan_reported_like_reference)
+    f = g.Forest(hf)
+    ll, nan = f.total_likelihood_batch(bad)
+    assert list(nan) == [False, True, False]
+    assert math.isnan(ll[1])
+    ref, _ = f.total_likelihood_batch(pts)
+    assert ll[0] == ref[0] and ll[2] == ref[2]
+    many = np.repeat(pts, 200, axis=0)
+    llm, nanm = f.total_likelihood_batch(many)
+    assert not nanm.any()
+    assert np.array_equal(llm, np.repeat(ref, 200))
+
+
+def test_batched_hessian_matches_point_formula(example_forests):
+    """num_hessian_batched = num_hessian_ll's expression over lane evaluations of the same points
+    from the same state (ll_error_bars' batched mode)"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as opt
+    hf = example_forests[("scaled", "binomial")]
+    P0 = np.asarray(CONFIGS[0][2])
+    idx = [0, 1, 3, 7]
+    f = g.Forest(hf)
+    H = opt.num_hessian_batched(f, P0, idx, 1e-2)
+    pts, h = opt.hessian_points(P0, idx, 1e-2)
+    ll = np.array([g.Forest(hf, kernel="lane").total_likelihood(p) for p in pts]).reshape(4, 4, 4)
+    for i in range(4):
+        for j in range(4):
+            want = (ll[i, j, 0] - ll[i, j, 1] - ll[i, j, 2] + ll[i, j, 3]) / (4 * h[i] * h[j])
+            assert H[i, j] == want

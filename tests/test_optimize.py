@@ -146,3 +146,31 @@ def test_cli_fails_loudly_without_a_device(tmp_path, example_paths):
              "-o", str(tmp_path / "out"))
     assert r.returncode == 1 and "Quit because of an error" in r.stdout
     assert os.path.exists(tmp_path / "out" / "input_error.log")
+
+
+def test_hessian_points_match_num_hessian_visits():
+    """the batched Hessian's points are exactly (bitwise, in order) those num_hessian_ll visits,
+    and its expression over them gives num_hessian's matrix bitwise"""
+    from gfp_gaussian_process_amd import optimize as O
+
+    class Batch:
+        def total_likelihood_batch(self, pts):
+            return np.array([f(p) for p in pts]), np.zeros(len(pts), bool)
+
+    seen = []
+
+    def f(x):
+        x = np.asarray(x, np.float64)
+        return float(-3 * x[0] ** 2 + 2 * x[0] * x[1] - 5 * x[1] ** 2 + np.sin(x[3]) * x[0])
+
+    def rec(x):
+        seen.append(np.array(x, np.float64))
+        return f(x)
+
+    x = np.array([1.3, 0.2, 7.0, 0.4, 2e-13])
+    idx = [0, 1, 3, 4]                                 # x[4] tiny: the 1e-12 step floor
+    H = O.num_hessian(rec, x, idx, 1e-2)
+    pts, h = O.hessian_points(x, idx, 1e-2)
+    assert np.array_equal(np.array(seen), pts)
+    assert np.array_equal(O.num_hessian_batched(Batch(), x, idx, 1e-2), H)
+    assert h[3] == 1e-12
