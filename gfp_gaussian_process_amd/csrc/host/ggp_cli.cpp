@@ -7,6 +7,7 @@
 //   -s  run_bound_1dscan      main.cpp:80-114
 //   -p  run_prediction_segments main.cpp:117-146 (write_predictions_to_file)
 //   -e  additive: one total log-likelihood at the parameter files' values
+//   -hb additive: -m's error bars from one batched call (ggp_total_loglik_batch)
 //   -j  run_joint_distribution  main.cpp:150-186 (collect_joint_distributions' dense joint
 //                                matrix, correlation_tree.h:9-23, 96-126, 588-648, 786-791);
 //                                as in the reference, -j implies -p (main.cpp:265-268)
@@ -335,6 +336,44 @@ double minimize(Objective &o, Params &P, double tolerance, bool log_space)
     return -minf;
 }
 
+// -hb (additive, opt-in): num_hessian_ll's 4 k^2 points (likelihood.h:211-258, same order, steps
+// and expression as ggp_num_hessian) in one ggp_total_loglik_batch call, each point from the
+// carried state left by the optimiser instead of chained from point to point
+void num_hessian_batched(Objective &o, const std::vector<double> &x, const std::vector<int> &idx, double epsilon,
+                         std::vector<double> &H)
+{
+    const int k = (int)idx.size();
+    std::vector<double> h(k), pts;
+    for (int a = 0; a < k; ++a) h[a] = std::max(x[idx[a]] * epsilon, 1e-12);
+    for (int a = 0; a < k; ++a)
+        for (int b = 0; b < k; ++b)
+            for (int q = 0; q < 4; ++q) {
+                std::vector<double> xx = x;
+                const int ii = idx[a], jj = idx[b];
+                xx[ii] = q < 2 ? xx[ii] + h[a] : xx[ii] - h[a];
+                xx[jj] = q % 2 == 0 ? xx[jj] + h[b] : xx[jj] - h[b];
+                pts.insert(pts.end(), xx.begin(), xx.end());
+            }
+    const int n = 4 * k * k;
+    std::vector<double> ll(n);
+    std::vector<int32_t> st(n);
+    const int rc = ggp_total_loglik_batch(o.forest, n, pts.data(), ll.data(), st.data());
+    if (rc != GGP_OK) throw std::runtime_error(std::string("GPU batched likelihood failed: ") + ggp_strerror(rc));
+    for (int i = 0; i < n; ++i)
+        if (st[i] == GGP_ENAN) {
+            g_log << "\n(num_hessian_batched) ERROR: Log likelihood is Nan\n";
+            throw std::domain_error("Likelihood is Nan");
+        }
+    g_iteration += n;
+    for (int a = 0; a < k; ++a)
+        for (int b = 0; b < k; ++b) {
+            const double *l = &ll[(size_t)4 * (a * k + b)];
+            H[(size_t)a * k + b] = (l[0] - l[1] - l[2] + l[3]) / (4 * h[a] * h[b]);
+        }
+}
+
+bool g_batched_hessian = false;
+
 std::vector<double> ll_error_bars(Params &P, Objective &o, double epsilon)
 {
     const std::vector<double> x = P.get_final();
@@ -342,6 +381,13 @@ std::vector<double> ll_error_bars(Params &P, Objective &o, double epsilon)
     const int k = (int)idx.size();
     std::vector<int32_t> idx32(idx.begin(), idx.end());
     std::vector<double> H((size_t)k * k), Hi((size_t)k * k);
+    if (g_batched_hessian) {
+        num_hessian_batched(o, x, idx, epsilon, H);
+        ggp_inverse_pplu(k, H.data(), Hi.data());
+        std::vector<double> err;
+        for (int i = 0; i < k; ++i) err.push_back(-Hi[(size_t)i * k + i]);
+        return err;
+    }
     struct Ctx { Objective *o; } ctx{&o};
     auto cb = [](const double *xx, double *v, void *data) -> int {
         auto *c = static_cast<Ctx *>(data);
@@ -656,6 +702,7 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
         {"-p", "--predict", "run prediction"},
         {"-j", "--joints", "run calculation of joint probabilities"},
         {"-e", "--evaluate", "evaluate the total log likelihood once at the parameter files' values"},
+        {"-hb", "--batched_hessian", "error bars from one batched GPU call (points not chained by carried state)"},
     };
     std::map<std::string, std::string> a;
     a["print_level"] = "0";
@@ -693,6 +740,7 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
             else if (key == "-s") a["scan"] = "1";
             else if (key == "-p") a["predict"] = "1";
             else if (key == "-e") a["evaluate"] = "1";
+            else if (key == "-hb") a["batched_hessian"] = "1";
             else if (key == "-j") {
                 a["joints"] = "1";
                 a["predict"] = "1";
@@ -790,6 +838,7 @@ int main(int argc, char **argv)
         }
         auto file_number = [&](int i) { return nseg > 1 ? i : -1; };
 
+        g_batched_hessian = args.count("batched_hessian") > 0;
         if (args.count("evaluate")) {
             for (int i = 0; i < nseg; ++i) {
                 Forest F;

@@ -205,3 +205,27 @@ def test_cli_joints_dense_matrix(tmp_path, example_paths):
         for col, v in got.items():
             ref = np.concatenate([exp[col][:8], exp[col][8:].reshape(8, 8)[iu]])
             assert np.allclose(v, ref, rtol=1e-5, atol=0), (s, col)
+
+
+def _errors(path):
+    block = open(path).read().split("errors^2:\n")[1].split("\n\n")[0].strip().splitlines()[1:]
+    return np.array([[float(v) for v in ln.split(",")] for ln in block])
+
+
+def test_cli_minimize_batched_hessian(tmp_path, example_paths):
+    """-m -hb: the same optimiser trajectory; the error bars from one batched call per epsilon
+    (points from the optimiser's final carried state, not chained).  The chained and unchained
+    Hessians differ only through the carried root off-diagonals: compared at 10%."""
+    pf = _param_file(tmp_path / "p.txt", {7: "3.35E-04, 3.35E-05", 8: "8.26E-01, 8.26E-02"})
+    for tag, extra in (("a", []), ("b", ["-hb"])):
+        _run(["-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-m", "-t", "1e-4",
+              "-o", str(tmp_path / tag), *extra], tmp_path)
+    ra = _ll_table(str(tmp_path / "a" / "input_f78_b") + "_iterations.csv")
+    rb = _ll_table(str(tmp_path / "b" / "input_f78_b") + "_iterations.csv")
+    assert ra == rb
+    ea = _errors(str(tmp_path / "a" / "input_f78_b") + "_final.csv")
+    eb = _errors(str(tmp_path / "b" / "input_f78_b") + "_final.csv")
+    assert ea.shape == eb.shape == (3, 3)
+    assert np.array_equal(ea[:, 0], eb[:, 0])
+    assert np.all(eb[:, 1:] > 0)
+    assert np.allclose(ea[:, 1:], eb[:, 1:], rtol=0.1), (ea, eb)
