@@ -63,8 +63,8 @@ def cpu_baseline(hf, budget_s: float):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--trees", type=int, default=1000, help="trees per GPU")
     ap.add_argument("--rows", type=int, default=200, help="rows per tree")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group", "wave"])

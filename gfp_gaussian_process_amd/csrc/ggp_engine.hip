@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1014,7 +1015,8 @@ constexpr int kRedThreads = 1024;
 __global__ __launch_bounds__(kRedThreads) void k_reduce(int64_t n, const double *__restrict__ cell_ll,
                                                          const int32_t *__restrict__ cell_nan,
                                                          double *__restrict__ out_ll,
-                                                         int64_t *__restrict__ out_nan)
+                                                         int64_t *__restrict__ out_nan,
+                                                         int64_t *__restrict__ out_seq, int64_t seq)
 {
     // cell_ll / cell_nan are stored in DFS order (F.dfs_rank): each thread adds a contiguous
     // chunk in that order, then a fixed pairwise tree over the threads (deterministic)
@@ -1043,9 +1045,13 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(int64_t n, const double 
         }
         __syncthreads();
     }
-    if (tid == 0) {   // straight into mapped host memory (read after the stream synchronises)
+    if (tid == 0) {   // straight into mapped host memory
         out_ll[0] = s_sum[0];
         out_nan[0] = s_nan[0];
+        if (out_seq) {   // then the call's sequence number: the host polls it (ggp_loglik_result)
+            __threadfence_system();
+            __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1105,6 +1111,14 @@ struct ggp_forest {
     int64_t *h_out_nan = nullptr;
     double *m_out_ll = nullptr;       // device views of the two
     int64_t *m_out_nan = nullptr;
+    // completion by polling: k_reduce stores the call's sequence number after the result (one
+    // more mapped slot); the host spins on it instead of waiting for the kernel-completion
+    // signal, with hipStreamQuery as the way out if the stream fails (GGP_SPIN=0: synchronise)
+    volatile int64_t *h_out_seq = nullptr;
+    int64_t *m_out_seq = nullptr;
+    int64_t seq = 0;
+    bool seq_pending = false;
+    bool spin = true;
     // schedule
     std::vector<int64_t> level_start;       // [n_levels+1] into level_cells
     std::vector<int32_t> h_dfs_order;
@@ -1195,7 +1209,10 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             f->n_prof++;
         }
     }
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kRedThreads), 0, f->stream, f->n_cells, f->d_cell_ll, f->d_cell_nan, f->m_out_ll, f->m_out_nan);
+    ++f->seq;
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kRedThreads), 0, f->stream, f->n_cells, f->d_cell_ll, f->d_cell_nan,
+                       f->m_out_ll, f->m_out_nan, f->m_out_seq, f->seq);
+    f->seq_pending = true;
     HIPCHK(hipGetLastError());
     return GGP_OK;
 }
@@ -1345,6 +1362,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     f->wave_max_cells = (int64_t)f->n_cu * 4 * 3;
     f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
     if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
     if (const char *e = getenv("GGP_GROUP_CPW")) {
         const int v = atoi(e);
@@ -1406,14 +1424,17 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     if (rc == GGP_OK && nc > 0 && hipMemset(f->d_state, 0, (size_t)nc * 20 * sizeof(double)) != hipSuccess) rc = GGP_EDEV;
     if (rc == GGP_OK) {   // the result slot: 16 B of pinned host memory the reduction writes over the bus
         void *h = nullptr, *m = nullptr;
-        if (hipHostMalloc(&h, 2 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        if (hipHostMalloc(&h, 3 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
         } else {
             f->h_out_ll = (double *)h;
             f->h_out_nan = (int64_t *)((char *)h + sizeof(double));
+            f->h_out_seq = (volatile int64_t *)((char *)h + 2 * sizeof(double));
+            *f->h_out_seq = 0;
             if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) rc = GGP_EDEV;
             f->m_out_ll = (double *)m;
             f->m_out_nan = (int64_t *)((char *)m + sizeof(double));
+            f->m_out_seq = (int64_t *)((char *)m + 2 * sizeof(double));
         }
     }
     if (rc != GGP_OK) {
@@ -1561,6 +1582,7 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
     if (f->n_cells == 0) {
         *f->h_out_ll = 0.0;
         *f->h_out_nan = 0x7fffffffffffffffLL;
+        f->seq_pending = false;
         return GGP_OK;
     }
     return launch_levels(f, P);
@@ -1569,7 +1591,16 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
 int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
     if (!f) return GGP_EINVAL;
-    HIPCHK(hipStreamSynchronize(f->stream));
+    bool seen = false;
+    if (f->spin && f->seq_pending) {
+        for (uint32_t it = 1;; ++it) {
+            if (*f->h_out_seq == f->seq) { seen = true; break; }
+            if ((it & 1023) == 0 && hipStreamQuery(f->stream) != hipErrorNotReady) break;
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    f->seq_pending = false;
+    if (!seen || f->profile) HIPCHK(hipStreamSynchronize(f->stream));
     const double v = *f->h_out_ll;
     const int64_t code = *f->h_out_nan;
     if (ll) *ll = v;
@@ -1662,7 +1693,7 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
             HIPCHK(hipGetLastError());
         }
         hipLaunchKernelGGL(k_reduce, dim3((unsigned)np), dim3(kRedThreads), 0, f->stream, nc, f->d_b_ll, f->d_b_nan,
-                           f->d_b_out_ll, f->d_b_out_nan);
+                           f->d_b_out_ll, f->d_b_out_nan, (int64_t *)nullptr, (int64_t)0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(ll + p0, f->d_b_out_ll, (size_t)np * sizeof(double), hipMemcpyDeviceToHost, f->stream));
         HIPCHK(hipMemcpyAsync(nan_code.data(), f->d_b_out_nan, (size_t)np * sizeof(int64_t), hipMemcpyDeviceToHost,
