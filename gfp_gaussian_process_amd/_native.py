@@ -64,6 +64,7 @@ ENGINE_SYMBOLS = {
                                   ctypes.c_int64, ctypes.c_int64, c_int64_p, c_double_p, c_int64_p]),
     "ggp_reset_state": (ctypes.c_int, [ctypes.c_void_p]),
     "ggp_get_state": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "ggp_set_state": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "ggp_last_launch_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                                c_int64_p, c_int32_p, ctypes.c_int32, c_int32_p]),
     "ggp_forest_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int32_p]),

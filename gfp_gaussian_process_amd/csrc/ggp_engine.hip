@@ -1573,6 +1573,15 @@ int ggp_get_state(ggp_forest *f, double *out)
     return GGP_OK;
 }
 
+int ggp_set_state(ggp_forest *f, const double *in)
+{
+    if (!f || !in) return GGP_EINVAL;
+    HIPCHK(hipSetDevice(f->device));
+    HIPCHK(hipStreamSynchronize(f->stream));
+    if (f->n_cells) HIPCHK(hipMemcpy(f->d_state, in, (size_t)f->n_cells * 20 * sizeof(double), hipMemcpyHostToDevice));
+    return GGP_OK;
+}
+
 int ggp_total_loglik_async(ggp_forest *f, const double *params)
 {
     if (!f || !params) return GGP_EINVAL;

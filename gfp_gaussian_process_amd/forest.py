@@ -362,6 +362,13 @@ class Forest:
         self._check(self._lib.ggp_get_state(self._h, out.ctypes.data_as(N.c_double_p)))
         return out
 
+    def set_state(self, state) -> None:
+        """restore a carried state read by state() (checkpoint / resume of a chain)"""
+        st = np.ascontiguousarray(state, np.float64)
+        if st.shape != (self.n_cells, N.STATE):
+            raise ValueError(f"state must be [{self.n_cells}, {N.STATE}], got {st.shape}")
+        self._check(self._lib.ggp_set_state(self._h, st.ctypes.data_as(N.c_double_p)))
+
     def predict(self, params_per_segment, outputs=(True, True, True)):
         """-p smoother (ggp_predict): (forward, backward, combined) [n_rows, 20] arrays; an output
         whose flag in `outputs` is False is not copied back and comes back as None"""

@@ -127,9 +127,12 @@ int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine);
 int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo,
                int64_t r_hi, int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out);
 
-/* carried state: zero it (fresh cells), or read it back ([n_cells*20]) */
+/* carried state: zero it (fresh cells), read it back, or restore one read earlier
+ * ([n_cells*20], cells in input order) -- a checkpoint of the MOMAdata mean/cov a scan or
+ * optimiser run has reached, so a resumed run continues the same chain of values */
 int ggp_reset_state(ggp_forest *f);
 int ggp_get_state(ggp_forest *f, double *out);
+int ggp_set_state(ggp_forest *f, const double *in);
 
 /* measurement hooks (bench.py): HIP-event timings of the launches of the last
  * ggp_total_loglik on the handle's stream.  ms[i], rows[i], kernel[i] for i < *n (cap

@@ -428,3 +428,62 @@ def test_batched_hessian_matches_point_formula(example_forests):
         for j in range(4):
             want = (ll[i, j, 0] - ll[i, j, 1] - ll[i, j, 2] + ll[i, j, 3]) / (4 * h[i] * h[j])
             assert H[i, j] == want
+
+
+def _tests_h_cell():
+    """the reference's own likelihood test cell (src/tests.h:263-300, commented out there): one
+    root, 3 rows at t = 0, 15, 30, a prior covariance whose off-diagonals the root keeps
+    (init_sc_distribution resets only the mean and the diagonal, predictions.h:63-78)"""
+    import gfp_gaussian_process_amd as g
+    cov = np.array([[4.25476409e-02, 4.81488709e+01, -6.17116203e-05, -1.25892662e-01],
+                    [4.81488709e+01, 1.67680116e+06, 2.59861605e-01, 7.45274531e+02],
+                    [-6.17116203e-05, 2.59861605e-01, 8.48575294e-07, 8.44383560e-05],
+                    [-1.25892662e-01, 7.45274531e+02, 8.44383560e-05, 1.63738212e+00]])
+    mean = np.array([6.93147181e-01, 6.03801845e+03, 1.00811380e-02, 9.56031050e+00])
+    a = dict(row_offset=np.array([0, 3], np.int64), parent=np.array([-1], np.int32),
+             daughter1=np.array([-1], np.int32), daughter2=np.array([-1], np.int32),
+             segment=np.zeros(3, np.int32), time=np.array([0.0, 15.0, 30.0]),
+             log_length=np.array([0.6621376048238568, 0.8057995840040671, 1.016156660637409]),
+             fp=np.array([6031.236638936349, 6179.754023612084, 6351.815340631341]),
+             root_mean_xg=mean[:2].copy(), root_var_xg=np.array([cov[0, 0], cov[1, 1]]),
+             leaf_mean_xg=mean[:2].copy(), leaf_var_xg=np.array([cov[0, 0], cov[1, 1]]),
+             noise_scaled=1, division_binomial=1, fp_auto=0.0)
+    state = np.concatenate([mean, cov.ravel()])[None, :]
+    params = [0.01, 0.01, 1e-05, 10, 0.01, 0.1, 0.001, 0.001, 5000.0, 0.001, 5000.0]
+    return g.HostForest(a), state, params
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_tests_h_cell_with_carried_covariance(kernel):
+    """ggp_set_state puts the test cell's covariance in the carried state; the GPU then follows
+    the oracle on it for three chained calls (parity unpinned against the reference binary: its
+    test prints the value but records none)"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf, state, params = _tests_h_cell()
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
+    fg.set_state(state)
+    of.state[:] = state
+    assert np.array_equal(fg.state(), state)
+    for call in range(3):
+        vg = fg.total_likelihood(params)
+        vo, nc, _ = of.total_likelihood(params)
+        assert nc == -1 and math.isfinite(vo)
+        assert _rel(vg, vo) < REL, (call, vg, vo)
+
+
+def test_set_state_resumes_the_chain(example_forests):
+    """checkpoint / resume: a forest given another's carried state continues its chain bitwise"""
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P = CONFIGS[0][2]
+    a = g.Forest(hf)
+    a.total_likelihood(P)
+    a.total_likelihood(P)
+    ckpt = a.state()
+    b = g.Forest(hf)
+    b.set_state(ckpt)
+    for _ in range(2):
+        assert b.total_likelihood(P) == a.total_likelihood(P)
+    with pytest.raises(ValueError):
+        b.set_state(ckpt[:-1])
