@@ -205,6 +205,31 @@ class HostForest:
             raise GGPError(_host_err())
         return cls._from_handle(h, with_ids=with_ids)
 
+    # -- binary SoA in/out (forests far beyond CSV scale) --
+    _SCALARS = ("noise_scaled", "division_binomial", "fp_auto")
+
+    def save(self, path: str) -> None:
+        """the flattened forest as one .npz (SoA arrays as stored, ids as fixed-width text)"""
+        out = {k: np.asarray(v) for k, v in self.a.items()}
+        if self.ids is not None:
+            out["_ids"] = np.array(self.ids, dtype=np.str_)
+            out["_parent_ids"] = np.array(self.parent_ids, dtype=np.str_)
+        if self.rows is not None:
+            out["_rows"] = np.asarray(self.rows, np.int64)
+        np.savez(path, **out)
+
+    @classmethod
+    def load(cls, path: str) -> "HostForest":
+        """read a forest written by save() (numpy's loader with allow_pickle=False)"""
+        with np.load(path, allow_pickle=False) as z:
+            a = {k: z[k] for k in z.files if not k.startswith("_")}
+            for k in cls._SCALARS:
+                a[k] = a[k].item()
+            ids = [str(x) for x in z["_ids"]] if "_ids" in z.files else None
+            pids = [str(x) for x in z["_parent_ids"]] if "_parent_ids" in z.files else None
+            rows = z["_rows"] if "_rows" in z.files else None
+        return cls(a, ids, pids, rows)
+
     # -- properties --
     @property
     def n_cells(self) -> int:

@@ -16,7 +16,12 @@ it reads /root/reference, which does not exist on the GPU box).
                        state chain of 3 calls) -- regression pin of the oracle itself
                        (self-generated: "parity unpinned" against a reference run)
 
-Doubles are stored as float.hex strings (exact).
+  oracle_example_predict.npz  -p of the CPU oracle on the example: forward / backward /
+                       combined state of every cell's first and last row + sha256 of all rows
+  oracle_tests_h_cell.json   the oracle's 3-call chain on the reference's tests.h:263-300 cell
+
+Doubles are stored as float.hex strings (exact) or in .npz (exact, loaded without pickle).
+`--oracle-only` regenerates just the two oracle fixtures from the committed example data.
 """
 from __future__ import annotations
 
@@ -176,7 +181,54 @@ def oracle_fixture(csv_path: str):
     return out
 
 
+def oracle_predict_fixture(csv_path: str):
+    """-p of the CPU oracle on the example (scaled / binomial, the example parameters): the
+    forward, backward and combined state of the first and last row of every cell, plus a
+    sha256 of the full [n_rows, 20] arrays (SURVEY.md §8(c) golden vector 7)"""
+    import hashlib
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.from_csv(csv_path, os.path.join(HERE, "example_csv_config.txt"), -1, "scaled", "binomial")
+    fwd, bwd, comb = O.OracleForest(hf.a).predict(PARAM_SETS["example"])
+    ro = hf.a["row_offset"]
+    rows = np.unique(np.concatenate([ro[:-1], ro[1:] - 1])).astype(np.int64)
+    sha = hashlib.sha256(b"".join(np.ascontiguousarray(x).tobytes() for x in (fwd, bwd, comb))).hexdigest()
+    np.savez_compressed(os.path.join(HERE, "oracle_example_predict.npz"), rows=rows, fwd=fwd[rows], bwd=bwd[rows],
+                        comb=comb[rows], params=np.array(PARAM_SETS["example"]),
+                        sha256=np.frombuffer(bytes.fromhex(sha), np.uint8))
+    return len(rows), sha
+
+
+def oracle_tests_h_fixture():
+    """the reference's own likelihood test cell (src/tests.h:263-300) with its covariance as
+    the carried state: the oracle's chain of 3 calls (SURVEY.md §8(c) golden vector 4)"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import pytest  # noqa: F401  (test module imports)
+    from oracle import oracle as O
+    src = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read()
+    i = src.index("def _tests_h_cell")
+    j = src.index("@pytest.mark.parametrize", i)
+    ns = {"np": np}
+    exec(src[i:j], ns)
+    hf, state, params = ns["_tests_h_cell"]()
+    of = O.OracleForest(hf.a)
+    of.state[:] = state
+    vals = [of.total_likelihood(params)[0] for _ in range(3)]
+    out = {"params": [hx(p) for p in params], "state": [hx(v) for v in state.ravel()], "ll": [hx(v) for v in vals]}
+    json.dump(out, open(os.path.join(HERE, "oracle_tests_h_cell.json"), "w"), indent=1)
+    return vals
+
+
 def main():
+    if "--oracle-only" in sys.argv:   # fixtures that need only the committed example data
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            csv = os.path.join(td, "input.csv")
+            with gzip.open(os.path.join(HERE, "example_input.csv.gz"), "rb") as fi, open(csv, "wb") as fo:
+                shutil.copyfileobj(fi, fo)
+            print("predict rows:", oracle_predict_fixture(csv))
+        print("tests.h cell:", oracle_tests_h_fixture())
+        return
     src = os.path.join(REF, "example_data_set")
     with open(os.path.join(src, "input.csv"), "rb") as fi, gzip.open(os.path.join(HERE, "example_input.csv.gz"), "wb", 9) as fo:
         shutil.copyfileobj(fi, fo)
@@ -191,6 +243,8 @@ def main():
     o = oracle_fixture(os.path.join(src, "input.csv"))
     for k, v in o.items():
         print(k, [float.fromhex(x) for x in v["ll"]], v["nan"])
+    print("predict rows:", oracle_predict_fixture(os.path.join(src, "input.csv")))
+    print("tests.h cell:", oracle_tests_h_fixture())
 
 
 if __name__ == "__main__":

@@ -487,3 +487,27 @@ def test_set_state_resumes_the_chain(example_forests):
         assert b.total_likelihood(P) == a.total_likelihood(P)
     with pytest.raises(ValueError):
         b.set_state(ckpt[:-1])
+
+
+def test_predict_example_vs_committed_fixture(example_forests):
+    """GPU -p against the committed oracle fixture (first and last row of every cell), so the
+    GPU box checks the smoother without rerunning the oracle"""
+    import gfp_gaussian_process_amd as g
+    gold = np.load(os.path.join(GOLDEN, "oracle_example_predict.npz"))
+    hf = example_forests[("scaled", "binomial")]
+    got = g.Forest(hf).predict(list(gold["params"]))
+    rows = gold["rows"]
+    for name, x in zip(("fwd", "bwd", "comb"), got):
+        em, ec = _smoother_err(x[rows], gold[name])
+        assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
+
+
+def test_tests_h_cell_vs_committed_fixture():
+    import gfp_gaussian_process_amd as g
+    gold = json.load(open(os.path.join(GOLDEN, "oracle_tests_h_cell.json")))
+    hf, state, params = _tests_h_cell()
+    assert np.array_equal(state.ravel(), [float.fromhex(x) for x in gold["state"]])
+    f = g.Forest(hf)
+    f.set_state(state)
+    for want in gold["ll"]:
+        assert _rel(f.total_likelihood(params), float.fromhex(want)) < REL

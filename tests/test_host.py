@@ -207,3 +207,25 @@ def test_engine_library_loads_without_gpu():
     lib = N.engine()
     assert lib.ggp_version().decode().startswith("ggp-mi355x")
     assert lib.ggp_strerror(N.GGP_ENAN).decode() == "Likelihood is Nan"
+
+
+def test_forest_binary_roundtrip(tmp_path, example_paths):
+    """HostForest.save / load: the SoA arrays, scalars and ids come back exactly, and the oracle
+    gives the same likelihood on the reloaded forest"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.from_csv(example_paths["csv"], example_paths["config"])
+    path = str(tmp_path / "forest.npz")
+    hf.save(path)
+    back = g.HostForest.load(path)
+    assert back.ids == hf.ids and back.parent_ids == hf.parent_ids
+    assert set(back.a) == set(hf.a)
+    for k, v in hf.a.items():
+        assert np.array_equal(np.asarray(back.a[k]), np.asarray(v)), k
+        assert np.asarray(back.a[k]).dtype == np.asarray(v).dtype, k
+    P = g.ParameterSet.load(example_paths["params"]).get_init()
+    assert O.OracleForest(back.a).total_likelihood(P)[0] == O.OracleForest(hf.a).total_likelihood(P)[0]
+    syn = g.HostForest.synthetic(20, 30)
+    syn.save(path)
+    s2 = g.HostForest.load(path)
+    assert s2.ids is None and np.array_equal(s2.a["time"], syn.a["time"])

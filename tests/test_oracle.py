@@ -141,3 +141,46 @@ def test_oracle_reports_first_nan(example_paths):
     of = O.OracleForest(hf.a)
     v, cell, row = of.total_likelihood(P)
     assert math.isnan(v) and cell == 0 and row >= 0
+
+
+def test_oracle_predict_regression(example_paths):
+    """-p of the oracle on the example against its committed fixture: first and last row of every
+    cell bitwise, and the sha256 of all rows (make_golden.py oracle_predict_fixture)"""
+    import hashlib
+    import os
+    import gfp_gaussian_process_amd as g
+    from conftest import GOLDEN
+    from oracle import oracle as O
+    gold = np.load(os.path.join(GOLDEN, "oracle_example_predict.npz"))
+    hf = g.HostForest.from_csv(example_paths["csv"], example_paths["config"], -1, "scaled", "binomial")
+    fwd, bwd, comb = O.OracleForest(hf.a).predict(list(gold["params"]))
+    rows = gold["rows"]
+    ro = hf.a["row_offset"]
+    assert set(rows) == set(ro[:-1]) | set(ro[1:] - 1)
+    for name, x in (("fwd", fwd), ("bwd", bwd), ("comb", comb)):
+        assert np.array_equal(x[rows], gold[name]), name
+    sha = hashlib.sha256(b"".join(np.ascontiguousarray(x).tobytes() for x in (fwd, bwd, comb))).digest()
+    assert sha == bytes(gold["sha256"])
+
+
+def test_oracle_tests_h_cell_regression():
+    """the reference's tests.h:263-300 cell with its carried covariance: the oracle's chain"""
+    import os
+    from conftest import GOLDEN
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    gold = _load("oracle_tests_h_cell.json")
+    params = [float.fromhex(x) for x in gold["params"]]
+    state = np.array([float.fromhex(x) for x in gold["state"]]).reshape(1, 20)
+    a = dict(row_offset=np.array([0, 3], np.int64), parent=np.array([-1], np.int32),
+             daughter1=np.array([-1], np.int32), daughter2=np.array([-1], np.int32),
+             segment=np.zeros(3, np.int32), time=np.array([0.0, 15.0, 30.0]),
+             log_length=np.array([0.6621376048238568, 0.8057995840040671, 1.016156660637409]),
+             fp=np.array([6031.236638936349, 6179.754023612084, 6351.815340631341]),
+             root_mean_xg=state[0, :2].copy(), root_var_xg=np.array([state[0, 4], state[0, 9]]),
+             leaf_mean_xg=state[0, :2].copy(), leaf_var_xg=np.array([state[0, 4], state[0, 9]]),
+             noise_scaled=1, division_binomial=1, fp_auto=0.0)
+    of = O.OracleForest(g.HostForest(a).a)
+    of.state[:] = state
+    got = [of.total_likelihood(params)[0] for _ in range(3)]
+    assert got == [float.fromhex(x) for x in gold["ll"]]
