@@ -196,7 +196,8 @@ GGP_DEV double dawson_arg(const Step &S, const LaneTasks &T)
 GGP_DEV double dawson_bf(const double x, const double *tab)
 {
     const double ax = fabs(x);
-    const double y100 = 100.0 / (1.0 + ax);
+    const double d1 = 1.0 + ax;
+    const double y100 = rdiv(100.0, d1, frcp(d1));   // IEEE 100 / (1 + ax) for finite ax
     const double yk = y100 >= 0.0 ? y100 : 0.0;
     const int k = min((int)yk, GGP_DAWSON_NINT - 1);
     const double *c = tab + GGP_DAWSON_NCOEF * k;
