@@ -511,3 +511,53 @@ def test_tests_h_cell_vs_committed_fixture():
     f.set_state(state)
     for want in gold["ll"]:
         assert _rel(f.total_likelihood(params), float.fromhex(want)) < REL
+
+
+_GATHER_CHILD = r'''
+import os, sys, time, json, math
+sys.path.insert(0, ROOT)
+import torch, torch.distributed as dist
+import numpy as np
+import gfp_gaussian_process_amd as g
+from gfp_gaussian_process_amd.distributed import ShardedObjective
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+P = PARAMS
+hf = g.HostForest.synthetic(1000, 200)
+a, b = g.Forest(hf), g.Forest(hf)
+obj = ShardedObjective(a, always_gather=True)
+same = all(obj.total_likelihood(P) == b.total_likelihood(P) for _ in range(3))
+bad = list(P); bad[2] = -1.0
+try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
+    ShardedObjective(g.Forest(hf), always_gather=True).total_likelihood(bad); nan_ok = False
+except g.LikelihoodIsNan:
+    nan_ok = True
+t = {}
+for name, fn in (("direct", b.total_likelihood), ("gather", obj.total_likelihood)):
+    for _ in range(20): fn(P)
+    t0 = time.perf_counter()
+    for _ in range(200): fn(P)
+    t[name] = 1e3 * (time.perf_counter() - t0) / 200
+dist.destroy_process_group()
+print(json.dumps({"same": same, "nan_ok": nan_ok, "ms": t}))
+'''
+
+
+def test_sharded_objective_collective_path_on_rccl():
+    """ShardedObjective's RCCL path (pinned staging, all_gather, rank-order sum) on a 1-rank
+    nccl group in a child process: bitwise the direct objective over a carried-state chain,
+    NaN raised; prints the per-call cost of the collective path"""
+    import socket
+    import subprocess
+    import sys
+    from conftest import ROOT
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    code = f"ROOT={ROOT!r}\nPARAMS={list(CONFIGS[0][2])!r}\n" + _GATHER_CHILD
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    print("collective path ms/call:", out["ms"])
+    assert out["same"] and out["nan_ok"]
