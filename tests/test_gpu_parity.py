@@ -527,6 +527,9 @@ hf = g.HostForest.synthetic(1000, 200)
 a, b = g.Forest(hf), g.Forest(hf)
 obj = ShardedObjective(a, always_gather=True)
 same = all(obj.total_likelihood(P) == b.total_likelihood(P) for _ in range(3))
+for _ in range(5):   # fresh objectives: their first collective is ordered after the engine
+    a2, b2 = g.Forest(hf), g.Forest(hf)
+    same = same and ShardedObjective(a2, always_gather=True).total_likelihood(P) == b2.total_likelihood(P)
 bad = list(P); bad[2] = -1.0
 try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
     ShardedObjective(g.Forest(hf), always_gather=True).total_likelihood(bad); nan_ok = False
