@@ -491,9 +491,10 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     const double rgl = S.r_gl, rgq = S.r_gq;
     const double ebt = X[XS_bt], ebglt = X[XS_bglt], e2bt = X[XS_2bt], ebgqt = X[XS_bgqt];
     const double egl = X[XS_gl], egq = X[XS_gq];
-    const double r_ebt = 1.0 / ebt, r_ebglt = 1.0 / ebglt, r_ebgqt = 1.0 / ebgqt;
+    // rdiv seeds only (frcp)
+    const double r_ebt = frcp(ebt), r_ebglt = frcp(ebglt), r_ebgqt = frcp(ebgqt);
     const double ebt_gl = ebt * gl, ebglt_gl = ebglt * gl;
-    const double r_ebt_gl = 1.0 / ebt_gl, r_ebglt_gl = 1.0 / ebglt_gl;
+    const double r_ebt_gl = frcp(ebt_gl), r_ebglt_gl = frcp(ebglt_gl);
     const double gq2 = S.gq2, gqq2 = S.gqq2;
     const double r_gq2 = S.r_gq2, r_gqq2 = S.r_gqq2;
 #define DGL(x) rdiv((x), gl, rgl)
@@ -630,7 +631,7 @@ GGP_DEV void cross_outputs(const Step &S, const IA &I, const XA &X, double *K)
     const double Cgq = S.Cgq, Cll = S.Cll, Clq = S.Clq, Cqq = S.Cqq;
     const double gl = S.gl, mq = S.mq, rgl = S.r_gl;
     const double ebt = X[XS_bt], egl = X[XS_gl], egq = X[XS_gq];
-    const double r_ebt = 1.0 / ebt;
+    const double r_ebt = frcp(ebt);   // rdiv seed
     // nm(1): mean_g at the end of the step, the same expression as outputs()
     const double nm1 = rdiv(bg, ebt, r_ebt) + Clq * I[O_2A] + mq * I[Z_1A] + (bq + Cxq - mq) * I[Z_2A];
     K[0] = Cxx + rdiv(Cxl * (1 - egl), gl, rgl);
@@ -698,7 +699,7 @@ GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, c
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
         PW[p] = pow_task(S, p);
-        PW[3 + p] = 1.0 / PW[p];
+        PW[3 + p] = frcp(PW[p]);   // rdiv seeds
     }
     double I[NI];
     lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
