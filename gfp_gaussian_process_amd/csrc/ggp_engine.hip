@@ -1091,7 +1091,7 @@ struct ggp_forest {
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
     int auto_small = GGP_KERNEL_WAVE;   // auto's schedule for small levels
-    int64_t wave_max_cells = 3072;    // auto: wave schedule for levels up to this size
+    int64_t wave_max_cells = 5120;    // auto: wave schedule for levels up to this size
     int64_t group_max_cells = 8192;   // auto: group schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int kernel_used = GGP_KERNEL_LANE;
@@ -1161,7 +1161,7 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             HIPCHK(hipEventRecord(f->ev[2 * f->n_prof], f->stream));
         }
         const int64_t n_simd = (int64_t)f->n_cu * 4;
-        // auto (measured, profiles/r04_schedule_scan.txt): up to 3 cells per SIMD the wave
+        // auto (measured, profiles/r08_schedule_scan.txt): up to 5 cells per SIMD the wave
         // schedule (GGP_AUTO_SMALL=group: the bitwise-lane-equal one), up to 8 per SIMD the
         // group schedule with 1-8 cells per wave, above that the lane schedule
         const int kind = f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
@@ -1359,7 +1359,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess) f->n_cu = prop.multiProcessorCount;
-    f->wave_max_cells = (int64_t)f->n_cu * 4 * 3;
+    f->wave_max_cells = (int64_t)f->n_cu * 4 * 5;   // r08 scan: wave ahead of group up to ~5 cells/SIMD
     f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
     if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
     if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;

@@ -76,7 +76,7 @@ typedef struct {
     int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
 } ggp_forest_desc;
 
-#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 3 cells per SIMD, GROUP up to
+#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 5 cells per SIMD, GROUP up to
                                  8, LANE above (measured crossovers)       */
 #define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
 #define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
