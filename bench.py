@@ -27,6 +27,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
+# FP64 VALU work of k_loglik_wave per update, all 64 lanes counted (redundant update lanes
+# included): (ADD + MUL + 2 FMA + TRANS) x 64 per launch / rows per launch, from the PMC pass
+# profiles/r09_fp64_pmc.txt (3.843e7 wave-instructions x 64 / 1.0e5 rows on C2)
+WAVE_FP64_FLOPS_PER_UPDATE = 24593.0
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (AMD spec)
 COMBINE_BYTES_PER_ROW = 484   # k_combine: fwd + bwd rows (2 x 160 B) + prior segment (4 B) read, 160 B written
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
              3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
@@ -246,6 +251,13 @@ def main() -> int:
                 "per_kernel_ms": {k: v[0] / v[2] for k, v in per.items()},
                 "note": "algorithmic bytes only; the path is FP64-latency/VALU bound (DESIGN.md)",
             },
+            "fp64": ({
+                "kernel": dom, "flops_per_update": WAVE_FP64_FLOPS_PER_UPDATE,
+                "achieved": WAVE_FP64_FLOPS_PER_UPDATE * (d_rows / d_n) / (avg_ms * 1e-3) / 1e12,
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": WAVE_FP64_FLOPS_PER_UPDATE * (d_rows / d_n) / (avg_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                "source": "profiles/r09_fp64_pmc.txt: SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes (FMA = 2)",
+            } if dom == "k_loglik_wave" and avg_ms > 0 else None),
             "total_log_likelihood": ll,
         }
         if large is not None:
