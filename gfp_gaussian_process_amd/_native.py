@@ -34,7 +34,8 @@ class ForestDesc(ctypes.Structure):
         ("root_mean_xg", ctypes.c_double * 2), ("root_var_xg", ctypes.c_double * 2),
         ("leaf_mean_xg", ctypes.c_double * 2), ("leaf_var_xg", ctypes.c_double * 2),
         ("noise_scaled", ctypes.c_int32), ("division_binomial", ctypes.c_int32),
-        ("fp_auto", ctypes.c_double), ("device", ctypes.c_int32), ("kernel", ctypes.c_int32),
+        ("fp_auto", ctypes.c_double), ("n_devices", ctypes.c_int32), ("kernel", ctypes.c_int32),
+        ("devices", c_int32_p), ("max_shard_rows", ctypes.c_int64),
     ]
 
 
@@ -68,6 +69,11 @@ ENGINE_SYMBOLS = {
     "ggp_last_launch_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                                c_int64_p, c_int32_p, ctypes.c_int32, c_int32_p]),
     "ggp_forest_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int32_p]),
+    "ggp_forest_shards": (ctypes.c_int, [ctypes.c_void_p, c_int32_p, c_int32_p, c_int64_p, c_int64_p,
+                                         ctypes.c_int32]),
+    "ggp_predict_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p]),
+    "ggp_debug_dawson": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, c_double_p, ctypes.c_int64, c_double_p]),
+    "ggp_debug_tauint": (ctypes.c_int, [ctypes.c_int32, c_double_p, ctypes.c_int64, c_double_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),
     "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "ggp_version": (ctypes.c_char_p, []),

@@ -1006,53 +1006,137 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
     if (!out_off) counts[i] = cnt;
 }
 
-// ------------------------------------------------------------------------------------------
-// Deterministic total: sum cell_ll in DFS pre-order (the reference's accumulation order at
-// cell granularity) with a fixed-shape tree; first NaN = min over (dfs rank, row).
-// ------------------------------------------------------------------------------------------
-constexpr int kRedThreads = 1024;
 
-__global__ __launch_bounds__(kRedThreads) void k_reduce(int64_t n, const double *__restrict__ cell_ll,
-                                                         const int32_t *__restrict__ cell_nan,
-                                                         double *__restrict__ out_ll,
-                                                         int64_t *__restrict__ out_nan,
-                                                         int64_t *__restrict__ out_seq, int64_t seq)
+// ------------------------------------------------------------------------------------------
+// Deterministic total whose bits do not depend on how the forest is sharded over devices:
+//   tree sum  : a tree's cell partials in DFS pre-order, added one after another (within a
+//               tree: the reference's own accumulation order, likelihood.h:110-122, at cell
+//               granularity)
+//   block sum : B consecutive trees of the global root order (B from the tree count only),
+//               one workgroup, a fixed LDS tree
+//   total     : the block sums in global block order, a fixed pairwise tree (host, top_sum)
+// A block always lives whole on one shard, so N shards give the same bits as one.  The first
+// NaN is the min over (global DFS rank << 24 | row): the reference's order (likelihood.h:71-93).
+// ------------------------------------------------------------------------------------------
+constexpr int kRedMax = 1024;
+constexpr long long kNoNan = 0x7fffffffffffffffLL;
+
+__global__ __launch_bounds__(kRedMax) void k_reduce_blocks(int64_t n_cells, const double *__restrict__ cell_ll,
+                                                            const int32_t *__restrict__ cell_nan,
+                                                            const int64_t *__restrict__ tree_dfs,
+                                                            const int32_t *__restrict__ blk_t0,
+                                                            const int32_t *__restrict__ blk_nt,
+                                                            const int32_t *__restrict__ gdfs, int n_lblocks,
+                                                            double *__restrict__ out_sum, int64_t *__restrict__ out_nan,
+                                                            unsigned *__restrict__ done, int64_t *__restrict__ out_seq,
+                                                            int64_t seq)
 {
-    // cell_ll / cell_nan are stored in DFS order (F.dfs_rank): each thread adds a contiguous
-    // chunk in that order, then a fixed pairwise tree over the threads (deterministic)
-    __shared__ double s_sum[kRedThreads];
-    __shared__ long long s_nan[kRedThreads];
-    const int tid = threadIdx.x;
-    cell_ll += (int64_t)blockIdx.x * n;   // one block per parameter point (a single evaluation: 1)
-    cell_nan += (int64_t)blockIdx.x * n;
-    out_ll += blockIdx.x;
-    out_nan += blockIdx.x;
-    const int64_t lo = n * tid / kRedThreads, hi = n * (tid + 1) / kRedThreads;
-    double acc = 0.0;
-    long long first = 0x7fffffffffffffffLL;
-    for (int64_t i = lo; i < hi; ++i) {
-        acc += cell_ll[i];
-        const int nr = cell_nan[i];
-        if (nr != kNanNone && first == 0x7fffffffffffffffLL) first = (i << 24) | (long long)nr;
+    __shared__ double s_sum[kRedMax];
+    __shared__ long long s_nan[kRedMax];
+    const int tid = threadIdx.x, nt = blockDim.x, j = blockIdx.x;
+    const int64_t pt = blockIdx.y;             // batch point (a single evaluation: 0)
+    cell_ll += pt * n_cells;
+    cell_nan += pt * n_cells;
+    double v = 0.0;
+    long long code = kNoNan;
+    if (tid < blk_nt[j]) {
+        const int64_t t = blk_t0[j] + tid;
+        for (int64_t i = tree_dfs[t]; i < tree_dfs[t + 1]; ++i) {
+            v += cell_ll[i];
+            const int nr = cell_nan[i];
+            if (nr != kNanNone && code == kNoNan) code = ((long long)gdfs[i] << 24) | (long long)nr;
+        }
     }
-    s_sum[tid] = acc;
-    s_nan[tid] = first;
+    s_sum[tid] = v;
+    s_nan[tid] = code;
     __syncthreads();
-    for (int w = kRedThreads / 2; w > 0; w >>= 1) {
+    for (int w = nt / 2; w > 0; w >>= 1) {
         if (tid < w) {
             s_sum[tid] = s_sum[tid] + s_sum[tid + w];
             s_nan[tid] = min(s_nan[tid], s_nan[tid + w]);
         }
         __syncthreads();
     }
-    if (tid == 0) {   // straight into mapped host memory
-        out_ll[0] = s_sum[0];
-        out_nan[0] = s_nan[0];
-        if (out_seq) {   // then the call's sequence number: the host polls it (ggp_loglik_result)
+    if (tid == 0) {
+        out_sum[pt * n_lblocks + j] = s_sum[0];
+        out_nan[pt * n_lblocks + j] = s_nan[0];
+        if (out_seq) {
+            // the last workgroup to finish publishes the call's sequence number (the host polls
+            // it, ggp_loglik_result); every block's result is fenced before its count
             __threadfence_system();
-            __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned prev = atomicAdd(done, 1u);
+            if (prev + 1 == gridDim.x * gridDim.y) {
+                *done = 0u;                    // ready for the next call (stream ordered)
+                __threadfence_system();
+                __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Test-only device entry points (tests/test_gpu_device_math.py): the device Dawson in both
+// forms the kernels use, and the four tauint integrals of mean_cov_model.h:9-67 built from
+// the same device primitives (rdiv, ocml exp, table Dawson, a^k sqrt(a)) in tau_body's
+// expression order, at arbitrary (t0, t1, a, b, c).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_debug_dawson(const double *__restrict__ x, int64_t n, int variant,
+                                                     double *__restrict__ out)
+{
+    __shared__ double s_tab[kDawsonTab];
+    load_dawson_table(s_tab, threadIdx.x);
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    const double v = i < n ? x[i] : 0.0;
+    // every lane of the wave takes part (the wave form's ballots are wave-wide)
+    const double r = variant == 0 ? ggp_dawson_tab(v, s_tab) : ggp::wave::dawson_bf(v, s_tab);
+    if (i < n) out[i] = r;
+}
+
+GGP_DEV double debug_tauint(const int k, const double t0, const double t1, const double a, const double b,
+                            const double c, const double *tab)
+{
+    // the tauint formulas with the integral bounds as given (mean_cov_model.h:9-67); z, the
+    // exponentials and the powers formed as the propagator forms them (ggp_prop.h)
+    const double sa = sqrt(a);
+    const double two_sa = 2. * sa, m2sa = -2. * sa, two_a = 2. * a, four_a = 4. * a, four_aa = 4 * (a * a);
+    const double r_two_sa = ggp::frcp(two_sa), r_four_a = ggp::frcp(four_a);
+    const double z0 = ggp::rdiv(b + two_a * t0, two_sa, r_two_sa), z1 = ggp::rdiv(b + two_a * t1, two_sa, r_two_sa);
+    const double D0 = ggp_dawson_tab(z0, tab), D1 = ggp_dawson_tab(z1, tab);
+    const double n_ = ggp::rdiv(-(b * b), four_a, r_four_a);
+    if (k == 0) {
+        const double Z0 = exp(a * (t0 * t0) + b * t0 + c), Z1 = exp(a * (t1 * t1) + b * t1 + c);
+        return ggp::rdiv(2. * (-Z0 * D0 + Z1 * D1), two_sa, r_two_sa);
+    }
+    const double E0 = exp(n_ + c + z0 * z0), E1 = exp(n_ + c + z1 * z1);
+    const double ec = exp(c), ea0 = exp(t0 * (b + a * t0)), ea1 = exp(t1 * (b + a * t1));
+    const double pw = k == 1 ? 4. * (a * sa) : k == 2 ? 8. * ((a * a) * sa) : 16. * (((a * a) * a) * sa);
+    const double rpw = ggp::frcp(pw);
+    const double B = b;
+    double x;
+    if (k == 1)
+        x = (m2sa * ec * (ea0 - ea1) + B * 2. * (E0 * D0 - E1 * D1));
+    else if (k == 2)
+        x = (two_sa * ec * (ea0 * (B - two_a * t0) - ea1 * (B - two_a * t1)) +
+             (E0 * (two_a - B * B) * 2. * D0 + E1 * (-two_a + B * B) * 2. * D1));
+    else
+        x = (m2sa * ec *
+             ((B * B) * (ea0 - ea1) - two_a * ea0 * (2. + B * t0) + two_a * ea1 * (2 + B * t1) +
+              four_aa * (ea0 * (t0 * t0) - ea1 * (t1 * t1)))) +
+            E0 * B * (-6. * a + B * B) * 2. * D0 - E1 * B * (-6 * a + B * B) * 2. * D1;
+    return ggp::rdiv(x, pw, rpw);
+}
+
+__global__ __launch_bounds__(64) void k_debug_tauint(const double *__restrict__ in, int64_t n,
+                                                     double *__restrict__ out)
+{
+    __shared__ double s_tab[kDawsonTab];
+    load_dawson_table(s_tab, threadIdx.x);
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const double *q = in + 6 * i;   // k, t0, t1, a, b, c
+    out[i] = debug_tauint((int)q[0], q[1], q[2], q[3], q[4], q[5], s_tab);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1082,9 +1166,43 @@ int dev_upload(T **dst, const T *src, size_t n)
     return GGP_OK;
 }
 
+// trees per reduction block: a function of the tree count only (the sum's shape must not depend
+// on the sharding); at most 1024 (one workgroup), about 256-512 blocks for large forests
+int64_t block_trees_for(int64_t n_trees)
+{
+    int64_t B = 1;
+    while (B < kRedMax && B * 256 < n_trees) B *= 2;
+    return B;
+}
+
+// fixed pairwise tree over the block sums in global order (zero padded to a power of two)
+double top_sum(std::vector<double> v)
+{
+    size_t n = 1;
+    while (n < v.size()) n *= 2;
+    v.resize(n, 0.0);
+    for (; n > 1; n /= 2)
+        for (size_t i = 0; i < n / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+    return v.empty() ? 0.0 : v[0];
+}
+
 }  // namespace
 
-struct ggp_forest {
+// One device (HIP ordinal) used by the handle: its stream, and the -p workspace its shards
+// share (forward + backward rows, sized to the largest shard on the device; shards on one
+// device are smoothed one after another on its stream).
+struct DeviceCtx {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    int n_cu = 256;
+    double *sm_fwd = nullptr, *sm_bwd = nullptr;
+    int64_t sm_rows = 0;
+};
+
+// One shard: whole trees (whole reduction blocks) of the forest, cells in input order, on one
+// device.  Everything below works on the shard's local numbering.
+struct Shard {
+    DeviceCtx *dev = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     int64_t n_cells = 0, n_rows = 0;
@@ -1106,22 +1224,30 @@ struct ggp_forest {
     int32_t *d_row_cell = nullptr;    // -j: cell of every row
     double *d_state = nullptr, *d_cell_ll = nullptr;
     int32_t *d_cell_nan = nullptr;
-    // the result: pinned, mapped host memory that k_reduce writes directly (no copy back)
-    double *h_out_ll = nullptr;
-    int64_t *h_out_nan = nullptr;
-    double *m_out_ll = nullptr;       // device views of the two
-    int64_t *m_out_nan = nullptr;
-    // completion by polling: k_reduce stores the call's sequence number after the result (one
-    // more mapped slot); the host spins on it instead of waiting for the kernel-completion
-    // signal, with hipStreamQuery as the way out if the stream fails (GGP_SPIN=0: synchronise)
-    volatile int64_t *h_out_seq = nullptr;
-    int64_t *m_out_seq = nullptr;
+    // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
+    int64_t n_trees = 0, n_lblocks = 0;
+    int red_threads = 64;
+    int64_t *d_tree_dfs = nullptr;
+    int32_t *d_blk_t0 = nullptr, *d_blk_nt = nullptr, *d_gdfs = nullptr;
+    unsigned *d_done = nullptr;
+    std::vector<int64_t> blk_global;   // local block -> global block
+    // the result: pinned, mapped host memory k_reduce_blocks writes directly (no copy back):
+    // block sums [n_lblocks], first-NaN codes [n_lblocks], then the call's sequence number
+    // (the host spins on it instead of waiting for the kernel-completion signal, with
+    // hipStreamQuery as the way out if the stream fails; GGP_SPIN=0: synchronise)
+    void *h_res = nullptr;
+    double *h_sum = nullptr, *m_sum = nullptr;
+    int64_t *h_nan = nullptr, *m_nan = nullptr;
+    volatile int64_t *h_seq = nullptr;
+    int64_t *m_seq = nullptr;
     int64_t seq = 0;
     bool seq_pending = false;
     bool spin = true;
+    // numbering
+    std::vector<int32_t> cell_g;       // local cell -> global cell (ascending); empty = identity
+    std::vector<int64_t> row_off;      // local row_offset (host copy)
     // schedule
-    std::vector<int64_t> level_start;       // [n_levels+1] into level_cells
-    std::vector<int32_t> h_dfs_order;
+    std::vector<int64_t> level_start;  // [n_levels+1] into level_cells
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> ev;
@@ -1129,27 +1255,41 @@ struct ggp_forest {
     std::vector<int32_t> ev_kernel;   // per profiled launch: kind << 8 | lanes per cell
     std::vector<int64_t> ev_rows_launch;
     int n_prof = 0;
-    // -p workspace, allocated on the first ggp_predict and kept for the handle's lifetime (a
-    // scan of predictions or a bench loop then pays no hipMalloc/hipFree per call)
-    double *d_sm_ptab = nullptr, *d_sm_pstate = nullptr, *d_sm_fwd = nullptr, *d_sm_bwd = nullptr,
-           *d_sm_comb = nullptr;
-    int32_t sm_ptab_cap = 0;   // segments d_sm_ptab holds
+    // -p: per-cell working state, the combined rows (kept in HBM until the next ggp_predict so
+    // ggp_predict_rows can stream them), the parameter table; device-time events
+    double *d_sm_ptab = nullptr, *d_sm_pstate = nullptr, *d_sm_comb = nullptr;
+    int32_t sm_ptab_cap = 0;
     hipEvent_t ev_pred[3] = {nullptr, nullptr, nullptr};   // start, after fwd+bwd, after combine
     bool pred_timed = false;
     // batched-objective workspace (ggp_total_loglik_batch), grown on demand
-    double *d_b_ptab = nullptr, *d_b_state = nullptr, *d_b_ll = nullptr, *d_b_out_ll = nullptr;
+    double *d_b_ptab = nullptr, *d_b_state = nullptr, *d_b_ll = nullptr, *d_b_sum = nullptr;
     int32_t *d_b_nan = nullptr;
-    int64_t *d_b_out_nan = nullptr;
+    int64_t *d_b_code = nullptr;
     int64_t b_cap = 0;   // points the workspace holds
+    // -j: the smoother and the per-row joint tables, kept for the parameters they were made with
+    // (the CLI asks for many start-row ranges with the same parameters)
+    double *d_j_ptab = nullptr, *d_j_pstate = nullptr, *d_j_fwd = nullptr, *d_j_bwd = nullptr;
+    double *d_j_back = nullptr, *d_j_cond = nullptr, *d_j_start = nullptr;
+    std::vector<double> j_params;      // the table the joint tables hold (empty: none)
 };
+
+struct ggp_forest {
+    int64_t n_cells = 0, n_rows = 0, n_trees = 0, blk_trees = 1, n_blocks = 0;
+    std::vector<DeviceCtx *> devs;
+    std::vector<Shard *> shards;
+    std::vector<int32_t> dfs_order;    // global DFS position -> global cell
+    std::vector<int64_t> row_off;      // global row_offset
+};
+
+namespace {
 
 // Lane schedule: a wave's cost per step does not depend on how many of its lanes hold a
 // cell (FP64 issue is per wave-instruction, and the clock falls with the number of busy
 // SIMDs), so cells are packed 64 per wave at every level size (tools/lane_scan.py: 1k-30k
 // trees, cpw 64 fastest everywhere).
-static int lane_cpw(const ggp_forest *f) { return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : 64; }
+int lane_cpw(const Shard *f) { return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : 64; }
 
-static int launch_levels(ggp_forest *f, const ggp_params &P)
+int launch_levels(Shard *f, const ggp_params &P)
 {
     const int n_levels = (int)f->level_start.size() - 1;
     f->n_prof = 0;
@@ -1209,18 +1349,47 @@ static int launch_levels(ggp_forest *f, const ggp_params &P)
             f->n_prof++;
         }
     }
-    ++f->seq;
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kRedThreads), 0, f->stream, f->n_cells, f->d_cell_ll, f->d_cell_nan,
-                       f->m_out_ll, f->m_out_nan, f->m_out_seq, f->seq);
-    f->seq_pending = true;
+    return GGP_OK;
+}
+
+// one evaluation on a shard: the levels, then the block sums straight into mapped host memory
+int shard_launch(Shard *s, const ggp_params &P)
+{
+    if (s->n_cells == 0) return GGP_OK;
+    HIPCHK(hipSetDevice(s->device));
+    const int rc = launch_levels(s, P);
+    if (rc != GGP_OK) return rc;
+    ++s->seq;
+    hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, 1), dim3(s->red_threads), 0, s->stream,
+                       s->n_cells, s->d_cell_ll, s->d_cell_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt, s->d_gdfs,
+                       (int)s->n_lblocks, s->m_sum, s->m_nan, s->d_done, s->m_seq, s->seq);
+    s->seq_pending = true;
     HIPCHK(hipGetLastError());
+    return GGP_OK;
+}
+
+int shard_wait(Shard *s)
+{
+    if (s->n_cells == 0) return GGP_OK;
+    bool seen = false;
+    if (s->spin && s->seq_pending) {
+        for (uint32_t it = 1;; ++it) {
+            if (*s->h_seq == s->seq) { seen = true; break; }
+            if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    s->seq_pending = false;
+    if (!seen || s->profile) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
     return GGP_OK;
 }
 
 // forward then backward pass of the smoother (predictions.h:93-444) into device buffers; pstate
 // is left holding every cell's backward final state (MOMAdata::mean/cov after -p)
-static hipError_t run_smoother(ggp_forest *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd,
-                               double *d_bwd)
+hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd, double *d_bwd)
 {
     const int n_levels = (int)f->level_start.size() - 1;
     hipError_t e = hipMemsetAsync(d_pstate, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream);
@@ -1244,6 +1413,472 @@ static hipError_t run_smoother(ggp_forest *f, const double *d_ptab, int n_seg, d
     }
     return e;
 }
+
+void shard_free_joints(Shard *f)
+{
+    for (double **p : {&f->d_j_ptab, &f->d_j_pstate, &f->d_j_fwd, &f->d_j_bwd, &f->d_j_back, &f->d_j_cond,
+                       &f->d_j_start}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    f->j_params.clear();
+}
+
+void batch_free(Shard *f)
+{
+    for (void *p : {(void *)f->d_b_ptab, (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_sum,
+                    (void *)f->d_b_nan, (void *)f->d_b_code})
+        if (p) (void)hipFree(p);
+    f->d_b_ptab = f->d_b_state = f->d_b_ll = f->d_b_sum = nullptr;
+    f->d_b_nan = nullptr;
+    f->d_b_code = nullptr;
+    f->b_cap = 0;
+}
+
+void shard_destroy(Shard *f)
+{
+    if (!f) return;
+    (void)hipSetDevice(f->device);
+    if (f->stream) (void)hipStreamSynchronize(f->stream);
+    for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
+                    (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
+                    (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell,
+                    (void *)f->d_state, (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_tree_dfs,
+                    (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
+                    (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
+        if (p) (void)hipFree(p);
+    batch_free(f);
+    shard_free_joints(f);
+    for (auto &e : f->ev_pred)
+        if (e) (void)hipEventDestroy(e);
+    if (f->h_res) (void)hipHostFree(f->h_res);
+    for (auto &e : f->ev) (void)hipEventDestroy(e);
+    delete f;
+}
+
+// validated topology of a descriptor: generation depth per cell, the DFS pre-order (roots in
+// input order, daughter1 before daughter2: likelihood_recr) and where each tree starts in it
+int check_topology(const ggp_forest_desc *d, std::vector<int32_t> &depth, std::vector<int32_t> &dfs,
+                   std::vector<int64_t> &tree_start)
+{
+    const int64_t nc = d->n_cells, nr = d->n_rows;
+    if (nc < 0 || nr < 0 || (nc > 0 && (!d->row_offset || !d->parent || !d->daughter1 || !d->daughter2)) ||
+        (nr > 0 && (!d->time || !d->log_length || !d->fp))) {
+        g_last_err = "incomplete forest descriptor";
+        return GGP_EINVAL;
+    }
+    if (nc >= (int64_t)1 << 31 || nr >= (int64_t)1 << 40) { g_last_err = "forest too large"; return GGP_EINVAL; }
+    // bad indices would fault on the device: validate on the host
+    if (nc > 0 && (d->row_offset[0] != 0 || d->row_offset[nc] != nr)) {
+        g_last_err = "row_offset must start at 0 and end at n_rows";
+        return GGP_EINVAL;
+    }
+    for (int64_t c = 0; c < nc; ++c) {
+        if (d->row_offset[c + 1] <= d->row_offset[c]) { g_last_err = "every cell needs >= 1 row"; return GGP_EINVAL; }
+        if (d->row_offset[c + 1] - d->row_offset[c] >= (int64_t)1 << 24) { g_last_err = "a cell has >= 2^24 rows"; return GGP_EINVAL; }
+        for (int32_t v : {d->parent[c], d->daughter1[c], d->daughter2[c]})
+            if (v < -1 || v >= nc || v == c) { g_last_err = "genealogy index out of range"; return GGP_EINVAL; }
+    }
+    depth.assign(nc, -1);
+    dfs.clear();
+    dfs.reserve(nc);
+    tree_start.clear();
+    std::vector<int32_t> stack;
+    for (int64_t r = 0; r < nc; ++r) {
+        if (d->parent[r] != -1) continue;
+        tree_start.push_back((int64_t)dfs.size());
+        depth[r] = 0;
+        stack.push_back((int32_t)r);
+        while (!stack.empty()) {
+            int32_t c = stack.back();
+            stack.pop_back();
+            dfs.push_back(c);
+            for (int32_t ch : {d->daughter2[c], d->daughter1[c]}) {
+                if (ch < 0) continue;
+                if (depth[ch] != -1) { g_last_err = "genealogy is not a forest"; return GGP_EINVAL; }
+                depth[ch] = depth[c] + 1;
+                stack.push_back(ch);
+            }
+        }
+    }
+    tree_start.push_back((int64_t)dfs.size());
+    for (int64_t c = 0; c < nc; ++c)
+        if (depth[c] < 0) { g_last_err = "cell not reachable from a root (cycle)"; return GGP_EINVAL; }
+    // a daughter's parent pointer must be the cell that lists it (single-parent forest)
+    for (int64_t c = 0; c < nc; ++c)
+        for (int32_t ch : {d->daughter1[c], d->daughter2[c]})
+            if (ch >= 0 && d->parent[ch] != c) {
+                g_last_err = "daughter/parent pointers disagree";
+                return GGP_EINVAL;
+            }
+    return GGP_OK;
+}
+
+// A shard from a (sub-)forest descriptor `d` in its own numbering.  gdfs_of_cell: the global
+// DFS rank of every local cell; blk_ntrees: the shard's reduction blocks in order (trees each,
+// consecutive local trees), blk_global: their global indices; B: trees per block.
+int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int32_t> &gdfs_of_cell,
+                 const std::vector<int32_t> &blk_ntrees, const std::vector<int64_t> &blk_global, int64_t B,
+                 Shard **out)
+{
+    *out = nullptr;
+    const int64_t nc = d->n_cells, nr = d->n_rows;
+    std::vector<int32_t> depth, dfs;
+    std::vector<int64_t> tree_start;
+    int rc = check_topology(d, depth, dfs, tree_start);
+    if (rc != GGP_OK) return rc;
+    auto *f = new Shard();
+    f->dev = dev;
+    f->device = dev->id;
+    f->stream = dev->stream;
+    f->n_cells = nc;
+    f->n_rows = nr;
+    f->kernel_pref = d->kernel;
+    f->n_cu = dev->n_cu;
+    f->wave_max_cells = (int64_t)f->n_cu * 4 * 5;   // r08 scan: wave ahead of group up to ~5 cells/SIMD
+    f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
+    if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
+    if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
+    if (const char *e = getenv("GGP_GROUP_CPW")) {
+        const int v = atoi(e);
+        f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+    }
+    if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
+    f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
+    if (nc == 0) f->row_off.assign(1, 0);
+    if (hipSetDevice(f->device) != hipSuccess) {
+        g_last_err = "hipSetDevice failed";
+        delete f;
+        return GGP_EDEV;
+    }
+    auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+    // ---- level schedule: cells by generation depth, each level longest first ----
+    int32_t max_depth = 0;
+    for (int64_t c = 0; c < nc; ++c) max_depth = std::max(max_depth, depth[c]);
+    std::vector<int32_t> level_cells(nc);
+    std::iota(level_cells.begin(), level_cells.end(), 0);
+    std::stable_sort(level_cells.begin(), level_cells.end(), [&](int32_t a, int32_t b) {
+        if (depth[a] != depth[b]) return depth[a] < depth[b];
+        return (d->row_offset[a + 1] - d->row_offset[a]) > (d->row_offset[b + 1] - d->row_offset[b]);
+    });
+    f->level_start.assign(nc > 0 ? max_depth + 2 : 1, 0);
+    for (int64_t c = 0; c < nc; ++c) f->level_start[depth[c] + 1]++;
+    for (size_t L = 1; L < f->level_start.size(); ++L) f->level_start[L] += f->level_start[L - 1];
+    // ---- uploads ----
+    check(dev_upload(&f->d_time, d->time, nr));
+    check(dev_upload(&f->d_logl, d->log_length, nr));
+    check(dev_upload(&f->d_fp, d->fp, nr));
+    check(dev_upload(&f->d_row_off, d->row_offset, nc + 1));
+    check(dev_upload(&f->d_parent, d->parent, nc));
+    check(dev_upload(&f->d_d1, d->daughter1, nc));
+    check(dev_upload(&f->d_d2, d->daughter2, nc));
+    if (d->segment) check(dev_upload(&f->d_seg, d->segment, nr));
+    check(dev_upload(&f->d_level_cells, level_cells.data(), nc));
+    {
+        std::vector<int32_t> rank(nc), gd(nc);
+        for (int64_t k = 0; k < nc; ++k) {
+            rank[dfs[k]] = (int32_t)k;
+            gd[k] = gdfs_of_cell[dfs[k]];
+        }
+        check(dev_upload(&f->d_dfs_rank, rank.data(), nc));
+        check(dev_upload(&f->d_gdfs, gd.data(), nc));
+    }
+    {
+        // combine_predictions' prior (predictions.h:475-490): a cell's first row divides by the
+        // parameters that initialised it (its own for a root, the parent's last row otherwise)
+        std::vector<int32_t> prior(nr, 0);
+        if (d->segment) {
+            for (int64_t c = 0; c < nc; ++c) {
+                const int64_t r0 = d->row_offset[c];
+                for (int64_t r = r0; r < d->row_offset[c + 1]; ++r) prior[r] = d->segment[r];
+                if (d->parent[c] >= 0) prior[r0] = d->segment[d->row_offset[d->parent[c] + 1] - 1];
+            }
+        }
+        check(dev_upload(&f->d_prior_seg, prior.data(), nr));
+        std::vector<int32_t> row_cell(nr);
+        for (int64_t c = 0; c < nc; ++c)
+            for (int64_t r = d->row_offset[c]; r < d->row_offset[c + 1]; ++r) row_cell[r] = (int32_t)c;
+        check(dev_upload(&f->d_row_cell, row_cell.data(), nr));
+    }
+    check(dev_upload<double>(&f->d_state, nullptr, (size_t)nc * 20));
+    check(dev_upload<double>(&f->d_cell_ll, nullptr, nc));
+    check(dev_upload<int32_t>(&f->d_cell_nan, nullptr, nc));
+    if (rc == GGP_OK && nc > 0 && hipMemset(f->d_state, 0, (size_t)nc * 20 * sizeof(double)) != hipSuccess) rc = GGP_EDEV;
+    // ---- reduction blocks ----
+    f->n_trees = (int64_t)tree_start.size() - 1;
+    f->n_lblocks = (int64_t)blk_ntrees.size();
+    f->blk_global = blk_global;
+    f->red_threads = (int)std::max<int64_t>(64, B);
+    {
+        std::vector<int32_t> t0(f->n_lblocks);
+        int64_t t = 0;
+        for (int64_t j = 0; j < f->n_lblocks; ++j) {
+            t0[j] = (int32_t)t;
+            t += blk_ntrees[j];
+        }
+        if (t != f->n_trees && rc == GGP_OK) {
+            g_last_err = "shard blocks do not cover its trees";
+            rc = GGP_EINVAL;
+        }
+        check(dev_upload(&f->d_tree_dfs, tree_start.data(), tree_start.size()));
+        check(dev_upload(&f->d_blk_t0, t0.data(), t0.size()));
+        check(dev_upload(&f->d_blk_nt, blk_ntrees.data(), blk_ntrees.size()));
+        check(dev_upload<unsigned>(&f->d_done, nullptr, 1));
+        if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
+    }
+    if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1;
+        void *h = nullptr, *m = nullptr;
+        if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            rc = GGP_ENOMEM;
+        } else {
+            f->h_res = h;
+            f->h_sum = (double *)h;
+            f->h_nan = (int64_t *)((char *)h + f->n_lblocks * sizeof(double));
+            f->h_seq = (volatile int64_t *)((char *)h + 2 * f->n_lblocks * sizeof(double));
+            *f->h_seq = 0;
+            if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) rc = GGP_EDEV;
+            f->m_sum = (double *)m;
+            f->m_nan = (int64_t *)((char *)m + f->n_lblocks * sizeof(double));
+            f->m_seq = (int64_t *)((char *)m + 2 * f->n_lblocks * sizeof(double));
+        }
+    }
+    if (rc != GGP_OK) {
+        shard_destroy(f);
+        return rc;
+    }
+    DevForest &F = f->F;
+    F.time = f->d_time; F.logl = f->d_logl; F.fp = f->d_fp;
+    F.row_off = f->d_row_off; F.parent = f->d_parent; F.d1 = f->d_d1; F.d2 = f->d_d2; F.seg = f->d_seg;
+    F.dfs_rank = f->d_dfs_rank;
+    F.root_mean0 = d->root_mean_xg[0]; F.root_mean1 = d->root_mean_xg[1];
+    F.root_var0 = d->root_var_xg[0]; F.root_var1 = d->root_var_xg[1];
+    F.leaf_mean0 = d->leaf_mean_xg[0]; F.leaf_mean1 = d->leaf_mean_xg[1];
+    F.leaf_var0 = d->leaf_var_xg[0]; F.leaf_var1 = d->leaf_var_xg[1];
+    F.fp_auto = d->fp_auto;
+    F.two_log_2pi = 2 * std::log(2 * M_PI);
+    F.log2 = std::log(2.);
+    F.scaled = d->noise_scaled ? 1 : 0;
+    F.binomial = d->division_binomial ? 1 : 0;
+    // per-level rows for the roofline bookkeeping
+    f->ev_rows.assign(f->level_start.size() - 1, 0);
+    for (size_t L = 0; L + 1 < f->level_start.size(); ++L)
+        for (int64_t i = f->level_start[L]; i < f->level_start[L + 1]; ++i) {
+            int32_t c = level_cells[i];
+            f->ev_rows[L] += d->row_offset[c + 1] - d->row_offset[c];
+        }
+    *out = f;
+    return GGP_OK;
+}
+
+// ---- numbering helpers -------------------------------------------------------------------
+int64_t g_cell(const Shard *s, int64_t lc) { return s->cell_g.empty() ? lc : s->cell_g[lc]; }
+
+// the shard's local rows whose global rows fall in [r_lo, r_hi) (a contiguous local range:
+// the shard keeps its cells in input order)
+void local_rows(const ggp_forest *f, const Shard *s, int64_t r_lo, int64_t r_hi, int64_t &l_lo, int64_t &l_hi)
+{
+    l_lo = l_hi = 0;
+    if (r_hi <= r_lo || s->n_cells == 0) return;
+    if (s->cell_g.empty()) {
+        l_lo = r_lo;
+        l_hi = r_hi;
+        return;
+    }
+    const auto &G = f->row_off;
+    const int64_t gc_lo = (int64_t)(std::upper_bound(G.begin(), G.end(), r_lo) - G.begin()) - 1;
+    const int64_t gc_hi = (int64_t)(std::upper_bound(G.begin(), G.end(), r_hi - 1) - G.begin()) - 1;
+    const int64_t lc0 = std::lower_bound(s->cell_g.begin(), s->cell_g.end(), (int32_t)gc_lo) - s->cell_g.begin();
+    const int64_t lc1 = std::upper_bound(s->cell_g.begin(), s->cell_g.end(), (int32_t)gc_hi) - s->cell_g.begin();
+    if (lc0 >= lc1) return;
+    const int64_t gc0 = s->cell_g[lc0], gcl = s->cell_g[lc1 - 1];
+    l_lo = s->row_off[lc0] + std::max<int64_t>(0, r_lo - G[gc0]);
+    l_hi = s->row_off[lc1 - 1] + std::min(G[gcl + 1], r_hi) - G[gcl];
+}
+
+int64_t g_row(const ggp_forest *f, const Shard *s, int64_t lr)
+{
+    if (s->cell_g.empty()) return lr;
+    const int64_t lc = (int64_t)(std::upper_bound(s->row_off.begin(), s->row_off.end(), lr) - s->row_off.begin()) - 1;
+    return f->row_off[s->cell_g[lc]] + (lr - s->row_off[lc]);
+}
+
+// local rows [l_lo, l_hi) of a [rows x w] host array -> their global rows of out (row base r_base)
+void scatter_rows(const ggp_forest *f, const Shard *s, const double *src, int64_t l_lo, int64_t l_hi, int w,
+                  double *out, int64_t r_base)
+{
+    if (l_hi <= l_lo) return;
+    int64_t lc = (int64_t)(std::upper_bound(s->row_off.begin(), s->row_off.end(), l_lo) - s->row_off.begin()) - 1;
+    for (int64_t lr = l_lo; lr < l_hi;) {
+        const int64_t end = std::min(l_hi, s->row_off[lc + 1]);
+        const int64_t gr = f->row_off[g_cell(s, lc)] + (lr - s->row_off[lc]);
+        std::memcpy(out + (gr - r_base) * w, src + (lr - l_lo) * w, (size_t)(end - lr) * w * sizeof(double));
+        lr = end;
+        ++lc;
+    }
+}
+
+// -j on one shard (local start rows [r_lo, r_hi)): collect_joint_distributions (correlation_tree.h
+// :464-651).  The smoother and the per-row tables are kept for the parameters they were made with.
+int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi, int64_t cap,
+                 int64_t *out_idx, double *out_val, int64_t *n_out)
+{
+    const int64_t nc = f->n_cells, nr = f->n_rows;
+    *n_out = 0;
+    if (nc == 0 || r_hi <= r_lo) return GGP_OK;
+    HIPCHK(hipSetDevice(f->device));
+    HIPCHK(hipStreamSynchronize(f->stream));
+    const std::vector<double> key(params, params + (size_t)n_seg * 11);
+    if (!f->d_j_back) {
+        int rc = GGP_OK;
+        auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+        check(dev_upload<double>(&f->d_j_pstate, nullptr, (size_t)nc * 20));
+        check(dev_upload<double>(&f->d_j_fwd, nullptr, (size_t)nr * 20));
+        check(dev_upload<double>(&f->d_j_bwd, nullptr, (size_t)nr * 20));
+        check(dev_upload<double>(&f->d_j_back, nullptr, (size_t)nr * kJBack));
+        check(dev_upload<double>(&f->d_j_cond, nullptr, (size_t)nr * kJCond));
+        check(dev_upload<double>(&f->d_j_start, nullptr, (size_t)nr * kJStart));
+        if (rc != GGP_OK) {
+            shard_free_joints(f);
+            g_last_err = "ggp_joints: device allocation failed";
+            return rc;
+        }
+    }
+    hipError_t e = hipSuccess;
+    if (key != f->j_params) {   // smoother + per-row tables for these parameters
+        f->j_params.clear();
+        if (f->d_j_ptab) (void)hipFree(f->d_j_ptab);
+        f->d_j_ptab = nullptr;
+        const int rc = dev_upload(&f->d_j_ptab, params, (size_t)n_seg * 11);
+        if (rc != GGP_OK) return rc;
+        e = run_smoother(f, f->d_j_ptab, n_seg, f->d_j_pstate, f->d_j_fwd, f->d_j_bwd);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_joint_rows, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, f->stream, f->F,
+                               f->d_j_ptab, n_seg, f->d_row_cell, nr, f->d_j_fwd, f->d_j_bwd, f->d_j_back,
+                               f->d_j_cond, f->d_j_start);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) f->j_params = key;
+    }
+    std::vector<void *> bufs;
+    auto alloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return p;
+    };
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(f->stream);
+        for (void *p : bufs) (void)hipFree(p);
+    };
+    const int64_t ns = r_hi - r_lo;
+    const int depth = (int)f->level_start.size();   // generations below any start, plus one
+    auto *d_stack_j = (double *)alloc((size_t)ns * depth * kJStart * sizeof(double));
+    auto *d_stack_c = (int32_t *)alloc((size_t)ns * depth * sizeof(int32_t));
+    auto *d_counts = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
+    if (!d_stack_j || !d_stack_c || !d_counts) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
+    const unsigned wblocks = (unsigned)((ns + 63) / 64);
+    if (e == hipSuccess) {   // pass 1: count
+        hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, f->d_j_ptab, n_seg,
+                           f->d_row_cell, f->d_j_pstate, f->d_j_back, f->d_j_cond, f->d_j_start, tol, r_lo, ns, depth,
+                           d_stack_j, d_stack_c, d_counts, (const int64_t *)nullptr, (int64_t *)nullptr,
+                           (double *)nullptr);
+        e = hipGetLastError();
+    }
+    std::vector<int64_t> counts(ns), off(ns);
+    if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    int64_t total = 0;
+    for (int64_t k = 0; k < ns; ++k) {
+        off[k] = total;
+        total += counts[k];
+    }
+    *n_out = total;
+    if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
+        auto *d_off = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
+        auto *d_idx = (int64_t *)alloc((size_t)total * 2 * sizeof(int64_t));
+        auto *d_val = (double *)alloc((size_t)total * kJStart * sizeof(double));
+        if (!d_off || !d_idx || !d_val) {
+            cleanup();
+            g_last_err = "ggp_joints: device allocation failed";
+            return GGP_ENOMEM;
+        }
+        e = hipMemcpyAsync(d_off, off.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, f->d_j_ptab, n_seg,
+                               f->d_row_cell, f->d_j_pstate, f->d_j_back, f->d_j_cond, f->d_j_start, tol, r_lo, ns,
+                               depth, d_stack_j, d_stack_c, d_counts, (const int64_t *)d_off, d_idx, d_val);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    }
+    cleanup();
+    if (e != hipSuccess) {
+        f->j_params.clear();
+        g_last_err = std::string("ggp_joints: ") + hipGetErrorString(e);
+        return GGP_EDEV;
+    }
+    return GGP_OK;
+}
+
+// sub-forest descriptor of the cells `cells` (global indices, ascending; whole trees)
+struct SubDesc {
+    ggp_forest_desc d{};
+    std::vector<int64_t> row_offset;
+    std::vector<int32_t> parent, d1, d2, segment;
+    std::vector<double> time, logl, fp;
+};
+
+void make_subdesc(const ggp_forest_desc *g, const std::vector<int32_t> &cells, SubDesc &s)
+{
+    const int64_t n = (int64_t)cells.size();
+    std::unordered_map<int32_t, int32_t> remap;
+    remap.reserve((size_t)n * 2);
+    for (int64_t k = 0; k < n; ++k) remap[cells[k]] = (int32_t)k;
+    auto rm = [&](int32_t v) { return v < 0 ? -1 : remap.at(v); };
+    s.row_offset.assign(n + 1, 0);
+    for (int64_t k = 0; k < n; ++k)
+        s.row_offset[k + 1] = s.row_offset[k] + (g->row_offset[cells[k] + 1] - g->row_offset[cells[k]]);
+    const int64_t nr = s.row_offset[n];
+    s.parent.resize(n);
+    s.d1.resize(n);
+    s.d2.resize(n);
+    for (int64_t k = 0; k < n; ++k) {
+        s.parent[k] = rm(g->parent[cells[k]]);
+        s.d1[k] = rm(g->daughter1[cells[k]]);
+        s.d2[k] = rm(g->daughter2[cells[k]]);
+    }
+    s.time.resize(nr);
+    s.logl.resize(nr);
+    s.fp.resize(nr);
+    if (g->segment) s.segment.resize(nr);
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t a = g->row_offset[cells[k]], b = g->row_offset[cells[k] + 1], o = s.row_offset[k];
+        std::memcpy(&s.time[o], g->time + a, (size_t)(b - a) * sizeof(double));
+        std::memcpy(&s.logl[o], g->log_length + a, (size_t)(b - a) * sizeof(double));
+        std::memcpy(&s.fp[o], g->fp + a, (size_t)(b - a) * sizeof(double));
+        if (g->segment) std::memcpy(&s.segment[o], g->segment + a, (size_t)(b - a) * sizeof(int32_t));
+    }
+    s.d = *g;
+    s.d.n_cells = n;
+    s.d.n_rows = nr;
+    s.d.row_offset = s.row_offset.data();
+    s.d.parent = s.parent.data();
+    s.d.daughter1 = s.d1.data();
+    s.d.daughter2 = s.d2.data();
+    s.d.segment = g->segment ? s.segment.data() : nullptr;
+    s.d.time = s.time.data();
+    s.d.log_length = s.logl.data();
+    s.d.fp = s.fp.data();
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1272,21 +1907,15 @@ int ggp_device_count(int32_t *n)
 void ggp_forest_destroy(ggp_forest *f)
 {
     if (!f) return;
-    (void)hipSetDevice(f->device);
-    if (f->stream) (void)hipStreamSynchronize(f->stream);
-    for (void *p : {(void *)f->d_time, (void *)f->d_logl, (void *)f->d_fp, (void *)f->d_row_off,
-                    (void *)f->d_parent, (void *)f->d_d1, (void *)f->d_d2, (void *)f->d_seg,
-                    (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell, (void *)f->d_state,
-                    (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_sm_ptab, (void *)f->d_sm_pstate,
-                    (void *)f->d_sm_fwd, (void *)f->d_sm_bwd, (void *)f->d_sm_comb, (void *)f->d_b_ptab,
-                    (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_out_ll, (void *)f->d_b_nan,
-                    (void *)f->d_b_out_nan})
-        if (p) (void)hipFree(p);
-    for (auto &e : f->ev_pred)
-        if (e) (void)hipEventDestroy(e);
-    if (f->h_out_ll) (void)hipHostFree(f->h_out_ll);   // one allocation: ll, then the NaN code
-    for (auto &e : f->ev) (void)hipEventDestroy(e);
-    if (f->stream) (void)hipStreamDestroy(f->stream);
+    for (Shard *s : f->shards) shard_destroy(s);
+    for (DeviceCtx *d : f->devs) {
+        (void)hipSetDevice(d->id);
+        if (d->stream) (void)hipStreamSynchronize(d->stream);
+        if (d->sm_fwd) (void)hipFree(d->sm_fwd);
+        if (d->sm_bwd) (void)hipFree(d->sm_bwd);
+        if (d->stream) (void)hipStreamDestroy(d->stream);
+        delete d;
+    }
     delete f;
 }
 
@@ -1294,263 +1923,126 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
 {
     if (!d || !out) { g_last_err = "null argument"; return GGP_EINVAL; }
     *out = nullptr;
-    const int64_t nc = d->n_cells, nr = d->n_rows;
-    if (nc < 0 || nr < 0 || (nc > 0 && (!d->row_offset || !d->parent || !d->daughter1 || !d->daughter2)) ||
-        (nr > 0 && (!d->time || !d->log_length || !d->fp))) {
-        g_last_err = "incomplete forest descriptor";
-        return GGP_EINVAL;
-    }
-    if (nc >= (int64_t)1 << 31 || nr >= (int64_t)1 << 40) { g_last_err = "forest too large"; return GGP_EINVAL; }
-    // ---- validate topology on the host (bad indices would fault on the device) ----
-    if (nc > 0 && (d->row_offset[0] != 0 || d->row_offset[nc] != nr)) {
-        g_last_err = "row_offset must start at 0 and end at n_rows";
-        return GGP_EINVAL;
-    }
-    for (int64_t c = 0; c < nc; ++c) {
-        if (d->row_offset[c + 1] <= d->row_offset[c]) { g_last_err = "every cell needs >= 1 row"; return GGP_EINVAL; }
-        for (int32_t v : {d->parent[c], d->daughter1[c], d->daughter2[c]})
-            if (v < -1 || v >= nc || v == c) { g_last_err = "genealogy index out of range"; return GGP_EINVAL; }
-    }
-    // ---- generation depth (iterative, parents may follow children in input order) ----
-    std::vector<int32_t> depth(nc, -1);
-    std::vector<int32_t> dfs;
-    dfs.reserve(nc);
-    {
-        std::vector<int32_t> stack;
-        for (int64_t r = 0; r < nc; ++r) {
-            if (d->parent[r] != -1) continue;
-            depth[r] = 0;
-            stack.push_back((int32_t)r);
-            while (!stack.empty()) {
-                int32_t c = stack.back();
-                stack.pop_back();
-                dfs.push_back(c);
-                for (int32_t ch : {d->daughter2[c], d->daughter1[c]}) {
-                    if (ch < 0) continue;
-                    if (depth[ch] != -1) { g_last_err = "genealogy is not a forest"; return GGP_EINVAL; }
-                    depth[ch] = depth[c] + 1;
-                    stack.push_back(ch);
-                }
-            }
-        }
-        for (int64_t c = 0; c < nc; ++c)
-            if (depth[c] < 0) { g_last_err = "cell not reachable from a root (cycle)"; return GGP_EINVAL; }
-        // a daughter's parent pointer must be the cell that lists it (single-parent forest)
-        for (int64_t c = 0; c < nc; ++c)
-            for (int32_t ch : {d->daughter1[c], d->daughter2[c]})
-                if (ch >= 0 && d->parent[ch] != c) {
-                    g_last_err = "daughter/parent pointers disagree";
-                    return GGP_EINVAL;
-                }
-    }
     if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_WAVE) {
         g_last_err = "ggp_forest_create: unknown kernel policy";
         return GGP_EINVAL;
     }
-    auto *f = new ggp_forest();
-    f->device = d->device;
-    f->n_cells = nc;
-    f->n_rows = nr;
-    f->kernel_pref = d->kernel;
-    if (hipSetDevice(d->device) != hipSuccess) {
-        g_last_err = "hipSetDevice failed";
-        delete f;
+    std::vector<int32_t> depth, dfs;
+    std::vector<int64_t> tree_start;
+    int rc = check_topology(d, depth, dfs, tree_start);
+    if (rc != GGP_OK) return rc;
+    // ---- devices ----
+    int n_vis = 0;
+    if (hipGetDeviceCount(&n_vis) != hipSuccess || n_vis <= 0) {
+        g_last_err = "no HIP device";
         return GGP_EDEV;
     }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, d->device) == hipSuccess) f->n_cu = prop.multiProcessorCount;
-    f->wave_max_cells = (int64_t)f->n_cu * 4 * 5;   // r08 scan: wave ahead of group up to ~5 cells/SIMD
-    f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
-    if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
-    if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
-    if (const char *e = getenv("GGP_GROUP_CPW")) {
-        const int v = atoi(e);
-        f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+    if (d->n_devices < 0) { g_last_err = "n_devices < 0"; return GGP_EINVAL; }
+    std::vector<int32_t> devlist;
+    const int nd = d->n_devices > 0 ? d->n_devices : n_vis;
+    for (int k = 0; k < nd; ++k) {
+        const int32_t id = (d->n_devices > 0 && d->devices) ? d->devices[k] : k;
+        if (id < 0 || id >= n_vis) { g_last_err = "device ordinal out of range"; return GGP_EINVAL; }
+        devlist.push_back(id);
     }
-    if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
-    int rc = GGP_OK;
-    auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
-    check(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess ? GGP_OK : GGP_EDEV);
-    // ---- level schedule ----
-    int32_t max_depth = 0;
-    for (int64_t c = 0; c < nc; ++c) max_depth = std::max(max_depth, depth[c]);
-    std::vector<int32_t> level_cells(nc);
-    std::iota(level_cells.begin(), level_cells.end(), 0);
-    std::stable_sort(level_cells.begin(), level_cells.end(), [&](int32_t a, int32_t b) {
-        if (depth[a] != depth[b]) return depth[a] < depth[b];
-        return (d->row_offset[a + 1] - d->row_offset[a]) > (d->row_offset[b + 1] - d->row_offset[b]);
-    });
-    f->level_start.assign(nc > 0 ? max_depth + 2 : 1, 0);
-    for (int64_t c = 0; c < nc; ++c) f->level_start[depth[c] + 1]++;
-    for (size_t L = 1; L < f->level_start.size(); ++L) f->level_start[L] += f->level_start[L - 1];
-    f->h_dfs_order = dfs;
-    // ---- uploads ----
-    check(dev_upload(&f->d_time, d->time, nr));
-    check(dev_upload(&f->d_logl, d->log_length, nr));
-    check(dev_upload(&f->d_fp, d->fp, nr));
-    check(dev_upload(&f->d_row_off, d->row_offset, nc + 1));
-    check(dev_upload(&f->d_parent, d->parent, nc));
-    check(dev_upload(&f->d_d1, d->daughter1, nc));
-    check(dev_upload(&f->d_d2, d->daughter2, nc));
-    if (d->segment) check(dev_upload(&f->d_seg, d->segment, nr));
-    check(dev_upload(&f->d_level_cells, level_cells.data(), nc));
+    auto *f = new ggp_forest();
+    const int64_t nc = d->n_cells, nr = d->n_rows;
+    f->n_cells = nc;
+    f->n_rows = nr;
+    f->n_trees = (int64_t)tree_start.size() - 1;
+    f->dfs_order = dfs;
+    f->row_off.assign(d->row_offset ? d->row_offset : nullptr, d->row_offset ? d->row_offset + nc + 1 : nullptr);
+    if (nc == 0) f->row_off.assign(1, 0);
+    f->blk_trees = block_trees_for(f->n_trees);
+    f->n_blocks = (f->n_trees + f->blk_trees - 1) / f->blk_trees;
+    // ---- shards: whole reduction blocks, LPT over the blocks' row counts ----
+    int64_t n_shards = (int64_t)devlist.size();
+    if (d->max_shard_rows > 0) n_shards = std::max<int64_t>(n_shards, (nr + d->max_shard_rows - 1) / d->max_shard_rows);
+    n_shards = std::max<int64_t>(1, std::min<int64_t>(n_shards, std::max<int64_t>(1, f->n_blocks)));
+    std::vector<int32_t> tree_of_cell(nc, 0);
+    std::vector<int64_t> blk_rows(f->n_blocks, 0);
+    for (int64_t t = 0; t < f->n_trees; ++t)
+        for (int64_t k = tree_start[t]; k < tree_start[t + 1]; ++k) {
+            const int32_t c = dfs[k];
+            tree_of_cell[c] = (int32_t)t;
+            blk_rows[t / f->blk_trees] += d->row_offset[c + 1] - d->row_offset[c];
+        }
+    std::vector<int32_t> blk_shard(f->n_blocks, 0);
     {
-        std::vector<int32_t> rank(nc);
-        for (int64_t k = 0; k < nc; ++k) rank[dfs[k]] = (int32_t)k;
-        check(dev_upload(&f->d_dfs_rank, rank.data(), nc));
+        std::vector<int64_t> order(f->n_blocks);
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return blk_rows[a] > blk_rows[b]; });
+        std::vector<int64_t> load(n_shards, 0);
+        for (int64_t b : order) {
+            const int64_t s = std::min_element(load.begin(), load.end()) - load.begin();
+            blk_shard[b] = (int32_t)s;
+            load[s] += blk_rows[b];
+        }
     }
-    {
-        // combine_predictions' prior (predictions.h:475-490): a cell's first row divides by the
-        // parameters that initialised it (its own for a root, the parent's last row otherwise)
-        std::vector<int32_t> prior(nr, 0);
-        if (d->segment) {
-            for (int64_t c = 0; c < nc; ++c) {
-                const int64_t r0 = d->row_offset[c];
-                for (int64_t r = r0; r < d->row_offset[c + 1]; ++r) prior[r] = d->segment[r];
-                if (d->parent[c] >= 0) prior[r0] = d->segment[d->row_offset[d->parent[c] + 1] - 1];
+    // ---- device contexts (one per distinct ordinal) ----
+    std::vector<DeviceCtx *> shard_dev(n_shards, nullptr);
+    for (int64_t s = 0; s < n_shards && rc == GGP_OK; ++s) {
+        const int id = devlist[s % devlist.size()];
+        DeviceCtx *ctx = nullptr;
+        for (DeviceCtx *c : f->devs)
+            if (c->id == id) ctx = c;
+        if (!ctx) {
+            ctx = new DeviceCtx();
+            ctx->id = id;
+            f->devs.push_back(ctx);
+            if (hipSetDevice(id) != hipSuccess ||
+                hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+                g_last_err = "hipSetDevice / hipStreamCreate failed";
+                rc = GGP_EDEV;
+                break;
             }
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, id) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
         }
-        check(dev_upload(&f->d_prior_seg, prior.data(), nr));
-        std::vector<int32_t> row_cell(nr);
-        for (int64_t c = 0; c < nc; ++c)
-            for (int64_t r = d->row_offset[c]; r < d->row_offset[c + 1]; ++r) row_cell[r] = (int32_t)c;
-        check(dev_upload(&f->d_row_cell, row_cell.data(), nr));
+        shard_dev[s] = ctx;
     }
-    check(dev_upload<double>(&f->d_state, nullptr, (size_t)nc * 20));
-    check(dev_upload<double>(&f->d_cell_ll, nullptr, nc));
-    check(dev_upload<int32_t>(&f->d_cell_nan, nullptr, nc));
-    if (rc == GGP_OK && nc > 0 && hipMemset(f->d_state, 0, (size_t)nc * 20 * sizeof(double)) != hipSuccess) rc = GGP_EDEV;
-    if (rc == GGP_OK) {   // the result slot: 16 B of pinned host memory the reduction writes over the bus
-        void *h = nullptr, *m = nullptr;
-        if (hipHostMalloc(&h, 3 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            rc = GGP_ENOMEM;
+    std::vector<int32_t> gdfs_rank(nc);
+    for (int64_t k = 0; k < nc; ++k) gdfs_rank[dfs[k]] = (int32_t)k;
+    for (int64_t s = 0; s < n_shards && rc == GGP_OK; ++s) {
+        std::vector<int32_t> ntrees;
+        std::vector<int64_t> bglob;
+        for (int64_t b = 0; b < f->n_blocks; ++b)
+            if (blk_shard[b] == s) {
+                bglob.push_back(b);
+                ntrees.push_back((int32_t)(std::min(f->n_trees, (b + 1) * f->blk_trees) - b * f->blk_trees));
+            }
+        Shard *sh = nullptr;
+        if (n_shards == 1) {
+            rc = shard_create(d, shard_dev[s], gdfs_rank, ntrees, bglob, f->blk_trees, &sh);
         } else {
-            f->h_out_ll = (double *)h;
-            f->h_out_nan = (int64_t *)((char *)h + sizeof(double));
-            f->h_out_seq = (volatile int64_t *)((char *)h + 2 * sizeof(double));
-            *f->h_out_seq = 0;
-            if (hipHostGetDevicePointer(&m, h, 0) != hipSuccess) rc = GGP_EDEV;
-            f->m_out_ll = (double *)m;
-            f->m_out_nan = (int64_t *)((char *)m + sizeof(double));
-            f->m_out_seq = (int64_t *)((char *)m + 2 * sizeof(double));
+            std::vector<int32_t> cells;
+            for (int64_t c = 0; c < nc; ++c)
+                if (blk_shard[tree_of_cell[c] / f->blk_trees] == s) cells.push_back((int32_t)c);
+            SubDesc sd;
+            make_subdesc(d, cells, sd);
+            std::vector<int32_t> gd(cells.size());
+            for (size_t k = 0; k < cells.size(); ++k) gd[k] = gdfs_rank[cells[k]];
+            rc = shard_create(&sd.d, shard_dev[s], gd, ntrees, bglob, f->blk_trees, &sh);
+            if (sh) sh->cell_g = std::move(cells);
         }
+        if (sh) f->shards.push_back(sh);
     }
     if (rc != GGP_OK) {
         ggp_forest_destroy(f);
         return rc;
     }
-    DevForest &F = f->F;
-    F.time = f->d_time; F.logl = f->d_logl; F.fp = f->d_fp;
-    F.row_off = f->d_row_off; F.parent = f->d_parent; F.d1 = f->d_d1; F.d2 = f->d_d2; F.seg = f->d_seg;
-    F.dfs_rank = f->d_dfs_rank;
-    F.root_mean0 = d->root_mean_xg[0]; F.root_mean1 = d->root_mean_xg[1];
-    F.root_var0 = d->root_var_xg[0]; F.root_var1 = d->root_var_xg[1];
-    F.leaf_mean0 = d->leaf_mean_xg[0]; F.leaf_mean1 = d->leaf_mean_xg[1];
-    F.leaf_var0 = d->leaf_var_xg[0]; F.leaf_var1 = d->leaf_var_xg[1];
-    F.fp_auto = d->fp_auto;
-    F.two_log_2pi = 2 * std::log(2 * M_PI);
-    F.log2 = std::log(2.);
-    F.scaled = d->noise_scaled ? 1 : 0;
-    F.binomial = d->division_binomial ? 1 : 0;
-    // per-level rows for the roofline bookkeeping
-    f->ev_rows.assign(f->level_start.size() - 1, 0);
-    for (size_t L = 0; L + 1 < f->level_start.size(); ++L)
-        for (int64_t i = f->level_start[L]; i < f->level_start[L + 1]; ++i) {
-            int32_t c = level_cells[i];
-            f->ev_rows[L] += d->row_offset[c + 1] - d->row_offset[c];
-        }
     *out = f;
     return GGP_OK;
 }
 
-int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
-               int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+int ggp_forest_shards(ggp_forest *f, int32_t *n, int32_t *device, int64_t *rows, int64_t *cells, int32_t cap)
 {
-    if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
-    const int64_t nc = f->n_cells, nr = f->n_rows;
-    if (r_lo < 0) r_lo = 0;
-    if (r_hi > nr) r_hi = nr;
-    *n_out = 0;
-    if (nc == 0 || r_hi <= r_lo) return GGP_OK;
-    HIPCHK(hipSetDevice(f->device));
-    HIPCHK(hipStreamSynchronize(f->stream));
-    std::vector<void *> bufs;
-    auto alloc = [&](size_t bytes) -> void * {
-        void *p = nullptr;
-        if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
-        bufs.push_back(p);
-        return p;
-    };
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(f->stream);
-        for (void *p : bufs) (void)hipFree(p);
-    };
-    const int64_t ns = r_hi - r_lo;
-    const int depth = (int)f->level_start.size();   // generations below any start, plus one
-    auto *d_ptab = (double *)alloc((size_t)n_seg * 11 * sizeof(double));
-    auto *d_pstate = (double *)alloc((size_t)nc * 20 * sizeof(double));
-    auto *d_fwd = (double *)alloc((size_t)nr * 20 * sizeof(double));
-    auto *d_bwd = (double *)alloc((size_t)nr * 20 * sizeof(double));
-    auto *d_back = (double *)alloc((size_t)nr * kJBack * sizeof(double));
-    auto *d_cond = (double *)alloc((size_t)nr * kJCond * sizeof(double));
-    auto *d_start = (double *)alloc((size_t)nr * kJStart * sizeof(double));
-    auto *d_stack_j = (double *)alloc((size_t)ns * depth * kJStart * sizeof(double));
-    auto *d_stack_c = (int32_t *)alloc((size_t)ns * depth * sizeof(int32_t));
-    auto *d_counts = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
-    for (void *p : bufs)
-        if (!p) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
-    if (bufs.size() != 10) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
-    hipError_t e = hipMemcpyAsync(d_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice, f->stream);
-    if (e == hipSuccess) e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_joint_rows, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                           f->d_row_cell, nr, d_fwd, d_bwd, d_back, d_cond, d_start);
-        e = hipGetLastError();
-    }
-    const unsigned wblocks = (unsigned)((ns + 63) / 64);
-    if (e == hipSuccess) {   // pass 1: count
-        hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_row_cell,
-                           d_pstate, d_back, d_cond, d_start, tol, r_lo, ns, depth, d_stack_j, d_stack_c, d_counts,
-                           (const int64_t *)nullptr, (int64_t *)nullptr, (double *)nullptr);
-        e = hipGetLastError();
-    }
-    std::vector<int64_t> counts(ns), off(ns);
-    if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
-    int64_t total = 0;
-    for (int64_t k = 0; k < ns; ++k) {
-        off[k] = total;
-        total += counts[k];
-    }
-    *n_out = total;
-    if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
-        auto *d_off = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
-        auto *d_idx = (int64_t *)alloc((size_t)total * 2 * sizeof(int64_t));
-        auto *d_val = (double *)alloc((size_t)total * kJStart * sizeof(double));
-        if (!d_off || !d_idx || !d_val) {
-            cleanup();
-            g_last_err = "ggp_joints: device allocation failed";
-            return GGP_ENOMEM;
-        }
-        e = hipMemcpyAsync(d_off, off.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_row_cell,
-                               d_pstate, d_back, d_cond, d_start, tol, r_lo, ns, depth, d_stack_j, d_stack_c, d_counts,
-                               (const int64_t *)d_off, d_idx, d_val);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
-    }
-    cleanup();
-    if (e != hipSuccess) {
-        g_last_err = std::string("ggp_joints: ") + hipGetErrorString(e);
-        return GGP_EDEV;
+    if (!f || !n) return GGP_EINVAL;
+    *n = (int32_t)f->shards.size();
+    for (int32_t k = 0; k < *n && k < cap; ++k) {
+        if (device) device[k] = f->shards[k]->device;
+        if (rows) rows[k] = f->shards[k]->n_rows;
+        if (cells) cells[k] = f->shards[k]->n_cells;
     }
     return GGP_OK;
 }
@@ -1558,74 +2050,90 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
 int ggp_reset_state(ggp_forest *f)
 {
     if (!f) return GGP_EINVAL;
-    HIPCHK(hipSetDevice(f->device));
-    if (f->n_cells) HIPCHK(hipMemsetAsync(f->d_state, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream));
-    HIPCHK(hipStreamSynchronize(f->stream));
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipMemsetAsync(s->d_state, 0, (size_t)s->n_cells * 20 * sizeof(double), s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
     return GGP_OK;
 }
 
 int ggp_get_state(ggp_forest *f, double *out)
 {
     if (!f || !out) return GGP_EINVAL;
-    HIPCHK(hipSetDevice(f->device));
-    HIPCHK(hipStreamSynchronize(f->stream));
-    if (f->n_cells) HIPCHK(hipMemcpy(out, f->d_state, (size_t)f->n_cells * 20 * sizeof(double), hipMemcpyDeviceToHost));
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (s->cell_g.empty()) {
+            HIPCHK(hipMemcpy(out, s->d_state, (size_t)s->n_cells * 20 * sizeof(double), hipMemcpyDeviceToHost));
+            continue;
+        }
+        std::vector<double> tmp((size_t)s->n_cells * 20);
+        HIPCHK(hipMemcpy(tmp.data(), s->d_state, tmp.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int64_t c = 0; c < s->n_cells; ++c)
+            std::memcpy(out + (size_t)20 * s->cell_g[c], &tmp[(size_t)20 * c], 20 * sizeof(double));
+    }
     return GGP_OK;
 }
 
 int ggp_set_state(ggp_forest *f, const double *in)
 {
     if (!f || !in) return GGP_EINVAL;
-    HIPCHK(hipSetDevice(f->device));
-    HIPCHK(hipStreamSynchronize(f->stream));
-    if (f->n_cells) HIPCHK(hipMemcpy(f->d_state, in, (size_t)f->n_cells * 20 * sizeof(double), hipMemcpyHostToDevice));
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (s->cell_g.empty()) {
+            HIPCHK(hipMemcpy(s->d_state, in, (size_t)s->n_cells * 20 * sizeof(double), hipMemcpyHostToDevice));
+            continue;
+        }
+        std::vector<double> tmp((size_t)s->n_cells * 20);
+        for (int64_t c = 0; c < s->n_cells; ++c)
+            std::memcpy(&tmp[(size_t)20 * c], in + (size_t)20 * s->cell_g[c], 20 * sizeof(double));
+        HIPCHK(hipMemcpy(s->d_state, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     return GGP_OK;
 }
 
 int ggp_total_loglik_async(ggp_forest *f, const double *params)
 {
     if (!f || !params) return GGP_EINVAL;
-    HIPCHK(hipSetDevice(f->device));
     ggp_params P;
     std::memcpy(P.p, params, sizeof P.p);
-    if (f->n_cells == 0) {
-        *f->h_out_ll = 0.0;
-        *f->h_out_nan = 0x7fffffffffffffffLL;
-        f->seq_pending = false;
-        return GGP_OK;
+    for (Shard *s : f->shards) {   // every device enqueued before any is waited for
+        const int rc = shard_launch(s, P);
+        if (rc != GGP_OK) return rc;
     }
-    return launch_levels(f, P);
+    return GGP_OK;
 }
 
 int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
     if (!f) return GGP_EINVAL;
-    bool seen = false;
-    if (f->spin && f->seq_pending) {
-        for (uint32_t it = 1;; ++it) {
-            if (*f->h_out_seq == f->seq) { seen = true; break; }
-            if ((it & 1023) == 0 && hipStreamQuery(f->stream) != hipErrorNotReady) break;
+    std::vector<double> blocks((size_t)f->n_blocks, 0.0);
+    long long code = kNoNan;
+    for (Shard *s : f->shards) {
+        const int rc = shard_wait(s);
+        if (rc != GGP_OK) return rc;
+        for (int64_t j = 0; j < s->n_lblocks; ++j) {
+            blocks[(size_t)s->blk_global[j]] = s->h_sum[j];
+            code = std::min<long long>(code, s->h_nan[j]);
         }
-        std::atomic_thread_fence(std::memory_order_acquire);
     }
-    f->seq_pending = false;
-    if (!seen || f->profile) HIPCHK(hipStreamSynchronize(f->stream));
-    const double v = *f->h_out_ll;
-    const int64_t code = *f->h_out_nan;
+    const double v = top_sum(std::move(blocks));
     if (ll) *ll = v;
     if (nan_cell) *nan_cell = -1;
     if (nan_row) *nan_row = -1;
-    if (code != 0x7fffffffffffffffLL) {
+    if (code != kNoNan) {
         const int64_t rank = code >> 24, row = code & 0xffffff;
-        if (nan_cell) *nan_cell = f->h_dfs_order[rank];
+        if (nan_cell) *nan_cell = f->dfs_order[rank];
         if (nan_row) *nan_row = row;
         if (ll) *ll = std::nan("");
         return GGP_ENAN;
     }
-    if (std::isnan(v)) {   // NaN from +inf + -inf across cells (see include/ggp.h)
-        if (ll) *ll = v;
-        return GGP_ENAN;
-    }
+    if (std::isnan(v)) return GGP_ENAN;   // NaN from +inf + -inf across cells (see include/ggp.h)
     return GGP_OK;
 }
 
@@ -1638,20 +2146,9 @@ int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *n
 
 // Batched objective: n_pts parameter points, each evaluated from the handle's carried state as
 // it is at the call (the carried state itself is left unchanged).  Points run in chunks that
-// keep the per-point state slices under kBatchBytes; every level of a chunk is one launch of
-// the lane schedule with blockIdx.y = point, then one k_reduce block per point.
+// keep the per-point state slices under kBatchBytes per shard; every level of a chunk is one
+// launch of the lane schedule with blockIdx.y = point, then the block sums of every point.
 static constexpr int64_t kBatchBytes = int64_t(4) << 30;
-
-static void batch_free(ggp_forest *f)
-{
-    for (void *p : {(void *)f->d_b_ptab, (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_out_ll,
-                    (void *)f->d_b_nan, (void *)f->d_b_out_nan})
-        if (p) (void)hipFree(p);
-    f->d_b_ptab = f->d_b_state = f->d_b_ll = f->d_b_out_ll = nullptr;
-    f->d_b_nan = nullptr;
-    f->d_b_out_nan = nullptr;
-    f->b_cap = 0;
-}
 
 int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *status)
 {
@@ -1660,68 +2157,100 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
         return GGP_EINVAL;
     }
     if (n_pts == 0) return GGP_OK;
-    HIPCHK(hipSetDevice(f->device));
-    const int64_t nc = f->n_cells;
-    if (nc == 0) {
+    if (f->n_cells == 0) {
         for (int32_t i = 0; i < n_pts; ++i) { ll[i] = 0.0; status[i] = GGP_OK; }
         return GGP_OK;
     }
-    const int64_t per_pt = nc * (20 * 8 + 8 + 4);
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({(int64_t)n_pts, kBatchBytes / per_pt, 65535}));
-    if (chunk > f->b_cap) {
-        HIPCHK(hipStreamSynchronize(f->stream));
-        batch_free(f);
+    int64_t chunk = std::min<int64_t>((int64_t)n_pts, 65535);
+    for (Shard *s : f->shards)
+        if (s->n_cells) chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, kBatchBytes / (s->n_cells * (20 * 8 + 8 + 4))));
+    for (Shard *s : f->shards) {
+        if (!s->n_cells || chunk <= s->b_cap) continue;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        batch_free(s);
         int rc = GGP_OK;
         auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
-        check(dev_upload<double>(&f->d_b_ptab, nullptr, (size_t)chunk * 11));
-        check(dev_upload<double>(&f->d_b_state, nullptr, (size_t)chunk * nc * 20));
-        check(dev_upload<double>(&f->d_b_ll, nullptr, (size_t)chunk * nc));
-        check(dev_upload<int32_t>(&f->d_b_nan, nullptr, (size_t)chunk * nc));
-        check(dev_upload<double>(&f->d_b_out_ll, nullptr, (size_t)chunk));
-        check(dev_upload<int64_t>(&f->d_b_out_nan, nullptr, (size_t)chunk));
-        if (rc != GGP_OK) { batch_free(f); return rc; }
-        f->b_cap = chunk;
+        const int64_t nc = s->n_cells;
+        check(dev_upload<double>(&s->d_b_ptab, nullptr, (size_t)chunk * 11));
+        check(dev_upload<double>(&s->d_b_state, nullptr, (size_t)chunk * nc * 20));
+        check(dev_upload<double>(&s->d_b_ll, nullptr, (size_t)chunk * nc));
+        check(dev_upload<int32_t>(&s->d_b_nan, nullptr, (size_t)chunk * nc));
+        check(dev_upload<double>(&s->d_b_sum, nullptr, (size_t)chunk * s->n_lblocks));
+        check(dev_upload<int64_t>(&s->d_b_code, nullptr, (size_t)chunk * s->n_lblocks));
+        if (rc != GGP_OK) { batch_free(s); return rc; }
+        s->b_cap = chunk;
     }
-    const int n_levels = (int)f->level_start.size() - 1;
-    const int cpw = lane_cpw(f);
-    std::vector<int64_t> nan_code((size_t)chunk);
+    const size_t ns = f->shards.size();
+    std::vector<std::vector<double>> sums(ns);
+    std::vector<std::vector<int64_t>> codes(ns);
     for (int64_t p0 = 0; p0 < n_pts; p0 += chunk) {
         const int64_t np = std::min<int64_t>(chunk, n_pts - p0);
-        HIPCHK(hipMemcpyAsync(f->d_b_ptab, params + 11 * p0, (size_t)np * 11 * sizeof(double), hipMemcpyHostToDevice,
-                              f->stream));
-        const int64_t total = nc * 20 * np;
-        const int rblocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
-        hipLaunchKernelGGL(k_replicate, dim3(rblocks), dim3(256), 0, f->stream, f->d_state, nc * 20, f->d_b_state, np);
-        HIPCHK(hipGetLastError());
-        for (int L = 0; L < n_levels; ++L) {
-            const int64_t a = f->level_start[L];
-            const int n = (int)(f->level_start[L + 1] - a);
-            if (n <= 0) continue;
-            hipLaunchKernelGGL(k_loglik_level_batch, dim3((n + cpw - 1) / cpw, (unsigned)np), dim3(64), 0, f->stream,
-                               f->F, f->d_b_ptab, f->d_level_cells + a, n, cpw, nc, f->d_b_state, f->d_b_ll, f->d_b_nan);
+        for (size_t k = 0; k < ns; ++k) {   // enqueue every shard
+            Shard *s = f->shards[k];
+            if (!s->n_cells) continue;
+            const int64_t nc = s->n_cells;
+            HIPCHK(hipSetDevice(s->device));
+            HIPCHK(hipMemcpyAsync(s->d_b_ptab, params + 11 * p0, (size_t)np * 11 * sizeof(double),
+                                  hipMemcpyHostToDevice, s->stream));
+            const int64_t total = nc * 20 * np;
+            const int rblocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
+            hipLaunchKernelGGL(k_replicate, dim3(rblocks), dim3(256), 0, s->stream, s->d_state, nc * 20, s->d_b_state, np);
             HIPCHK(hipGetLastError());
+            const int n_levels = (int)s->level_start.size() - 1;
+            const int cpw = lane_cpw(s);
+            for (int L = 0; L < n_levels; ++L) {
+                const int64_t a = s->level_start[L];
+                const int n = (int)(s->level_start[L + 1] - a);
+                if (n <= 0) continue;
+                hipLaunchKernelGGL(k_loglik_level_batch, dim3((n + cpw - 1) / cpw, (unsigned)np), dim3(64), 0,
+                                   s->stream, s->F, s->d_b_ptab, s->d_level_cells + a, n, cpw, nc, s->d_b_state,
+                                   s->d_b_ll, s->d_b_nan);
+                HIPCHK(hipGetLastError());
+            }
+            hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,
+                               s->stream, nc, s->d_b_ll, s->d_b_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt,
+                               s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
+                               (int64_t *)nullptr, (int64_t)0);
+            HIPCHK(hipGetLastError());
+            sums[k].resize((size_t)np * s->n_lblocks);
+            codes[k].resize((size_t)np * s->n_lblocks);
+            HIPCHK(hipMemcpyAsync(sums[k].data(), s->d_b_sum, sums[k].size() * sizeof(double), hipMemcpyDeviceToHost,
+                                  s->stream));
+            HIPCHK(hipMemcpyAsync(codes[k].data(), s->d_b_code, codes[k].size() * sizeof(int64_t),
+                                  hipMemcpyDeviceToHost, s->stream));
         }
-        hipLaunchKernelGGL(k_reduce, dim3((unsigned)np), dim3(kRedThreads), 0, f->stream, nc, f->d_b_ll, f->d_b_nan,
-                           f->d_b_out_ll, f->d_b_out_nan, (int64_t *)nullptr, (int64_t)0);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(ll + p0, f->d_b_out_ll, (size_t)np * sizeof(double), hipMemcpyDeviceToHost, f->stream));
-        HIPCHK(hipMemcpyAsync(nan_code.data(), f->d_b_out_nan, (size_t)np * sizeof(int64_t), hipMemcpyDeviceToHost,
-                              f->stream));
-        HIPCHK(hipStreamSynchronize(f->stream));
+        for (Shard *s : f->shards) {
+            if (!s->n_cells) continue;
+            HIPCHK(hipSetDevice(s->device));
+            HIPCHK(hipStreamSynchronize(s->stream));
+        }
         for (int64_t i = 0; i < np; ++i) {
-            const bool bad = nan_code[(size_t)i] != 0x7fffffffffffffffLL || std::isnan(ll[p0 + i]);
+            std::vector<double> blocks((size_t)f->n_blocks, 0.0);
+            bool bad = false;
+            for (size_t k = 0; k < ns; ++k) {
+                const Shard *s = f->shards[k];
+                for (int64_t j = 0; j < s->n_lblocks; ++j) {
+                    blocks[(size_t)s->blk_global[j]] = sums[k][(size_t)(i * s->n_lblocks + j)];
+                    bad = bad || codes[k][(size_t)(i * s->n_lblocks + j)] != kNoNan;
+                }
+            }
+            const double v = top_sum(std::move(blocks));
+            bad = bad || std::isnan(v);
             status[p0 + i] = bad ? GGP_ENAN : GGP_OK;
-            if (bad) ll[p0 + i] = std::nan("");
+            ll[p0 + i] = bad ? std::nan("") : v;
         }
     }
     return GGP_OK;
 }
 
-int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)
+int ggp_last_launch_profile(ggp_forest *ff, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)
 {
-    if (!f || !n) return GGP_EINVAL;
+    if (!ff || !n || ff->shards.empty()) return GGP_EINVAL;
+    Shard *f = ff->shards[0];   // the first shard's launches
     if (!f->profile) {
         // enable for subsequent calls: one event pair per level
+        HIPCHK(hipSetDevice(f->device));
         const size_t levels = f->level_start.size() - 1;
         f->ev.resize(2 * levels);
         for (auto &e : f->ev) HIPCHK(hipEventCreate(&e));
@@ -1731,6 +2260,7 @@ int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *ke
         *n = 0;
         return GGP_OK;
     }
+    HIPCHK(hipSetDevice(f->device));
     HIPCHK(hipStreamSynchronize(f->stream));
     int k = 0;
     for (int L = 0; L < f->n_prof && k < cap; ++L, ++k) {
@@ -1747,87 +2277,278 @@ int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *ke
 int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, int32_t *kernel_used)
 {
     if (!f) return GGP_EINVAL;
-    int64_t mx = 0;
-    for (size_t L = 0; L + 1 < f->level_start.size(); ++L)
-        mx = std::max(mx, f->level_start[L + 1] - f->level_start[L]);
-    if (n_levels) *n_levels = (int64_t)f->level_start.size() - 1;
+    int64_t mx = 0, nl = 0;
+    for (const Shard *s : f->shards) {
+        for (size_t L = 0; L + 1 < s->level_start.size(); ++L)
+            mx = std::max(mx, s->level_start[L + 1] - s->level_start[L]);
+        nl = std::max(nl, (int64_t)s->level_start.size() - 1);
+    }
+    if (n_levels) *n_levels = nl;
     if (max_level_cells) *max_level_cells = mx;
-    if (kernel_used) *kernel_used = f->kernel_used;
+    if (kernel_used) *kernel_used = f->shards.empty() ? GGP_KERNEL_LANE : f->shards[0]->kernel_used;
     return GGP_OK;
 }
 
 int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine)
 {
-    if (!f || !f->pred_timed) { g_last_err = "ggp_predict_profile: no completed ggp_predict"; return GGP_EINVAL; }
-    HIPCHK(hipSetDevice(f->device));
-    float a = 0, b = 0;
-    HIPCHK(hipEventElapsedTime(&a, f->ev_pred[0], f->ev_pred[1]));
-    HIPCHK(hipEventElapsedTime(&b, f->ev_pred[1], f->ev_pred[2]));
-    if (ms_smooth) *ms_smooth = a;
-    if (ms_combine) *ms_combine = b;
+    if (!f) return GGP_EINVAL;
+    // per device: its shards run one after another; report the slowest device
+    float best_a = 0, best_b = 0;
+    bool any = false;
+    for (const DeviceCtx *dv : f->devs) {
+        float a = 0, b = 0;
+        for (Shard *s : f->shards) {
+            if (s->dev != dv || !s->n_cells) continue;
+            if (!s->pred_timed) { g_last_err = "ggp_predict_profile: no completed ggp_predict"; return GGP_EINVAL; }
+            HIPCHK(hipSetDevice(s->device));
+            float x = 0, y = 0;
+            HIPCHK(hipEventElapsedTime(&x, s->ev_pred[0], s->ev_pred[1]));
+            HIPCHK(hipEventElapsedTime(&y, s->ev_pred[1], s->ev_pred[2]));
+            a += x;
+            b += y;
+            any = true;
+        }
+        if (a + b > best_a + best_b) { best_a = a; best_b = b; }
+    }
+    if (!any) { g_last_err = "ggp_predict_profile: no completed ggp_predict"; return GGP_EINVAL; }
+    if (ms_smooth) *ms_smooth = best_a;
+    if (ms_combine) *ms_combine = best_b;
     return GGP_OK;
 }
 
+// -p: per device, its shards one after another through the device's forward/backward workspace;
+// each shard's combined rows stay in HBM (ggp_predict_rows streams them)
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd, double *out_bwd,
                 double *out_comb)
 {
     if (!f || !params || n_seg < 1) { g_last_err = "ggp_predict: null params or n_seg < 1"; return GGP_EINVAL; }
-    HIPCHK(hipSetDevice(f->device));
-    HIPCHK(hipStreamSynchronize(f->stream));
-    const int64_t nc = f->n_cells, nr = f->n_rows;
-    if (nc == 0) return GGP_OK;
-    // fresh cells (main.cpp:434-438): the smoother never touches the likelihood's carried state.
-    // The workspace (per-cell state + three [n_rows x 20] row buffers) lives in the handle.
-    if (!f->d_sm_pstate) {
+    if (f->n_cells == 0) return GGP_OK;
+    // ---- workspaces ----
+    for (DeviceCtx *dv : f->devs) {
+        int64_t need = 0;
+        for (const Shard *s : f->shards)
+            if (s->dev == dv) need = std::max(need, s->n_rows);
+        if (need <= dv->sm_rows) continue;
+        HIPCHK(hipSetDevice(dv->id));
+        HIPCHK(hipStreamSynchronize(dv->stream));
+        for (double **p : {&dv->sm_fwd, &dv->sm_bwd}) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+        }
+        dv->sm_rows = 0;
         int rc = GGP_OK;
         auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
-        check(dev_upload<double>(&f->d_sm_pstate, nullptr, (size_t)nc * 20));
-        check(dev_upload<double>(&f->d_sm_fwd, nullptr, (size_t)nr * 20));
-        check(dev_upload<double>(&f->d_sm_bwd, nullptr, (size_t)nr * 20));
-        check(dev_upload<double>(&f->d_sm_comb, nullptr, (size_t)nr * 20));
-        for (auto &ev : f->ev_pred)
-            if (rc == GGP_OK && hipEventCreate(&ev) != hipSuccess) rc = GGP_EDEV;
+        check(dev_upload<double>(&dv->sm_fwd, nullptr, (size_t)need * 20));
+        check(dev_upload<double>(&dv->sm_bwd, nullptr, (size_t)need * 20));
         if (rc != GGP_OK) {
-            for (double **p : {&f->d_sm_pstate, &f->d_sm_fwd, &f->d_sm_bwd, &f->d_sm_comb}) {
+            for (double **p : {&dv->sm_fwd, &dv->sm_bwd}) {
                 if (*p) (void)hipFree(*p);
                 *p = nullptr;
             }
             return rc;
         }
+        dv->sm_rows = need;
     }
-    if (n_seg > f->sm_ptab_cap) {
-        if (f->d_sm_ptab) (void)hipFree(f->d_sm_ptab);
-        f->d_sm_ptab = nullptr;
-        f->sm_ptab_cap = 0;
-        const int rc = dev_upload<double>(&f->d_sm_ptab, nullptr, (size_t)n_seg * 11);
-        if (rc != GGP_OK) return rc;
-        f->sm_ptab_cap = n_seg;
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        HIPCHK(hipSetDevice(s->device));
+        if (!s->d_sm_pstate) {
+            int rc = GGP_OK;
+            auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+            check(dev_upload<double>(&s->d_sm_pstate, nullptr, (size_t)s->n_cells * 20));
+            check(dev_upload<double>(&s->d_sm_comb, nullptr, (size_t)s->n_rows * 20));
+            for (auto &ev : s->ev_pred)
+                if (rc == GGP_OK && hipEventCreate(&ev) != hipSuccess) rc = GGP_EDEV;
+            if (rc != GGP_OK) return rc;
+        }
+        if (n_seg > s->sm_ptab_cap) {
+            HIPCHK(hipStreamSynchronize(s->stream));
+            if (s->d_sm_ptab) (void)hipFree(s->d_sm_ptab);
+            s->d_sm_ptab = nullptr;
+            s->sm_ptab_cap = 0;
+            const int rc = dev_upload<double>(&s->d_sm_ptab, nullptr, (size_t)n_seg * 11);
+            if (rc != GGP_OK) return rc;
+            s->sm_ptab_cap = n_seg;
+        }
+        s->pred_timed = false;
     }
-    double *d_ptab = f->d_sm_ptab, *d_pstate = f->d_sm_pstate, *d_fwd = f->d_sm_fwd, *d_bwd = f->d_sm_bwd,
-           *d_comb = f->d_sm_comb;
-    f->pred_timed = false;
-    hipError_t e = hipMemcpyAsync(d_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice, f->stream);
-    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[0], f->stream);
-    if (e == hipSuccess) e = run_smoother(f, d_ptab, n_seg, d_pstate, d_fwd, d_bwd);
-    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[1], f->stream);
-    if (e == hipSuccess) {
-        const int64_t blocks = (nr + 255) / 256;
-        hipLaunchKernelGGL(k_combine, dim3((unsigned)blocks), dim3(256), 0, f->stream, d_ptab, n_seg,
-                           f->d_prior_seg, nr, d_fwd, d_bwd, d_comb);
-        e = hipGetLastError();
+    // ---- smoother + combine, shard by shard on each device (devices run concurrently) ----
+    const bool direct = f->shards.size() == 1 && f->shards[0]->cell_g.empty();
+    std::vector<double> stage;
+    hipError_t e = hipSuccess;
+    for (Shard *s : f->shards) {
+        if (!s->n_cells || e != hipSuccess) continue;
+        DeviceCtx *dv = s->dev;
+        e = hipSetDevice(s->device);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(s->d_sm_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice,
+                               s->stream);
+        if (e == hipSuccess) e = hipEventRecord(s->ev_pred[0], s->stream);
+        if (e == hipSuccess) e = run_smoother(s, s->d_sm_ptab, n_seg, s->d_sm_pstate, dv->sm_fwd, dv->sm_bwd);
+        if (e == hipSuccess) e = hipEventRecord(s->ev_pred[1], s->stream);
+        if (e == hipSuccess) {
+            const int64_t blocks = (s->n_rows + 255) / 256;
+            hipLaunchKernelGGL(k_combine, dim3((unsigned)blocks), dim3(256), 0, s->stream, s->d_sm_ptab, n_seg,
+                               s->d_prior_seg, s->n_rows, dv->sm_fwd, dv->sm_bwd, s->d_sm_comb);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(s->ev_pred[2], s->stream);
+        // forward / backward rows leave the shared workspace before the device's next shard
+        const size_t bytes = (size_t)s->n_rows * 20 * sizeof(double);
+        for (int which = 0; which < 2 && e == hipSuccess; ++which) {
+            double *dst = which == 0 ? out_fwd : out_bwd;
+            const double *src = which == 0 ? dv->sm_fwd : dv->sm_bwd;
+            if (!dst) continue;
+            if (direct) {
+                e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream);
+            } else {
+                stage.resize((size_t)s->n_rows * 20);
+                e = hipMemcpyAsync(stage.data(), src, bytes, hipMemcpyDeviceToHost, s->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+                if (e == hipSuccess) scatter_rows(f, s, stage.data(), 0, s->n_rows, 20, dst, 0);
+            }
+        }
     }
-    if (e == hipSuccess) e = hipEventRecord(f->ev_pred[2], f->stream);
-    const size_t bytes = (size_t)nr * 20 * sizeof(double);
-    if (e == hipSuccess && out_fwd) e = hipMemcpyAsync(out_fwd, d_fwd, bytes, hipMemcpyDeviceToHost, f->stream);
-    if (e == hipSuccess && out_bwd) e = hipMemcpyAsync(out_bwd, d_bwd, bytes, hipMemcpyDeviceToHost, f->stream);
-    if (e == hipSuccess && out_comb) e = hipMemcpyAsync(out_comb, d_comb, bytes, hipMemcpyDeviceToHost, f->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
-    f->pred_timed = e == hipSuccess;
+    for (Shard *s : f->shards) {
+        if (!s->n_cells || e != hipSuccess) continue;
+        e = hipSetDevice(s->device);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        if (e == hipSuccess) s->pred_timed = true;
+    }
     if (e != hipSuccess) {
         g_last_err = std::string("ggp_predict: ") + hipGetErrorString(e);
         return GGP_EDEV;
     }
+    if (out_comb) return ggp_predict_rows(f, 0, f->n_rows, out_comb);
     return GGP_OK;
+}
+
+// combined rows [r_lo, r_hi) of the last ggp_predict (input order) -> out[(r - r_lo) * 20]
+int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out)
+{
+    if (!f || !out || r_lo < 0 || r_hi > f->n_rows || r_hi < r_lo) {
+        g_last_err = "ggp_predict_rows: bad arguments";
+        return GGP_EINVAL;
+    }
+    std::vector<double> stage;
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        if (!s->pred_timed || !s->d_sm_comb) { g_last_err = "ggp_predict_rows: no completed ggp_predict"; return GGP_EINVAL; }
+        int64_t l_lo, l_hi;
+        local_rows(f, s, r_lo, r_hi, l_lo, l_hi);
+        if (l_hi <= l_lo) continue;
+        HIPCHK(hipSetDevice(s->device));
+        const size_t bytes = (size_t)(l_hi - l_lo) * 20 * sizeof(double);
+        if (s->cell_g.empty()) {
+            HIPCHK(hipMemcpy(out + (l_lo - r_lo) * 20, s->d_sm_comb + l_lo * 20, bytes, hipMemcpyDeviceToHost));
+            continue;
+        }
+        stage.resize((size_t)(l_hi - l_lo) * 20);
+        HIPCHK(hipMemcpy(stage.data(), s->d_sm_comb + l_lo * 20, bytes, hipMemcpyDeviceToHost));
+        scatter_rows(f, s, stage.data(), l_lo, l_hi, 20, out, r_lo);
+    }
+    return GGP_OK;
+}
+
+int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
+               int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+{
+    if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
+    if (r_lo < 0) r_lo = 0;
+    if (r_hi > f->n_rows) r_hi = f->n_rows;
+    *n_out = 0;
+    if (f->n_cells == 0 || r_hi <= r_lo) return GGP_OK;
+    if (f->shards.size() == 1 && f->shards[0]->cell_g.empty())
+        return shard_joints(f->shards[0], params, n_seg, tol, r_lo, r_hi, cap, out_idx, out_val, n_out);
+    // several shards: every start row belongs to one; count first, then each shard's joints in
+    // global numbering, merged by start row (each start's joints keep their add order)
+    const size_t ns = f->shards.size();
+    std::vector<int64_t> lo(ns), hi(ns), cnt(ns, 0);
+    int64_t total = 0;
+    for (size_t k = 0; k < ns; ++k) {
+        local_rows(f, f->shards[k], r_lo, r_hi, lo[k], hi[k]);
+        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], 0, nullptr, nullptr, &cnt[k]);
+        if (rc != GGP_OK) return rc;
+        total += cnt[k];
+    }
+    *n_out = total;
+    if (total == 0 || total > cap || !out_idx || !out_val) return GGP_OK;
+    std::vector<int64_t> idx;
+    std::vector<double> val;
+    std::vector<std::pair<int64_t, int64_t>> order;   // (global start, position in idx/val)
+    order.reserve((size_t)total);
+    idx.reserve((size_t)total * 2);
+    val.reserve((size_t)total * kJStart);
+    for (size_t k = 0; k < ns; ++k) {
+        if (!cnt[k]) continue;
+        std::vector<int64_t> li((size_t)cnt[k] * 2);
+        std::vector<double> lv((size_t)cnt[k] * kJStart);
+        int64_t got = 0;
+        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], cnt[k], li.data(), lv.data(), &got);
+        if (rc != GGP_OK) return rc;
+        for (int64_t q = 0; q < got; ++q) {
+            const int64_t gs = g_row(f, f->shards[k], li[2 * q]), gt = g_row(f, f->shards[k], li[2 * q + 1]);
+            order.emplace_back(gs, (int64_t)idx.size() / 2);
+            idx.push_back(gs);
+            idx.push_back(gt);
+        }
+        val.insert(val.end(), lv.begin(), lv.begin() + got * kJStart);
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [](const std::pair<int64_t, int64_t> &a, const std::pair<int64_t, int64_t> &b) { return a.first < b.first; });
+    for (size_t q = 0; q < order.size(); ++q) {
+        const int64_t p = order[q].second;
+        out_idx[2 * q] = idx[2 * p];
+        out_idx[2 * q + 1] = idx[2 * p + 1];
+        std::memcpy(out_val + q * kJStart, &val[(size_t)p * kJStart], kJStart * sizeof(double));
+    }
+    return GGP_OK;
+}
+
+// ---- test-only device math (tests/test_gpu_device_math.py) --------------------------------
+int ggp_debug_dawson(int32_t device, int32_t variant, const double *x, int64_t n, double *out)
+{
+    if (!x || !out || n < 0 || variant < 0 || variant > 1) { g_last_err = "ggp_debug_dawson: bad arguments"; return GGP_EINVAL; }
+    if (n == 0) return GGP_OK;
+    HIPCHK(hipSetDevice(device));
+    double *dx = nullptr, *dy = nullptr;
+    int rc = dev_upload(&dx, x, (size_t)n);
+    if (rc == GGP_OK) rc = dev_upload<double>(&dy, nullptr, (size_t)n);
+    if (rc == GGP_OK) {
+        hipLaunchKernelGGL(k_debug_dawson, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, dx, n, variant, dy);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(out, dy, (size_t)n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+            g_last_err = "ggp_debug_dawson: launch failed";
+            rc = GGP_EDEV;
+        }
+    }
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    return rc;
+}
+
+int ggp_debug_tauint(int32_t device, const double *in, int64_t n, double *out)
+{
+    if (!in || !out || n < 0) { g_last_err = "ggp_debug_tauint: bad arguments"; return GGP_EINVAL; }
+    for (int64_t i = 0; i < n; ++i)
+        if (in[6 * i] < 0 || in[6 * i] > 3 || in[6 * i] != (double)(int)in[6 * i]) {
+            g_last_err = "ggp_debug_tauint: k must be 0..3";
+            return GGP_EINVAL;
+        }
+    if (n == 0) return GGP_OK;
+    HIPCHK(hipSetDevice(device));
+    double *di = nullptr, *dy = nullptr;
+    int rc = dev_upload(&di, in, (size_t)n * 6);
+    if (rc == GGP_OK) rc = dev_upload<double>(&dy, nullptr, (size_t)n);
+    if (rc == GGP_OK) {
+        hipLaunchKernelGGL(k_debug_tauint, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, di, n, dy);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(out, dy, (size_t)n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+            g_last_err = "ggp_debug_tauint: launch failed";
+            rc = GGP_EDEV;
+        }
+    }
+    if (di) (void)hipFree(di);
+    if (dy) (void)hipFree(dy);
+    return rc;
 }
 
 }  // extern "C"

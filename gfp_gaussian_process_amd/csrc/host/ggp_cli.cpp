@@ -267,6 +267,11 @@ double total_likelihood(const std::vector<double> &params, Objective &o)
     return ll;
 }
 
+// -g / -chunk (additive): the devices the forest is sharded over (default: every
+// visible device; repeats = logical shards on one device) and the rows per shard cap
+std::vector<int32_t> g_devices;
+int64_t g_max_shard_rows = 0;
+
 struct Forest {
     ggp_host_forest *host = nullptr;
     ggp_forest_desc desc{};
@@ -283,7 +288,9 @@ void build_forest(Forest &F, const ggp_dataset *d, int segment, const std::strin
     if (ggp_forest_build(d, segment, noise == "scaled", div == "binomial", &F.host) != GGP_OK)
         throw std::invalid_argument(ggp_host_last_error());
     ggp_host_forest_desc(F.host, &F.desc);
-    F.desc.device = 0;
+    F.desc.n_devices = (int32_t)g_devices.size();   // 0: every visible device
+    F.desc.devices = g_devices.empty() ? nullptr : g_devices.data();
+    F.desc.max_shard_rows = g_max_shard_rows;
     F.desc.kernel = GGP_KERNEL_AUTO;
     const int rc = ggp_forest_create(&F.desc, &F.gpu);
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_forest_create: ") + ggp_strerror(rc));
@@ -511,9 +518,12 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         pv.insert(pv.end(), v.begin(), v.end());
     }
     const int64_t nr = F.desc.n_rows, nc = F.desc.n_cells;
-    std::vector<double> comb((size_t)nr * 20);
-    const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, comb.data());
+    // the combined rows stay in HBM; the writer streams them by row ranges (bounded host memory)
+    const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, nullptr);
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
+    const int64_t span = (int64_t)1 << 18;
+    std::vector<double> comb((size_t)std::min<int64_t>(span, std::max<int64_t>(nr, 1)) * 20);
+    int64_t b_lo = 0, b_hi = 0;   // rows held in comb
     g_log << "Outfile: " << outfile << "\n";
     for (size_t i = 0; i < plist.size(); ++i) {
         if (i == 0)
@@ -529,7 +539,13 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         for (int64_t r = F.desc.row_offset[c]; r < F.desc.row_offset[c + 1]; ++r) {
             file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
                  << F.desc.time[r] << "," << F.desc.log_length[r] << "," << F.desc.fp[r] << ",";
-            const double *s = &comb[(size_t)r * 20];
+            if (r >= b_hi) {
+                b_lo = r;
+                b_hi = std::min(nr, r + span);
+                const int rr = ggp_predict_rows(F.gpu, b_lo, b_hi, comb.data());
+                if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
+            }
+            const double *s = &comb[(size_t)(r - b_lo) * 20];
             for (int k = 0; k < 4; ++k) {
                 if (k > 0) file << ",";
                 file << s[k];
@@ -703,6 +719,8 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
         {"-j", "--joints", "run calculation of joint probabilities"},
         {"-e", "--evaluate", "evaluate the total log likelihood once at the parameter files' values"},
         {"-hb", "--batched_hessian", "error bars from one batched GPU call (points not chained by carried state)"},
+        {"-g", "--gpus", "GPUs to shard the forest over: 'all' (default), a count N, or ordinals '0,1,..' (repeats: logical shards)"},
+        {"-chunk", "--max_shard_rows", "at most this many rows per shard (caps the -p device workspace), default: one shard per GPU"},
     };
     std::map<std::string, std::string> a;
     a["print_level"] = "0";
@@ -741,6 +759,8 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
             else if (key == "-p") a["predict"] = "1";
             else if (key == "-e") a["evaluate"] = "1";
             else if (key == "-hb") a["batched_hessian"] = "1";
+            else if (key == "-g") a["gpus"] = next();
+            else if (key == "-chunk") a["max_shard_rows"] = next();
             else if (key == "-j") {
                 a["joints"] = "1";
                 a["predict"] = "1";
@@ -839,6 +859,18 @@ int main(int argc, char **argv)
         auto file_number = [&](int i) { return nseg > 1 ? i : -1; };
 
         g_batched_hessian = args.count("batched_hessian") > 0;
+        if (args.count("gpus") && args["gpus"] != "all") {
+            const std::string gs = args["gpus"];
+            if (gs.find(',') == std::string::npos) {
+                const int n = std::stoi(gs);
+                if (n < 1) throw std::invalid_argument("Invalide argument");
+                for (int k = 0; k < n; ++k) g_devices.push_back(k);
+            } else {
+                for (const auto &t : split_string_at(gs, ","))
+                    if (!t.empty()) g_devices.push_back(std::stoi(t));
+            }
+        }
+        if (args.count("max_shard_rows")) g_max_shard_rows = std::stoll(args["max_shard_rows"]);
         if (args.count("evaluate")) {
             for (int i = 0; i < nseg; ++i) {
                 Forest F;

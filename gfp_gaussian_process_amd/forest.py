@@ -125,9 +125,12 @@ class Dataset:
         return int(N.host().ggp_dataset_n_rows(self._h))
 
     def segment_indices(self) -> list:
-        buf = (ctypes.c_int32 * 4096)()
         n = ctypes.c_int32()
-        rc = N.host().ggp_dataset_segments(self._h, buf, 4096, ctypes.byref(n))
+        rc = N.host().ggp_dataset_segments(self._h, None, 0, ctypes.byref(n))   # the count first
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        buf = (ctypes.c_int32 * max(1, n.value))()
+        rc = N.host().ggp_dataset_segments(self._h, buf, n.value, ctypes.byref(n))
         if rc != N.GGP_OK:
             raise GGPError(_host_err())
         return list(buf[: n.value])
@@ -278,7 +281,9 @@ class HostForest:
         pids = [self.parent_ids[i] for i in idx] if self.parent_ids else None
         return HostForest(a, ids, pids, rows=np.asarray(rows, np.int64))
 
-    def desc(self, device: int = 0, kernel: str = "auto") -> N.ForestDesc:
+    def desc(self, devices=(0,), kernel: str = "auto", max_shard_rows: int = 0) -> N.ForestDesc:
+        """ggp_forest_desc; devices: HIP ordinals to shard over (repeats = logical shards on one
+        device), None = every visible device"""
         a = self.a
         d = N.ForestDesc()
         d.n_cells, d.n_rows = self.n_cells, self.n_rows
@@ -302,7 +307,15 @@ class HostForest:
         d.noise_scaled = a["noise_scaled"]
         d.division_binomial = a["division_binomial"]
         d.fp_auto = a["fp_auto"]
-        d.device = device
+        if devices is None:
+            d.n_devices, d.devices = 0, None
+        else:
+            dv = np.ascontiguousarray(devices, np.int32)
+            if dv.ndim != 1 or dv.size == 0:
+                raise ValueError("devices: a non-empty list of HIP ordinals (or None for all)")
+            self._devices = dv                      # keeps the array alive with the descriptor
+            d.n_devices, d.devices = dv.size, dv.ctypes.data_as(N.c_int32_p)
+        d.max_shard_rows = int(max_shard_rows)
         d.kernel = N.KERNELS[kernel]
         return d
 
@@ -319,12 +332,18 @@ def kernel_name(code: int) -> str:
 
 
 class Forest:
-    """Device-resident forest + carried state (one HIP device).  Owns a ggp_forest handle."""
+    """Device-resident forest + carried state.  Owns a ggp_forest handle.
 
-    def __init__(self, host_forest: HostForest, device: int = 0, kernel: str = "auto"):
+    device: one HIP ordinal; devices: a list of ordinals the forest is sharded over (whole
+    trees, include/ggp.h "Sharding"; repeats = logical shards on one device; None = every
+    visible device).  Results have the same bits for any device list."""
+
+    def __init__(self, host_forest: HostForest, device: int = 0, kernel: str = "auto", devices=(),
+                 max_shard_rows: int = 0):
         self.host = host_forest
         self._lib = N.engine()
-        d = host_forest.desc(device, kernel)
+        self._poisoned = False
+        d = host_forest.desc([device] if devices == () else devices, kernel, max_shard_rows)
         h = ctypes.c_void_p()
         rc = self._lib.ggp_forest_create(ctypes.byref(d), ctypes.byref(h))
         if rc != N.GGP_OK:
@@ -337,22 +356,34 @@ class Forest:
         if rc != N.GGP_OK:
             raise GGPError(self._lib.ggp_strerror(rc).decode())
 
+    def _nan(self, nc: int, nr: int):
+        # after a NaN the carried state is unspecified (include/ggp.h "Errors"): the next
+        # evaluation needs reset_state() or set_state() first
+        self._poisoned = True
+        cid = self.host.ids[nc] if (self.host.ids and nc >= 0) else None
+        return LikelihoodIsNan(nc, nr, cid)
+
+    def _usable(self):
+        if self._poisoned:
+            raise GGPError("carried state is unspecified after a NaN evaluation: call reset_state() or set_state()")
+
     def total_likelihood(self, params) -> float:
         p = np.ascontiguousarray(params, np.float64)
         if p.shape != (N.N_PARAMS,):
             raise ValueError("params must hold 11 values (Parameters.h:175 order)")
+        self._usable()
         ll = ctypes.c_double()
         nc, nr = ctypes.c_int64(), ctypes.c_int64()
         rc = self._lib.ggp_total_loglik(self._h, p.ctypes.data_as(N.c_double_p), ctypes.byref(ll),
                                         ctypes.byref(nc), ctypes.byref(nr))
         if rc == N.GGP_ENAN:
-            cid = self.host.ids[nc.value] if (self.host.ids and nc.value >= 0) else None
-            raise LikelihoodIsNan(nc.value, nr.value, cid)
+            raise self._nan(nc.value, nr.value)
         self._check(rc)
         return ll.value
 
     def submit(self, params) -> None:
         """enqueue one evaluation (ggp_total_loglik_async)"""
+        self._usable()
         self._pending = np.ascontiguousarray(params, np.float64)
         self._check(self._lib.ggp_total_loglik_async(self._h, self._pending.ctypes.data_as(N.c_double_p)))
 
@@ -361,7 +392,7 @@ class Forest:
         nc, nr = ctypes.c_int64(), ctypes.c_int64()
         rc = self._lib.ggp_loglik_result(self._h, ctypes.byref(ll), ctypes.byref(nc), ctypes.byref(nr))
         if rc == N.GGP_ENAN:
-            raise LikelihoodIsNan(nc.value, nr.value)
+            raise self._nan(nc.value, nr.value)
         self._check(rc)
         return ll.value
 
@@ -381,6 +412,7 @@ class Forest:
 
     def reset_state(self) -> None:
         self._check(self._lib.ggp_reset_state(self._h))
+        self._poisoned = False
 
     def state(self) -> np.ndarray:
         out = np.zeros((self.n_cells, N.STATE))
@@ -393,6 +425,7 @@ class Forest:
         if st.shape != (self.n_cells, N.STATE):
             raise ValueError(f"state must be [{self.n_cells}, {N.STATE}], got {st.shape}")
         self._check(self._lib.ggp_set_state(self._h, st.ctypes.data_as(N.c_double_p)))
+        self._poisoned = False
 
     def predict(self, params_per_segment, outputs=(True, True, True)):
         """-p smoother (ggp_predict): (forward, backward, combined) [n_rows, 20] arrays; an output
@@ -403,6 +436,22 @@ class Forest:
                                           *(o.ctypes.data_as(N.c_double_p) if o is not None else None
                                             for o in out)))
         return tuple(out)
+
+    def predict_rows(self, r_lo: int, r_hi: int) -> np.ndarray:
+        """combined rows [r_lo, r_hi) of the last predict (ggp_predict_rows), [r_hi - r_lo, 20]"""
+        out = np.zeros((max(0, r_hi - r_lo), N.STATE))
+        self._check(self._lib.ggp_predict_rows(self._h, r_lo, r_hi, out.ctypes.data_as(N.c_double_p)))
+        return out
+
+    def shards(self):
+        """[(device, rows, cells)] of the handle's shards"""
+        n = ctypes.c_int32()
+        self._check(self._lib.ggp_forest_shards(self._h, ctypes.byref(n), None, None, None, 0))
+        dv = (ctypes.c_int32 * max(1, n.value))()
+        rows = (ctypes.c_int64 * max(1, n.value))()
+        cells = (ctypes.c_int64 * max(1, n.value))()
+        self._check(self._lib.ggp_forest_shards(self._h, ctypes.byref(n), dv, rows, cells, n.value))
+        return [(dv[k], rows[k], cells[k]) for k in range(n.value)]
 
     def predict_profile(self):
         """device ms of the last predict: (forward + backward levels, k_combine)"""

@@ -18,6 +18,8 @@
  *                               combine_predictions                  predictions.h:466-499
  *   ggp_forest_create replaces  the in-memory std::vector<MOMAdata> after
  *                               build_cell_genealogy + init_cells    moma_input.h:125-151,738-741
+ *                               (sharded over the devices of the descriptor)
+ *   ggp_predict_rows  replaces  the row loop of write_predictions_to_file predictions.h:563-602
  *
  * Plain pointers and sizes only; no HIP or torch types.  The library copies its inputs.
  *
@@ -30,8 +32,10 @@
  *
  * Errors: return codes instead of C++ exceptions.  GGP_ENAN corresponds to the
  * std::domain_error("Likelihood is Nan") of likelihood.h:71-93; the first NaN in
- * reference order (roots in input order, DFS pre-order, row) is reported.
- * Not re-entrant: one host thread per handle.
+ * reference order (roots in input order, DFS pre-order, row) is reported.  After GGP_ENAN
+ * the carried state is unspecified (the reference terminates there; which cells the failed
+ * call updated depends on the schedule): ggp_reset_state or ggp_set_state before the next
+ * evaluation.  Not re-entrant: one host thread per handle.
  */
 #ifndef GGP_H
 #define GGP_H
@@ -72,9 +76,24 @@ typedef struct {
     int32_t noise_scaled;        /* 1 = "scaled" (default), 0 = "const"              */
     int32_t division_binomial;   /* 1 = "binomial" (default), 0 = "gauss"            */
     double fp_auto;              /* CSVconfig::fp_auto                               */
-    int32_t device;              /* HIP device ordinal                               */
+    int32_t n_devices;           /* shard the forest over these devices; 0 = every
+                                    visible device                                   */
     int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
+    const int32_t *devices;      /* [n_devices] HIP ordinals or NULL (= 0..n_devices-1);
+                                    an ordinal may repeat: logical shards on one device */
+    int64_t max_shard_rows;      /* 0: one shard per device entry; > 0: at least
+                                    ceil(n_rows / max_shard_rows) shards (chunks), dealt
+                                    round-robin over the devices, so the -p workspace
+                                    of a device holds one chunk at a time              */
 } ggp_forest_desc;
+
+/* Sharding.  Trees are independent (likelihood.h:125-159 has no term across
+ * trees), so the handle splits the forest into shards of whole trees -- whole reduction blocks
+ * of B consecutive trees in root order, B a function of the tree count only -- by LPT on row
+ * counts, one shard per device entry (or more, see max_shard_rows).  One host thread enqueues
+ * every device, then sums: each block's trees in a fixed order on its device, the block sums in
+ * a fixed pairwise tree on the host.  So every result (total, NaN location, -p rows, joints,
+ * carried state) has the same bits for any device list -- 8 GPUs, or N logical shards on one. */
 
 #define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 5 cells per SIMD, GROUP up to
                                  8, LANE above (measured crossovers)       */
@@ -126,6 +145,22 @@ int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine);
  * cap or a smaller row range). */
 int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo,
                int64_t r_hi, int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out);
+
+/* combined rows [r_lo, r_hi) (input order) of the last ggp_predict -> out[(r - r_lo) * 20]:
+ * the -p writer streams a forest far larger than host memory by row ranges
+ * (write_predictions_to_file, predictions.h:563-602).  The rows stay in HBM between calls. */
+int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out);
+
+/* the shards the handle made: *n shards; per shard (k < cap) its device, rows and cells */
+int ggp_forest_shards(ggp_forest *f, int32_t *n, int32_t *device, int64_t *rows, int64_t *cells, int32_t cap);
+
+/* test-only device math (tests/test_gpu_device_math.py), one kernel launch on `device`:
+ *   ggp_debug_dawson: Faddeeva::Dawson (Faddeeva.cc:467-471) as the kernels evaluate it;
+ *                     variant 0 = the lane/group form, 1 = the wave schedule's branch-free form
+ *   ggp_debug_tauint: in[6i..6i+5] = (k, t0, t1, a, b, c) -> the k-th tauint of
+ *                     mean_cov_model.h:9-67 from the device primitives (k = 0..3) */
+int ggp_debug_dawson(int32_t device, int32_t variant, const double *x, int64_t n, double *out);
+int ggp_debug_tauint(int32_t device, const double *in, int64_t n, double *out);
 
 /* carried state: zero it (fresh cells), read it back, or restore one read earlier
  * ([n_cells*20], cells in input order) -- a checkpoint of the MOMAdata mean/cov a scan or

@@ -1,0 +1,143 @@
+"""The device Dawson and tauint, pinned directly (not only through totals).
+
+Dawson (Faddeeva::Dawson, Faddeeva.cc:467-471, 1458-1888) in both forms the kernels use
+(variant 0: lane/group `ggp_dawson_tab`; variant 1: the wave schedule's branch-free
+`dawson_bf`), through the test-only C-ABI entry ggp_debug_dawson, against
+  * the reference's own Faddeeva.cc (tests/golden/dawson_ref.json: 6,810 x values incl. every
+    interval edge, |x| = 45 and 5e7; the oracle/_ref build made it): <= 16 ulp, mean < 3 ulp,
+    sign exact -- the bar the CPU oracle meets (test_oracle.py);
+  * the Maple values of Faddeeva.cc's self-test (:2378-2511): 1e-13, the self-test's bound.
+
+tauint (mean_cov_model.h:9-67) through ggp_debug_tauint (the device primitives in tau_body's
+expression order) against tests/golden/tauint_quad.json (quadrature, make_tauint_quad.py) and
+the CPU oracle.  The reference's expressions cancel catastrophically when a = Cll/2 is tiny (the
+propagator's regime: treetauint at a = 5e-8 is off the true integral by 1e5 relative -- in the
+reference itself), so the bar is split:
+  * where the reference's expression is accurate (oracle within 2e-9 of quadrature): the device
+    within 2e-9 of quadrature, incl. the reference test's t1 < t0 case (tests.h:112-117);
+  * everywhere: the device within 64 ulp of the expression's largest term of the oracle value --
+    the rounding the reference's own expression carries.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+
+
+def _engine():
+    from gfp_gaussian_process_amd import _native as N
+    return N.engine(), N
+
+
+def _dev_dawson(xs, variant):
+    lib, N = _engine()
+    x = np.ascontiguousarray(xs, np.float64)
+    out = np.zeros_like(x)
+    assert lib.ggp_debug_dawson(0, variant, x.ctypes.data_as(N.c_double_p), x.size,
+                                out.ctypes.data_as(N.c_double_p)) == N.GGP_OK
+    return out
+
+
+def _ulps(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return np.where(b != 0, np.abs(a - b) / np.spacing(np.abs(b)), np.abs(a) / np.spacing(1e-300))
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_device_dawson_matches_reference_faddeeva(variant):
+    g = json.load(open(os.path.join(GOLDEN, "dawson_ref.json")))
+    xs = np.array([float.fromhex(v) for v in g["x"]])
+    ref = np.array([float.fromhex(v) for v in g["dawson"]])
+    got = _dev_dawson(xs, variant)
+    assert np.array_equal(np.signbit(got), np.signbit(ref))
+    u = _ulps(got, ref)
+    assert u.max() <= 16, (u.max(), xs[int(u.argmax())])
+    assert np.mean(u) < 3
+    # the continued-fraction branch (|x| > 45) and the far tail are covered
+    assert np.sum(np.abs(xs) > 45) > 50 and np.sum(np.abs(xs) >= 5e7) >= 4
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_device_dawson_maple_values(variant):
+    g = json.load(open(os.path.join(GOLDEN, "dawson_maple.json")))
+    xs = [float.fromhex(v) for v in g["x"]]
+    got = _dev_dawson(xs, variant)
+    for x, w, v in zip(xs, (float.fromhex(h) for h in g["dawson"]), got):
+        assert abs(v - w) <= 1e-13 * abs(w), (x, v, w)   # Faddeeva.cc:2237
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_device_dawson_edges_and_lane_mixes(variant):
+    """NaN, 0, odd symmetry, both sides of every branch switch, and waves whose lanes take
+    different branches (the wave form forms the rare branches by ballot)"""
+    from oracle import oracle as O
+    edge = [0.0, -0.0, 1e-300, 1e-20, 0.0299, 0.0301, 44.999999, 45.0, 45.000001, 4.99e7, 5e7, 5.01e7,
+            1e9, 1e300, math.inf]
+    xs = np.array(edge + [-v for v in edge] + list(np.linspace(-60, 60, 97)))
+    got = _dev_dawson(xs, variant)
+    for x, v in zip(xs, got):
+        o = O.dawson(x)
+        if math.isinf(x):
+            assert v == 0.0 or abs(v) < 1e-300
+            continue
+        assert np.signbit(v) == np.signbit(o) or v == 0.0, x
+        assert abs(v - o) <= 8 * np.spacing(abs(o)) + 1e-320, (x, v, o)
+    assert np.isnan(_dev_dawson([math.nan], variant)[0])
+
+
+def _dev_tauint(rows):
+    lib, N = _engine()
+    a = np.ascontiguousarray(rows, np.float64)
+    out = np.zeros(len(a))
+    assert lib.ggp_debug_tauint(0, a.ctypes.data_as(N.c_double_p), len(a), out.ctypes.data_as(N.c_double_p)) == N.GGP_OK
+    return out
+
+
+def _term_scale(k, a, b, c, t0, t1):
+    """largest |term| / denominator of the reference's tauint expression (mean_cov_model.h:9-67)"""
+    from oracle import oracle as O
+    sa = math.sqrt(a)
+    z0, z1 = (b + 2 * a * t0) / (2 * sa), (b + 2 * a * t1) / (2 * sa)
+    D0, D1 = O.dawson(z0), O.dawson(z1)
+    if k == 0:
+        return 2 * max(abs(math.exp(a * t0 * t0 + b * t0 + c) * D0), abs(math.exp(a * t1 * t1 + b * t1 + c) * D1)) / (2 * sa)
+    n = -b * b / (4 * a)
+    E = [math.exp(n + c + z0 * z0), math.exp(n + c + z1 * z1)]
+    ea = [math.exp(t0 * (b + a * t0)), math.exp(t1 * (b + a * t1))]
+    Q = {1: 2 * b, 2: 2 * (2 * a - b * b), 3: 2 * b * (b * b - 6 * a)}[k]
+    P = {1: [1, 1], 2: [b - 2 * a * t0, b - 2 * a * t1],
+         3: [b * b - 4 * a - 2 * a * b * t0 + 4 * a * a * t0 * t0, b * b - 4 * a - 2 * a * b * t1 + 4 * a * a * t1 * t1]}[k]
+    terms = [abs(Q * E[0] * D0), abs(Q * E[1] * D1)] + [abs(2 * sa * math.exp(c) * ea[i] * P[i]) for i in range(2)]
+    den = {1: 4 * a ** 1.5, 2: 8 * a ** 2.5, 3: 16 * a ** 3.5}[k]
+    return max(terms) / den
+
+
+def test_device_tauint_vs_quadrature_and_oracle():
+    from oracle import oracle as O
+    g = json.load(open(os.path.join(GOLDEN, "tauint_quad.json")))["cases"]
+    rows, quad = [], []
+    for c in g:
+        f = lambda k: float.fromhex(c[k])
+        rows.append([c["k"], f("t0"), f("t1"), f("a"), f("b"), f("c")])
+        quad.append(f("value"))
+    dev = _dev_tauint(rows)
+    n_accurate = 0
+    for (k, t0, t1, a, b, cc), q, d in zip(rows, quad, dev):
+        k = int(k)
+        o = O.tauint(k, a, b, cc, t1, t0)
+        assert math.isfinite(d)
+        scale = _term_scale(k, a, b, cc, t0, t1)
+        assert abs(d - o) <= 64 * np.spacing(scale), (k, a, t0, t1, d, o, scale)
+        if abs(o - q) <= 2e-9 * abs(q):                 # the reference's expression is accurate here
+            n_accurate += 1
+            assert abs(d - q) <= 2e-9 * abs(q), (k, a, t0, t1, d, q)
+    assert n_accurate >= 16
+    # the reference test's own case (tests.h:112-117): t1 = 0.2 < t0 = 0.7, every k
+    rev = [r for r in rows if r[1] == 0.7 and r[2] == 0.2]
+    assert len(rev) == 4

@@ -1,0 +1,170 @@
+"""Sharding inside the C-ABI (include/ggp.h "Sharding"): one handle over a
+device list.  On the one-GPU box the list repeats ordinal 0 (logical shards, each a whole-tree
+sub-forest with its own device buffers), which exercises exactly the code an 8-GPU node runs:
+LPT over reduction blocks, per-shard launches from one host thread, block sums gathered and
+summed on the host, global NaN ranks, row/cell scatter.
+
+The bar is BITWISE: the total's shape (tree sums, block sums, a fixed pairwise tree over blocks)
+depends on the tree count only, so any device list gives the same bits as one device -- for
+the carried-state chain, NaN location, batch, -p rows, joints and the CLI's output files.
+"""
+import filecmp
+import math
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_cli import INIT, _param_file, _run, _small_csv
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+
+LISTS = [[0, 0], [0, 0, 0], [0] * 8]
+
+
+def _forest(n_trees=300, rows=60):
+    import gfp_gaussian_process_amd as g
+    return g.HostForest.synthetic(n_trees, rows, with_ids=True)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "lane", "wave"])
+def test_chain_bitwise_for_any_device_list(kernel):
+    import gfp_gaussian_process_amd as g
+    hf = _forest()
+    one = g.Forest(hf, kernel=kernel)
+    many = [g.Forest(hf, devices=d, kernel=kernel) for d in LISTS]
+    chunked = g.Forest(hf, kernel=kernel, max_shard_rows=hf.n_rows // 7)
+    assert [len(f.shards()) for f in many] == [2, 3, 8]
+    assert len(chunked.shards()) >= 7
+    assert sum(r for _, r, _ in chunked.shards()) == hf.n_rows
+    P = list(INIT)
+    for call in range(3):
+        want = one.total_likelihood(P)
+        for f in many + [chunked]:
+            assert f.total_likelihood(P) == want, call
+    st = one.state()
+    for f in many + [chunked]:
+        assert np.array_equal(f.state(), st)
+
+
+def test_shards_balanced_by_rows():
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(1000, 200)
+    f = g.Forest(hf, devices=[0] * 8)
+    rows = [r for _, r, _ in f.shards()]
+    assert sum(rows) == hf.n_rows and max(rows) - min(rows) <= 4 * 200   # blocks of 4 trees
+
+
+def test_nan_location_for_any_device_list():
+    import gfp_gaussian_process_amd as g
+    hf = _forest(60, 40)
+    P = list(INIT)
+    P[2] = -1.0                                   # var_lambda < 0 (test_nan_reported_like_reference)
+    got = []
+    for d in ([0], [0, 0, 0], [0] * 5):
+        with pytest.raises(g.LikelihoodIsNan) as e:
+            g.Forest(hf, devices=d).total_likelihood(P)
+        got.append((e.value.cell, e.value.row, e.value.cell_id))
+    assert got[0][0] >= 0 and all(x == got[0] for x in got)
+
+
+def test_nan_poisons_carried_state_until_reset():
+    """after a NaN the carried state is unspecified (include/ggp.h "Errors"): the Forest refuses
+    to evaluate until reset_state() or set_state()"""
+    import gfp_gaussian_process_amd as g
+    hf = _forest(20, 40)
+    f, ref = g.Forest(hf), g.Forest(hf)
+    bad = list(INIT)
+    bad[2] = -1.0
+    with pytest.raises(g.LikelihoodIsNan):
+        f.total_likelihood(bad)
+    with pytest.raises(g.GGPError, match="reset_state"):
+        f.total_likelihood(INIT)
+    f.reset_state()
+    assert f.total_likelihood(INIT) == ref.total_likelihood(INIT)
+
+
+def test_set_state_across_shards():
+    import gfp_gaussian_process_amd as g
+    hf = _forest(100, 40)
+    a = g.Forest(hf)
+    a.total_likelihood(INIT)
+    ck = a.state()
+    b = g.Forest(hf, devices=[0, 0, 0])
+    b.set_state(ck)
+    assert np.array_equal(b.state(), ck)
+    for _ in range(2):
+        assert b.total_likelihood(INIT) == a.total_likelihood(INIT)
+
+
+def test_batch_bitwise_for_any_device_list():
+    import gfp_gaussian_process_amd as g
+    hf = _forest(120, 40)
+    rng = np.random.default_rng(5)
+    pts = np.stack([np.asarray(INIT) * (1 + 0.02 * rng.standard_normal(11)) for _ in range(7)])
+    pts[3, 2] = -1.0
+    a = g.Forest(hf, kernel="lane")
+    want, wnan = a.total_likelihood_batch(pts)
+    assert list(wnan) == [k == 3 for k in range(7)]
+    for d in LISTS:
+        got, gnan = g.Forest(hf, devices=d).total_likelihood_batch(pts)
+        assert np.array_equal(gnan, wnan)
+        assert np.array_equal(got[~wnan], want[~wnan])
+
+
+@pytest.mark.parametrize("mode", ["devices", "chunks"])
+def test_predict_bitwise_for_any_sharding(mode):
+    """-p per shard (shards on one device share its forward/backward workspace, one after
+    another): every output bitwise the one-shard smoother; ggp_predict_rows streams any range"""
+    import gfp_gaussian_process_amd as g
+    hf = _forest(200, 60)
+    P = np.stack([np.asarray(INIT), np.asarray(INIT) * 1.01])
+    hf.a["segment"] = (hf.a["time"] >= np.median(hf.a["time"])).astype(np.int32)
+    want = g.Forest(hf).predict(P)
+    f = g.Forest(hf, devices=[0, 0, 0]) if mode == "devices" else g.Forest(hf, max_shard_rows=hf.n_rows // 5)
+    got = f.predict(P)
+    for w, x in zip(want, got):
+        assert np.array_equal(w, x)
+    for lo, hi in ((0, hf.n_rows), (17, 1234), (hf.n_rows - 5, hf.n_rows), (100, 100)):
+        assert np.array_equal(f.predict_rows(lo, hi), want[2][lo:hi])
+    sm, cb = f.predict_profile()
+    assert sm > 0 and cb > 0
+
+
+def test_joints_bitwise_for_any_device_list():
+    import gfp_gaussian_process_amd as g
+    hf = _forest(30, 40)
+    P = list(INIT)
+    P[8] = 2.6e4                                  # the well-conditioned joints case (test_gpu_joints.py)
+    one = g.Forest(hf)
+    three = g.Forest(hf, devices=[0, 0, 0])
+    for lo, hi in ((0, hf.n_rows), (33, 611)):
+        iw, vw = one.joints(P, 1e-10, lo, hi)
+        ig, vg = three.joints(P, 1e-10, lo, hi)
+        assert len(iw) > 0
+        assert np.array_equal(iw, ig) and np.array_equal(vw, vg)
+
+
+def _cli_files(tmp_path, csv, cfg, pf, tag, extra):
+    out = tmp_path / tag
+    _run(["-i", csv, "-b", pf, "-c", cfg, "-o", str(out), *extra], tmp_path)
+    return out
+
+
+def test_cli_outputs_identical_for_any_device_list(tmp_path, example_paths):
+    """-e / -s / -m / -p: the output files are byte-identical with the forest on one device, on
+    three logical shards (-g 0,0,0) and in chunks (-chunk)"""
+    csv = _small_csv(tmp_path / "forest.csv", n_trees=40, rows=40)
+    cfg = example_paths["config"]
+    pf = _param_file(tmp_path / "p.txt", {7: "3.35E-04, 3.35E-05", 8: "8.26E-01, 8.26E-02, 4.0E-01, 1.3E+00"})
+    runs = {}
+    for tag, extra in (("one", ["-g", "1"]), ("three", ["-g", "0,0,0"]), ("chunk", ["-g", "1", "-chunk", "300"])):
+        out = _cli_files(tmp_path, csv, cfg, pf, tag, ["-e", "-s", "-m", "-t", "1e-3", "-p", *extra])
+        runs[tag] = out
+    names = sorted(n for n in os.listdir(runs["one"]) if not n.endswith(".log"))
+    assert any(n.endswith("_prediction.csv") for n in names) and any("_scan_" in n for n in names)
+    assert any(n.endswith("_iterations.csv") for n in names)
+    for tag in ("three", "chunk"):
+        assert sorted(n for n in os.listdir(runs[tag]) if not n.endswith(".log")) == names
+        for n in names:
+            assert filecmp.cmp(runs["one"] / n, runs[tag] / n, shallow=False), (tag, n)
