@@ -90,6 +90,12 @@ HOST_SYMBOLS = {
     "ggp_dataset_n_cells": (ctypes.c_int64, [ctypes.c_void_p]),
     "ggp_dataset_n_rows": (ctypes.c_int64, [ctypes.c_void_p]),
     "ggp_dataset_segments": (ctypes.c_int, [ctypes.c_void_p, c_int32_p, ctypes.c_int32, c_int32_p]),
+    "ggp_dataset_is_binary": (ctypes.c_int, [ctypes.c_char_p]),
+    "ggp_dataset_save": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "ggp_dataset_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ggp_dataset_create": (ctypes.c_int, [ctypes.c_int64, c_int64_p, c_double_p, c_double_p, c_double_p, c_int32_p,
+                                          ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                          ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
     "ggp_forest_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "ggp_host_forest_free": (None, [ctypes.c_void_p]),

@@ -1972,11 +1972,17 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
         std::vector<int64_t> order(f->n_blocks);
         std::iota(order.begin(), order.end(), 0);
         std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return blk_rows[a] > blk_rows[b]; });
-        std::vector<int64_t> load(n_shards, 0);
-        for (int64_t b : order) {
-            const int64_t s = std::min_element(load.begin(), load.end()) - load.begin();
-            blk_shard[b] = (int32_t)s;
-            load[s] += blk_rows[b];
+        // LPT; with a row cap, more shards until every shard fits it (a block is never split)
+        for (;;) {
+            std::vector<int64_t> load(n_shards, 0);
+            for (int64_t b : order) {
+                const int64_t s = std::min_element(load.begin(), load.end()) - load.begin();
+                blk_shard[b] = (int32_t)s;
+                load[s] += blk_rows[b];
+            }
+            const int64_t mx = load.empty() ? 0 : *std::max_element(load.begin(), load.end());
+            if (d->max_shard_rows <= 0 || mx <= d->max_shard_rows || n_shards >= f->n_blocks) break;
+            ++n_shards;
         }
     }
     // ---- device contexts (one per distinct ordinal) ----

@@ -524,6 +524,33 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     const int64_t span = (int64_t)1 << 18;
     std::vector<double> comb((size_t)std::min<int64_t>(span, std::max<int64_t>(nr, 1)) * 20);
     int64_t b_lo = 0, b_hi = 0;   // rows held in comb
+    if (args.count("predict_binary")) {
+        // additive: the same 4 means + 10 upper-triangle covariances per row as the CSV, in input
+        // order, as raw doubles: "GGPP0001", int64 n_rows, then [n_rows x 14] f64
+        const std::string binfile = outfile.substr(0, outfile.size() - 4) + ".bin";
+        g_log << "Outfile: " << binfile << "\n";
+        std::ofstream bf(binfile, std::ios::binary);
+        bf.write("GGPP0001", 8);
+        bf.write(reinterpret_cast<const char *>(&nr), 8);
+        std::vector<double> row14;
+        for (int64_t lo = 0; lo < nr; lo += span) {
+            const int64_t hi = std::min(nr, lo + span);
+            const int rr = ggp_predict_rows(F.gpu, lo, hi, comb.data());
+            if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
+            row14.resize((size_t)(hi - lo) * 14);
+            for (int64_t r = lo; r < hi; ++r) {
+                const double *s = &comb[(size_t)(r - lo) * 20];
+                double *o = &row14[(size_t)(r - lo) * 14];
+                for (int k = 0; k < 4; ++k) o[k] = s[k];
+                int q = 4;
+                for (int m = 0; m < 4; ++m)
+                    for (int n = m; n < 4; ++n) o[q++] = s[4 + 4 * m + n];
+            }
+            bf.write(reinterpret_cast<const char *>(row14.data()), (std::streamsize)(row14.size() * sizeof(double)));
+        }
+        if (!bf) throw std::runtime_error("write failed: " + binfile);
+        return;
+    }
     g_log << "Outfile: " << outfile << "\n";
     for (size_t i = 0; i < plist.size(); ++i) {
         if (i == 0)
@@ -720,6 +747,7 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
         {"-e", "--evaluate", "evaluate the total log likelihood once at the parameter files' values"},
         {"-hb", "--batched_hessian", "error bars from one batched GPU call (points not chained by carried state)"},
         {"-g", "--gpus", "GPUs to shard the forest over: 'all' (default), a count N, or ordinals '0,1,..' (repeats: logical shards)"},
+        {"-pbin", "--predict_binary", "write -p's rows as raw doubles (_prediction.bin) instead of the CSV"},
         {"-chunk", "--max_shard_rows", "at most this many rows per shard (caps the -p device workspace), default: one shard per GPU"},
     };
     std::map<std::string, std::string> a;
@@ -761,6 +789,10 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
             else if (key == "-hb") a["batched_hessian"] = "1";
             else if (key == "-g") a["gpus"] = next();
             else if (key == "-chunk") a["max_shard_rows"] = next();
+            else if (key == "-pbin") {
+                a["predict_binary"] = "1";
+                a["predict"] = "1";
+            }
             else if (key == "-j") {
                 a["joints"] = "1";
                 a["predict"] = "1";
@@ -845,8 +877,12 @@ int main(int argc, char **argv)
         const char *cfg_path = args.count("csv_config") ? args["csv_config"].c_str() : "";
         if (ggp_csv_config_load(cfg_path, &cfg) != GGP_OK) throw std::invalid_argument(ggp_host_last_error());
         g_log << "-> Reading" << "\n";
-        if (ggp_dataset_read(args["infile"].c_str(), cfg, &data) != GGP_OK)
+        if (ggp_dataset_is_binary(args["infile"].c_str())) {   // additive: a GGPD0001 binary dataset
+            if (ggp_dataset_load(args["infile"].c_str(), &data) != GGP_OK)
+                throw std::invalid_argument(ggp_host_last_error());
+        } else if (ggp_dataset_read(args["infile"].c_str(), cfg, &data) != GGP_OK) {
             throw std::invalid_argument(ggp_host_last_error());
+        }
         int32_t nseg = 0;
         ggp_dataset_segments(data, nullptr, 0, &nseg);
         std::vector<int32_t> seg(nseg);

@@ -352,6 +352,156 @@ extern "C" int ggp_dataset_read(const char *infile, const ggp_csv_config *cfg_in
     return GGP_OK;
 }
 
+// ---- binary dataset: read_data's output as structure-of-arrays ---------
+// "GGPD0001", int64 n_cells, int64 n_rows, double fp_auto, int64 row_offset[n_cells + 1],
+// double time[n_rows] (already / rescale_time), double log_length[n_rows] (already log),
+// double fp[n_rows], int32 segment[n_rows], int64 n_id_bytes, then per cell its id and its
+// parent id, each NUL-terminated.  Cells in input order; little-endian, no padding.  A forest
+// of 1e9 rows loads at disk speed instead of through the CSV parser.
+namespace {
+const char kDatasetMagic[8] = {'G', 'G', 'P', 'D', '0', '0', '0', '1'};
+
+bool write_all(std::FILE *f, const void *p, size_t bytes) { return bytes == 0 || std::fwrite(p, 1, bytes, f) == bytes; }
+bool read_all(std::FILE *f, void *p, size_t bytes) { return bytes == 0 || std::fread(p, 1, bytes, f) == bytes; }
+}  // namespace
+
+extern "C" int ggp_dataset_is_binary(const char *path)
+{
+    if (!path) return 0;
+    std::FILE *f = std::fopen(path, "rb");
+    if (!f) return 0;
+    char m[8] = {};
+    const bool ok = std::fread(m, 1, 8, f) == 8 && std::memcmp(m, kDatasetMagic, 8) == 0;
+    std::fclose(f);
+    return ok ? 1 : 0;
+}
+
+extern "C" int ggp_dataset_save(const ggp_dataset *d, const char *path)
+{
+    if (!d || !path) return fail(GGP_EINVAL, "null argument");
+    std::FILE *f = std::fopen(path, "wb");
+    if (!f) return fail(GGP_EINVAL, std::string("cannot write ") + path);
+    const int64_t nc = (int64_t)d->cells.size();
+    std::vector<int64_t> ro(nc + 1, 0);
+    for (int64_t c = 0; c < nc; ++c) ro[c + 1] = ro[c] + (int64_t)d->cells[c].time.size();
+    const int64_t nr = ro[nc];
+    std::string ids;
+    for (const Cell &c : d->cells) {
+        ids += c.id;
+        ids.push_back('\0');
+        ids += c.parent_id;
+        ids.push_back('\0');
+    }
+    const int64_t nb = (int64_t)ids.size();
+    bool ok = write_all(f, kDatasetMagic, 8) && write_all(f, &nc, 8) && write_all(f, &nr, 8) &&
+              write_all(f, &d->fp_auto, 8) && write_all(f, ro.data(), ro.size() * 8);
+    for (int col = 0; col < 4 && ok; ++col)
+        for (const Cell &c : d->cells) {
+            if (col == 0) ok = ok && write_all(f, c.time.data(), c.time.size() * 8);
+            if (col == 1) ok = ok && write_all(f, c.log_length.data(), c.log_length.size() * 8);
+            if (col == 2) ok = ok && write_all(f, c.fp.data(), c.fp.size() * 8);
+            if (col == 3) ok = ok && write_all(f, c.segment.data(), c.segment.size() * 4);
+        }
+    ok = ok && write_all(f, &nb, 8) && write_all(f, ids.data(), ids.size());
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? GGP_OK : fail(GGP_EINVAL, std::string("write failed: ") + path);
+}
+
+extern "C" int ggp_dataset_load(const char *path, ggp_dataset **out)
+{
+    if (!path || !out) return fail(GGP_EINVAL, "null argument");
+    std::FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(GGP_EINVAL, std::string("cannot open ") + path);
+    auto bad = [&](const char *why) {
+        std::fclose(f);
+        return fail(GGP_EINVAL, std::string("(ggp_dataset_load) ERROR: ") + why + ": " + path);
+    };
+    char m[8];
+    int64_t nc = 0, nr = 0, nb = 0;
+    double fp_auto = 0;
+    if (!read_all(f, m, 8) || std::memcmp(m, kDatasetMagic, 8) != 0) return bad("not a GGPD0001 file");
+    if (!read_all(f, &nc, 8) || !read_all(f, &nr, 8) || !read_all(f, &fp_auto, 8) || nc < 0 || nr < 0 ||
+        nc > ((int64_t)1 << 31) || nr > ((int64_t)1 << 40))
+        return bad("bad header");
+    std::vector<int64_t> ro(nc + 1);
+    if (!read_all(f, ro.data(), ro.size() * 8) || ro[0] != 0 || ro[nc] != nr) return bad("bad row offsets");
+    for (int64_t c = 0; c < nc; ++c)
+        if (ro[c + 1] < ro[c]) return bad("bad row offsets");
+    std::vector<double> col((size_t)nr);
+    std::vector<int32_t> seg((size_t)nr);
+    auto *ds = new ggp_dataset();
+    ds->fp_auto = fp_auto;
+    ds->cells.resize((size_t)nc);
+    for (int k = 0; k < 3; ++k) {
+        if (!read_all(f, col.data(), col.size() * 8)) {
+            delete ds;
+            return bad("truncated columns");
+        }
+        for (int64_t c = 0; c < nc; ++c) {
+            Cell &cl = ds->cells[(size_t)c];
+            std::vector<double> &dst = k == 0 ? cl.time : k == 1 ? cl.log_length : cl.fp;
+            dst.assign(col.begin() + ro[c], col.begin() + ro[c + 1]);
+        }
+    }
+    if (!read_all(f, seg.data(), seg.size() * 4) || !read_all(f, &nb, 8) || nb < 0) {
+        delete ds;
+        return bad("truncated segments");
+    }
+    std::string ids((size_t)nb, '\0');
+    if (!read_all(f, &ids[0], (size_t)nb)) {
+        delete ds;
+        return bad("truncated ids");
+    }
+    size_t pos = 0;
+    for (int64_t c = 0; c < nc; ++c) {
+        Cell &cl = ds->cells[(size_t)c];
+        cl.segment.assign(seg.begin() + ro[c], seg.begin() + ro[c + 1]);
+        for (std::string *dst : {&cl.id, &cl.parent_id}) {
+            const size_t e = ids.find('\0', pos);
+            if (e == std::string::npos) {
+                delete ds;
+                return bad("truncated ids");
+            }
+            dst->assign(ids, pos, e - pos);
+            pos = e + 1;
+        }
+    }
+    std::fclose(f);
+    *out = ds;
+    return GGP_OK;
+}
+
+extern "C" int ggp_dataset_create(int64_t n_cells, const int64_t *row_offset, const double *time,
+                                  const double *log_length, const double *fp, const int32_t *segment,
+                                  const char *const *ids, const char *const *parent_ids, double fp_auto,
+                                  ggp_dataset **out)
+{
+    if (!out || n_cells < 0 || (n_cells > 0 && (!row_offset || !time || !log_length || !fp || !ids || !parent_ids)))
+        return fail(GGP_EINVAL, "null argument");
+    auto *ds = new ggp_dataset();
+    ds->fp_auto = fp_auto;
+    ds->cells.resize((size_t)n_cells);
+    for (int64_t c = 0; c < n_cells; ++c) {
+        const int64_t a = row_offset[c], b = row_offset[c + 1];
+        if (b < a) {
+            delete ds;
+            return fail(GGP_EINVAL, "bad row offsets");
+        }
+        Cell &cl = ds->cells[(size_t)c];
+        cl.id = ids[c];
+        cl.parent_id = parent_ids[c];
+        cl.time.assign(time + a, time + b);
+        cl.log_length.assign(log_length + a, log_length + b);
+        cl.fp.assign(fp + a, fp + b);
+        if (segment)
+            cl.segment.assign(segment + a, segment + b);
+        else
+            cl.segment.assign((size_t)(b - a), 0);
+    }
+    *out = ds;
+    return GGP_OK;
+}
+
 extern "C" void ggp_dataset_free(ggp_dataset *d) { delete d; }
 extern "C" int64_t ggp_dataset_n_cells(const ggp_dataset *d) { return d ? (int64_t)d->cells.size() : 0; }
 extern "C" int64_t ggp_dataset_n_rows(const ggp_dataset *d)

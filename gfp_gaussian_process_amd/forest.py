@@ -110,11 +110,48 @@ class Dataset:
 
     @classmethod
     def read(cls, infile: str, config: CSVConfig | None = None) -> "Dataset":
+        if N.host().ggp_dataset_is_binary(infile.encode()):
+            return cls.load(infile)
         h = ctypes.c_void_p()
         rc = N.host().ggp_dataset_read(infile.encode(), config._h if config else None, ctypes.byref(h))
         if rc != N.GGP_OK:
             raise GGPError(_host_err())
         return cls(h)
+
+    @classmethod
+    def load(cls, path: str) -> "Dataset":
+        """a binary dataset written by save() (ggp_dataset_load, "GGPD0001")"""
+        h = ctypes.c_void_p()
+        if N.host().ggp_dataset_load(path.encode(), ctypes.byref(h)) != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls(h)
+
+    @classmethod
+    def from_forest(cls, hf: "HostForest") -> "Dataset":
+        """the dataset a flattened forest came from (cells, ids, rows; ggp_dataset_create) --
+        e.g. a synthetic forest to save() for the CLI"""
+        if hf.ids is None or hf.parent_ids is None:
+            raise ValueError("the forest needs cell and parent ids (synthetic(..., with_ids=True))")
+        a = hf.a
+        n = hf.n_cells
+        ids = (ctypes.c_char_p * max(1, n))(*[s.encode() for s in hf.ids])
+        pids = (ctypes.c_char_p * max(1, n))(*[s.encode() for s in hf.parent_ids])
+        arr = {k: np.ascontiguousarray(a[k]) for k in ("row_offset", "time", "log_length", "fp", "segment")}
+        h = ctypes.c_void_p()
+        rc = N.host().ggp_dataset_create(n, arr["row_offset"].ctypes.data_as(N.c_int64_p),
+                                         arr["time"].ctypes.data_as(N.c_double_p),
+                                         arr["log_length"].ctypes.data_as(N.c_double_p),
+                                         arr["fp"].ctypes.data_as(N.c_double_p),
+                                         arr["segment"].astype(np.int32).ctypes.data_as(N.c_int32_p),
+                                         ids, pids, float(a["fp_auto"]), ctypes.byref(h))
+        if rc != N.GGP_OK:
+            raise GGPError(_host_err())
+        return cls(h)
+
+    def save(self, path: str) -> None:
+        """binary dataset ("GGPD0001", ggp_dataset_save): the CLI's -i reads it directly"""
+        if N.host().ggp_dataset_save(self._h, path.encode()) != N.GGP_OK:
+            raise GGPError(_host_err())
 
     @property
     def n_cells(self) -> int:

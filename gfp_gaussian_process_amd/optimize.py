@@ -62,9 +62,10 @@ def nldrmd_minimize(f, x0, lb, ub, dx, ftol_abs: float, maxeval: int = 0):
 
 
 def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, search_space: str = "log",
-                     start=None):
+                     start=None, maxeval: int = 0):
     """maximise objective(params) over the non-fixed parameters (minimizer_nlopt.h:10-215);
-    returns (final parameter vector, maximal log-likelihood, nlopt result)"""
+    returns (final parameter vector, maximal log-likelihood, nlopt result).  maxeval > 0 stops
+    after that many evaluations (MAXEVAL_REACHED; the reference sets none)"""
     log = search_space == "log"
     init = np.asarray(params.init, np.float64)
     start = init if start is None else np.asarray(start, np.float64)
@@ -81,7 +82,7 @@ def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, 
                 lb[i] = ln(params.lower[i])
                 ub[i] = ln(params.upper[i])
     f = (lambda v: -objective(np.exp(v))) if log else (lambda v: -objective(v))
-    xb, minf, rc, _ = nldrmd_minimize(f, x, lb, ub, dx, tolerance)
+    xb, minf, rc, _ = nldrmd_minimize(f, x, lb, ub, dx, tolerance, maxeval)
     if rc == INVALID_ARGS:
         raise ValueError("nlopt invalid argument")
     if rc == FAILURE:

@@ -81,8 +81,9 @@ typedef struct {
     int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
     const int32_t *devices;      /* [n_devices] HIP ordinals or NULL (= 0..n_devices-1);
                                     an ordinal may repeat: logical shards on one device */
-    int64_t max_shard_rows;      /* 0: one shard per device entry; > 0: at least
-                                    ceil(n_rows / max_shard_rows) shards (chunks), dealt
+    int64_t max_shard_rows;      /* 0: one shard per device entry; > 0: as many shards
+                                    (chunks) as it takes for each to hold at most this
+                                    many rows (a reduction block is never split), dealt
                                     round-robin over the devices, so the -p workspace
                                     of a device holds one chunk at a time              */
 } ggp_forest_desc;

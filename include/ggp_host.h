@@ -58,6 +58,19 @@ int ggp_dataset_read(const char *infile, const ggp_csv_config *cfg, ggp_dataset 
 void ggp_dataset_free(ggp_dataset *d);
 int64_t ggp_dataset_n_cells(const ggp_dataset *d);
 int64_t ggp_dataset_n_rows(const ggp_dataset *d);
+/* Binary dataset: read_data's output (cells in input order, time already
+ * rescaled, length already log'd, segment per row, ids) as structure-of-arrays, magic
+ * "GGPD0001" (layout in ggp_host.cpp).  Loads at disk speed where the CSV parser would take
+ * minutes (C4/C5 sizes); everything downstream (segments, get_segment, genealogy) is the same.
+ * ggp_dataset_is_binary: 1 if the file starts with the magic.  ggp_dataset_create: a dataset
+ * from arrays (e.g. a synthetic forest) to save. */
+int ggp_dataset_is_binary(const char *path);
+int ggp_dataset_save(const ggp_dataset *d, const char *path);
+int ggp_dataset_load(const char *path, ggp_dataset **out);
+int ggp_dataset_create(int64_t n_cells, const int64_t *row_offset, const double *time, const double *log_length,
+                       const double *fp, const int32_t *segment, const char *const *ids,
+                       const char *const *parent_ids, double fp_auto, ggp_dataset **out);
+
 /* segment indices in order of first occurrence; *n receives the count (<= cap copied) */
 int ggp_dataset_segments(const ggp_dataset *d, int32_t *out, int32_t cap, int32_t *n);
 

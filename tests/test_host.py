@@ -229,3 +229,35 @@ def test_forest_binary_roundtrip(tmp_path, example_paths):
     syn.save(path)
     s2 = g.HostForest.load(path)
     assert s2.ids is None and np.array_equal(s2.a["time"], syn.a["time"])
+
+
+def test_binary_dataset_roundtrip(tmp_path, example_paths):
+    """the C++ binary dataset ("GGPD0001", ggp_dataset_save / load): the example read from CSV,
+    saved and loaded, builds the bit-identical forest (topology, rows, init statistics) for the
+    whole data set and per segment; a synthetic forest round-trips through from_forest; a
+    truncated or foreign file is rejected"""
+    import gfp_gaussian_process_amd as g
+    ds = g.Dataset.read(example_paths["csv"], g.CSVConfig.load(example_paths["config"]))
+    path = str(tmp_path / "example.ggpd")
+    ds.save(path)
+    back = g.Dataset.read(path)                        # Dataset.read detects the magic
+    assert back.n_cells == ds.n_cells and back.n_rows == ds.n_rows
+    assert back.segment_indices() == ds.segment_indices()
+    a, b = g.HostForest.build(ds, -1), g.HostForest.build(back, -1)
+    assert a.ids == b.ids and a.parent_ids == b.parent_ids
+    for k, v in a.a.items():
+        assert np.array_equal(np.asarray(b.a[k]), np.asarray(v)), k
+    syn = g.HostForest.synthetic(30, 40, with_ids=True)
+    p2 = str(tmp_path / "syn.ggpd")
+    g.Dataset.from_forest(syn).save(p2)
+    s2 = g.HostForest.build(g.Dataset.read(p2), -1)
+    assert s2.ids == syn.ids and s2.a["parent"].tolist() == syn.a["parent"].tolist()
+    for k in ("time", "log_length", "fp", "row_offset", "daughter1", "daughter2", "root_mean_xg", "root_var_xg",
+              "leaf_mean_xg", "leaf_var_xg"):
+        assert np.array_equal(np.asarray(s2.a[k]), np.asarray(syn.a[k])), k
+    raw = open(p2, "rb").read()
+    open(p2, "wb").write(raw[: len(raw) // 2])
+    with pytest.raises(g.GGPError, match="truncated"):
+        g.Dataset.load(p2)
+    with pytest.raises(g.GGPError, match="GGPD0001"):
+        g.Dataset.load(example_paths["params"])
