@@ -3,11 +3,18 @@
 The oracle restatement itself is validated on CPU (tests/test_oracle_joints.py) by an
 identity of the model: with the constant noise model, the target marginal of every joint
 equals the smoothed marginal of -p to ~1e-11.  Here the GPU joints are compared with the
-oracle's: the set of (start, target) pairs (the walk stops where |C_ij / (m_i m_j)| falls
-below the tolerance, so a pair whose ratio sits within rounding of the threshold may stop one
-walk and not the other; every pair present on one side only must follow such a near-threshold
-pair, one whose cross ratio is within 1e3 x tol -- see _compare) and the values of common pairs, normalised by the standard
-deviations, at 1e-6.
+oracle's, start row by start row:
+
+  * pair sets: a walk stops at the first pair whose cross ratio max |C_ij / (m_i m_j)| is below
+    tol (crosscovariance_is_small, correlation_tree.h:484-493).  Every walk must emit exactly the
+    oracle's pairs, in the same order, except after a threshold event: the first pair where the
+    two walks part must have a cross ratio below BAND x tol on the side that emitted it (the
+    ratio of tiny cross-covariances is rounding-dominated there), and the walks may differ only
+    until they meet again (the next sibling subtree).  No blanket slack.
+  * values: every common pair whose cross ratio is above the margin (10 x tol) is compared,
+    normalised by the oracle's standard deviations: at 1e-6, or -- where the reference algorithm
+    itself is ill-conditioned -- at 10 x the oracle's own movement under +-1 ulp noise on exp()
+    (the example data set, whose filter is far less well conditioned than the synthetic forest's).
 """
 import numpy as np
 import pytest
@@ -74,25 +81,51 @@ def _stable(io, vo, ip, vp, bound=1e-6):
     return {keys[n] for n, x in zip(both, e) if x < bound}
 
 
-def _compare(ig, vg, io, vo, tol=1e-10, band=1e3, only=None):
-    kg = {tuple(k): n for n, k in enumerate(ig.tolist())}
-    ko = {tuple(k): n for n, k in enumerate(io.tolist())}
-    common = sorted(set(kg) & set(ko))
-    assert len(common) > 0
-    # The stop rule compares a ratio of tiny cross-covariances (~1e-10 of m_i m_j, far below
-    # the rounding noise of C - K S^-1 K^T at the scale of sd_i sd_j) with tol, so where a walk
-    # ends is itself rounding-dominated: the ORACLE against itself with +-1 ulp noise on exp()
-    # diverges on 4% of the example's pairs, each divergence starting at a pair whose ratio is
-    # 1-64 x tol (tools/joints_diag.py).  Every divergence must start below band * tol, and the
-    # pair sets must agree to within 10%.
-    assert len(set(kg) ^ set(ko)) <= 0.1 * len(ko), (len(set(kg) ^ set(ko)), len(ko))
+MARGIN = 10.0
+
+
+def _walks_agree(ig, vg, io, vo, tol, band):
+    """per start row: identical pair sequences up to the first difference; there the side that
+    emitted the extra pair must show a cross ratio < band * tol (a threshold event); after it
+    the walks may differ until they meet again.  Returns (unexplained events, worst event ratio)."""
+    kg, ko = set(map(tuple, ig.tolist())), set(map(tuple, io.tolist()))
     bad_g, wg = _unexplained(ig, vg, ko, tol, band)
     bad_o, wo = _unexplained(io, vo, kg, tol, band)
-    assert not bad_g and not bad_o, (bad_g[:5], bad_o[:5], len(kg), len(ko))
-    if only is not None:
-        common = [k for k in common if k in only]
+    # sequences: the common pairs come in the same order on both sides
+    for s in np.unique(np.concatenate([ig[:, 0], io[:, 0]])):
+        a = [tuple(k) for k in ig[ig[:, 0] == s].tolist() if tuple(k) in ko]
+        b = [tuple(k) for k in io[io[:, 0] == s].tolist() if tuple(k) in kg]
+        assert a == b, s
+    return bad_g + bad_o, max(wg, wo)
+
+
+def _compare(ig, vg, io, vo, tol=1e-10, band=MARGIN, noise=None, floor=1e-6):
+    """-> (max normalised error over the compared pairs, median, pairs compared, worst event ratio).
+    noise: [(ip, vp), ...] the oracle under +-1 ulp exp() noise (several seeds); a pair's bound
+    is then max(floor, 10 x its largest noise movement), and the pairs some noisy walk does not
+    reach (the reference itself is unstable there: <= 1%) are not compared."""
+    kg = {tuple(k): n for n, k in enumerate(ig.tolist())}
+    ko = {tuple(k): n for n, k in enumerate(io.tolist())}
+    bad, worst = _walks_agree(ig, vg, io, vo, tol, band)
+    assert not bad, (bad[:5], len(kg), len(ko))
+    common = [k for k in sorted(set(kg) & set(ko)) if _ratio(vo[ko[k]]) > MARGIN * tol]
+    assert len(common) > 0
     e = _norm_err(vg[[kg[k] for k in common]], vo[[ko[k] for k in common]])
-    return float(e.max()), float(np.median(e)), len(common)
+    bound = np.full(len(common), floor)
+    if noise is not None:
+        mv, seen = np.zeros(len(common)), np.zeros(len(common), int)
+        for ip, vp in noise:
+            kp = {tuple(k): n for n, k in enumerate(ip.tolist())}
+            has = [n for n, k in enumerate(common) if k in kp]
+            en = _norm_err(vp[[kp[common[n]] for n in has]], vo[[ko[common[n]] for n in has]])
+            mv[has] = np.maximum(mv[has], en)
+            seen[has] += 1
+        keep = seen == len(noise)
+        assert keep.sum() >= 0.99 * len(common), (keep.sum(), len(common))
+        bound = np.where(keep, np.maximum(floor, 10 * mv), np.inf)
+    over = np.nonzero(e > bound)[0]
+    assert len(over) == 0, [(common[n], float(e[n]), float(bound[n])) for n in over[:5]]
+    return float(e.max()), float(np.median(e)), len(common), worst
 
 
 @pytest.mark.parametrize("noise,div", [(1, 1), (0, 0), (1, 0), (0, 1)])
@@ -105,28 +138,38 @@ def test_joints_synthetic_vs_oracle(noise, div):
     p = P if noise else P_CONST
     ig, vg = g.Forest(hf).joints(p, 1e-10)
     io, vo = O.OracleForest(hf.a).joints(p, 1e-10)
-    err, _, n = _compare(ig, vg, io, vo)
+    err, _, n, worst = _compare(ig, vg, io, vo)
+    print(f"synthetic noise={noise} div={div}: {n} pairs, max err {err:.2e}, worst event ratio {worst:.2f} tol")
     assert err < 1e-6, (err, n)
+    # well conditioned: no threshold event at all, the pair lists are identical
+    assert ig.tolist() == io.tolist()
 
 
 def test_joints_example_subset_vs_oracle(example_paths):
     """the reference's example, start rows in the first root cell and around a division.
     The example's joints are far less well conditioned than the synthetic forest's: the oracle
-    against itself under +-1 ulp exp() noise moves them by 5e-7 (median, normalised), and two
-    noise seeds differ by up to 3e-5 on the pairs either seed moves < 1e-6 (measured).  Values
-    are compared on those stable pairs (at least half; the rest are rounding noise in the
-    reference algorithm itself, some with negative variances): max < 1e-4, median < 1e-5."""
+    against itself under +-1 ulp exp() noise moves them by 5e-7 (median, normalised).  Every pair
+    above the margin is compared against 10 x its largest movement over three noise seeds (floor
+    1e-6; measured GPU error / that movement: median 0.7, max 3.2, tools/joints_example_cal.py);
+    the walks' threshold events on this data reach tens of tol (the oracle against its noisy self
+    parts at 1-64 x tol, tools/joints_diag.py), so BAND is 100 here."""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = g.HostForest.from_csv(example_paths["csv"], example_paths["config"], -1, "scaled", "binomial")
-    fg, of, op = g.Forest(hf), O.OracleForest(hf.a), O.OracleForest(hf.a, exp_ulp_noise=12345)
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    ops = [O.OracleForest(hf.a, exp_ulp_noise=s) for s in (12345, 777, 4242)]
     ro = hf.a["row_offset"]
     last = int(ro[1]) - 1                       # the first cell's last row (a division if it has daughters)
     for lo, hi in ((0, 40), (max(0, last - 20), last + 1)):
         ig, vg = fg.joints(P, 1e-10, lo, hi, cap=1 << 21)
         io, vo = of.joints(P, 1e-10, lo, hi, cap=1 << 21)
-        ip, vp = op.joints(P, 1e-10, lo, hi, cap=1 << 21)
-        stable = _stable(io, vo, ip, vp)
-        assert len(stable) >= 0.5 * len(io), (lo, hi, len(stable), len(io))
-        err, med, n = _compare(ig, vg, io, vo, only=stable)
-        assert err < 1e-4 and med < 1e-5, (lo, hi, err, med, n)
+        noisy = [op.joints(P, 1e-10, lo, hi, cap=1 << 21) for op in ops]
+        ip, vp = noisy[0]
+        err, med, n, worst = _compare(ig, vg, io, vo, band=100.0, noise=noisy)
+        kg = {tuple(k): n_ for n_, k in enumerate(ig.tolist())}
+        ko = {tuple(k): n_ for n_, k in enumerate(io.tolist())}
+        st = sorted(k for k in _stable(io, vo, ip, vp) if k in kg)
+        e_st = _norm_err(vg[[kg[k] for k in st]], vo[[ko[k] for k in st]]) if st else np.zeros(1)
+        print(f"example [{lo},{hi}): {n} pairs, max err {err:.2e}, median {med:.2e}, worst event {worst:.1f} tol, "
+              f"stable-pair max {float(e_st.max()):.2e}")
+        assert med < 1e-6, (lo, hi, med)
