@@ -11,8 +11,10 @@ partial (RCCL over xGMI).  Weak scaling: rank r evaluates trees [r*T, (r+1)*T).
   python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group|wave]
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the one with the
-largest share of the evaluation), timed with HIP events on the engine's own stream; `cpu_baseline` is the CPU oracle
-(oracle/, a single-threaded C port of the reference path) timed on this host.
+largest share of the evaluation), timed with HIP events on the engine's own stream; `fp64` sets
+that launch time against the FP64 work per update counted by PMC on this same build
+(profiles/fp64_counts.json); `cpu_baseline` is the CPU oracle (oracle/, a C port of the
+reference path) timed on this host, single-threaded (as the reference) and tree-parallel.
 """
 from __future__ import annotations
 
@@ -27,10 +29,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
-# FP64 VALU work of k_loglik_wave per update, all 64 lanes counted (redundant update lanes
-# included): (ADD + MUL + 2 FMA + TRANS) x 64 per launch / rows per launch, from the PMC pass
-# profiles/r09_fp64_pmc.txt (3.843e7 wave-instructions x 64 / 1.0e5 rows on C2)
-WAVE_FP64_FLOPS_PER_UPDATE = 24593.0
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (AMD spec)
 COMBINE_BYTES_PER_ROW = 484   # k_combine: fwd + bwd rows (2 x 160 B) + prior segment (4 B) read, 160 B written
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
@@ -38,14 +36,46 @@ P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-0
 SEED = 20261015
 
 
-def traffic_for(kernel: str, args):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/traffic.json,
-    tools/pmc_traffic.py) when they were taken on this same default workload; else None"""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    if args.trees != 1000 or args.rows != 200 or not os.path.exists(path):
+def _engine_sha() -> str:
+    import hashlib
+    return hashlib.sha256(open(os.path.join(ROOT, "gfp_gaussian_process_amd", "lib", "libggp.so"), "rb").read()).hexdigest()
+
+
+def _profile_json(name: str, args):
+    """a committed PMC summary (profiles/<name>) -- only if it was taken on this same default
+    workload AND on this very engine build (its recorded sha256): never a stale figure"""
+    path = os.path.join(ROOT, "profiles", name)
+    if args.trees != 1000 or args.rows != 200 or args.kernel != "auto" or not os.path.exists(path):
         return None
-    k = json.load(open(path)).get("kernels", {}).get(kernel)
+    d = json.load(open(path))
+    return d if d.get("engine_sha256") == _engine_sha() else None
+
+
+def traffic_for(kernel: str, args):
+    """HBM bytes per launch of `kernel` from the PMC passes (profiles/traffic.json,
+    tools/pmc_traffic.py), same workload and build only; else None"""
+    d = _profile_json("traffic.json", args)
+    k = None if d is None else d.get("kernels", {}).get(kernel)
     return None if k is None else k["bytes_per_launch"]
+
+
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_threads() -> int:
+    """the host cores this process may use; on the GPU box the job's CPU share is 16
+    (OMP_NUM_THREADS), while os.cpu_count() reports the whole machine"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
 
 
 def cpu_baseline(hf, budget_s: float):
@@ -63,6 +93,25 @@ def cpu_baseline(hf, budget_s: float):
         if el >= budget_s:
             break
     return first, n_eval * hf.n_rows / el, n_eval, el
+
+
+def cpu_baseline_parallel(hf, budget_s: float, threads: int):
+    """the same oracle, tree-parallel: the forest in `threads` whole-tree shards (LPT, the
+    global init statistics kept), one thread each (ctypes drops the GIL in the C oracle);
+    whole evaluations of the forest until `budget_s` elapsed"""
+    from concurrent.futures import ThreadPoolExecutor
+    from gfp_gaussian_process_amd.distributed import shard
+    from oracle import oracle as O
+    parts = [O.OracleForest(shard(hf, r, threads).a) for r in range(threads)]
+    n_eval, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while True:
+            list(ex.map(lambda o: o.total_likelihood(P_EXAMPLE), parts))
+            n_eval += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                break
+    return n_eval * hf.n_rows / el, n_eval, el
 
 
 def main() -> int:
@@ -141,6 +190,22 @@ def main() -> int:
     bytes_per_launch = BYTES_PER_UPDATE * d_rows / d_n
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     info = fg.info()
+    # FP64 rates of the dominant kernel (profiles/fp64_counts.json, tools/fp64_summary.py; same
+    # workload and build only).  useful: the FP64 work one update needs (one lane running the
+    # whole update, the lane schedule on full waves) -- the figure to set against peak; issued:
+    # every lane of every FP64 wave-instruction of the wave schedule, scalar work run in all 64
+    # lanes and unused task candidates included -- an issue rate, not work done
+    fp64 = None
+    cnt = _profile_json("fp64_counts.json", args)
+    if cnt and dom == "k_loglik_wave" and avg_ms > 0 and cnt.get("useful_flops_per_update"):
+        upd_s = (d_rows / d_n) / (avg_ms * 1e-3)
+        useful = cnt["useful_flops_per_update"] * upd_s / 1e12
+        issued = (cnt.get("issued_flops_per_update") or 0.0) * upd_s / 1e12
+        fp64 = {"kernel": dom, "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+                "useful_flops_per_update": cnt["useful_flops_per_update"], "achieved_useful": useful,
+                "frac_useful": useful / FP64_PEAK_TFLOPS,
+                "issued_lane_flops_per_update": cnt.get("issued_flops_per_update"), "issued_lane_rate": issued,
+                "source": "profiles/fp64_counts.json (rocprofv3 PMC of this build) x the live launch time"}
 
     # ---- the same path on a C4-shard-sized forest (BASELINE configs[3]: 100k trees over 8
     # GPUs = 12.5k trees per GPU), reported beside the C2 headline ----
@@ -251,13 +316,7 @@ def main() -> int:
                 "per_kernel_ms": {k: v[0] / v[2] for k, v in per.items()},
                 "note": "algorithmic bytes only; the path is FP64-latency/VALU bound (DESIGN.md)",
             },
-            "fp64": ({
-                "kernel": dom, "flops_per_update": WAVE_FP64_FLOPS_PER_UPDATE,
-                "achieved": WAVE_FP64_FLOPS_PER_UPDATE * (d_rows / d_n) / (avg_ms * 1e-3) / 1e12,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": WAVE_FP64_FLOPS_PER_UPDATE * (d_rows / d_n) / (avg_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                "source": "profiles/r09_fp64_pmc.txt: SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes (FMA = 2)",
-            } if dom == "k_loglik_wave" and avg_ms > 0 else None),
+            "fp64": fp64,
             "total_log_likelihood": ll,
         }
         if large is not None:
@@ -269,10 +328,17 @@ def main() -> int:
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)
+            nth = cpu_threads()
+            prate, pn, pel = cpu_baseline_parallel(hf, args.cpu_budget * 0.6, nth)
             result["cpu_baseline"] = {
                 "value": rate, "unit": "updates/s", "cores": 1, "kind": "port",
                 "sample": f"{n_eval} full evaluations of the same {rows_rank}-row forest "
-                          f"({cel:.1f} s, single thread, oracle/ggp_oracle.c -O3)",
+                          f"({cel:.1f} s, single thread -- the reference is single-threaded -- "
+                          f"oracle/ggp_oracle.c -O3)",
+                "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+                "parallel": {"value": prate, "cores": nth,
+                             "sample": f"{pn} full evaluations in {pel:.1f} s, forest split into {nth} "
+                                       f"whole-tree shards, one oracle thread each"},
             }
             result["ll_rel_err_vs_cpu"] = abs(fresh - ref) / abs(ref)
         print(json.dumps(result), flush=True)

@@ -39,7 +39,12 @@ for k in set(fetch) | set(write):
     if s.startswith("k_"):
         out[s] = {"fetch_bytes": fetch.get(k), "write_bytes": write.get(k),
                   "bytes_per_launch": (fetch.get(k) or 0.0) + (write.get(k) or 0.0)}
+import hashlib
+import os
+lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gfp_gaussian_process_amd", "lib", "libggp.so")
 json.dump({"note": "FETCH_SIZE+WRITE_SIZE (KiB*1024) per dispatch, mean over dispatches; uncorrected "
                    "(8-B loads: the guide's x2 FETCH_SIZE correction is for 16-B/lane streams only)",
+           "engine_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+           "workload": "bench.py defaults (C2: 1000 trees x 200)",
            "kernels": out}, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out, indent=1))
