@@ -659,16 +659,27 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             groups[(size_t)dup[(size_t)f0]].push_back(r);
         }
     }
+    // additive (-js): the sparse form -- one line per (start row, column) a joint lands in, in
+    // the reference's add order, the same 44 value fields; O(joints) instead of O(rows^2).
+    // gfp_gaussian_process_amd/joints_format.py rebuilds the dense file from it byte for byte.
+    const bool sparse = args.count("joints_sparse") > 0;
+    if (sparse) outfile = outfile.substr(0, outfile.size() - 4) + "_sparse.csv";
     g_log << "Outfile: " << outfile << "\n";
     std::ofstream file(outfile);
     for (const Params &P : plist) P.to_csv(file);   // setup_outfile_joints
-    file << "\ncell_id,parent_id,time";
-    file << ",";                                     // write_column_indices
-    for (int64_t r = 0; r < nr; ++r) {
-        file << ggp_host_forest_cell_id(F.host, row_cell[(size_t)r]) << '_' << time[r];
-        write_commas(file, r == nr - 1 ? 43 : 44);
+    if (sparse) {
+        file << "\nstart_row,column,mean_0,mean_1,mean_2,mean_3,mean_4,mean_5,mean_6,mean_7,cov_upper_triangle";
+        for (int k = 0; k < 35; ++k) file << ",";
+        file << "\n";
+    } else {
+        file << "\ncell_id,parent_id,time";
+        file << ",";                                 // write_column_indices
+        for (int64_t r = 0; r < nr; ++r) {
+            file << ggp_host_forest_cell_id(F.host, row_cell[(size_t)r]) << '_' << time[r];
+            write_commas(file, r == nr - 1 ? 43 : 44);
+        }
+        file << "\n";
     }
-    file << "\n";
     const int64_t max_cap = (int64_t)1 << 21;        // joints per call (72 doubles each)
     int64_t cap = (int64_t)1 << 14, chunk = 4096;
     std::vector<int64_t> idx((size_t)(2 * cap));
@@ -701,11 +712,27 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             cols.clear();
             for (; k < n_out && idx[(size_t)(2 * k)] == s; ++k) {
                 const int64_t tgt = idx[(size_t)(2 * k + 1)];
+                if (sparse) {   // every column the add reaches, in add order
+                    const double *j = &val[(size_t)(72 * k)];
+                    auto line = [&](int64_t col) {
+                        file << s << "," << col << ",";
+                        output_values(file, j, 8);
+                        file << ",";
+                        output_upper(file, j + 8, 8);
+                        file << "\n";
+                    };
+                    if (dup[(size_t)tgt] < 0)
+                        line(tgt);
+                    else
+                        for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) line(col);
+                    continue;
+                }
                 if (dup[(size_t)tgt] < 0)
                     cols[tgt] = k;
                 else
                     for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) cols[col] = k;
             }
+            if (sparse) continue;
             file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
                  << time[s];
             int64_t prev = 0;
@@ -747,6 +774,7 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
         {"-e", "--evaluate", "evaluate the total log likelihood once at the parameter files' values"},
         {"-hb", "--batched_hessian", "error bars from one batched GPU call (points not chained by carried state)"},
         {"-g", "--gpus", "GPUs to shard the forest over: 'all' (default), a count N, or ordinals '0,1,..' (repeats: logical shards)"},
+        {"-js", "--joints_sparse", "-j with one line per joint (_joints_sparse.csv) instead of the dense matrix"},
         {"-pbin", "--predict_binary", "write -p's rows as raw doubles (_prediction.bin) instead of the CSV"},
         {"-chunk", "--max_shard_rows", "at most this many rows per shard (caps the -p device workspace), default: one shard per GPU"},
     };
@@ -789,7 +817,11 @@ std::map<std::string, std::string> arg_parser(int argc, char **argv)
             else if (key == "-hb") a["batched_hessian"] = "1";
             else if (key == "-g") a["gpus"] = next();
             else if (key == "-chunk") a["max_shard_rows"] = next();
-            else if (key == "-pbin") {
+            else if (key == "-js") {
+                a["joints"] = "1";
+                a["joints_sparse"] = "1";
+                a["predict"] = "1";
+            } else if (key == "-pbin") {
                 a["predict_binary"] = "1";
                 a["predict"] = "1";
             }

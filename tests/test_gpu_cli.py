@@ -229,3 +229,21 @@ def test_cli_minimize_batched_hessian(tmp_path, example_paths):
     assert np.array_equal(ea[:, 0], eb[:, 0])
     assert np.all(eb[:, 1:] > 0)
     assert np.allclose(ea[:, 1:], eb[:, 1:], rtol=0.1), (ea, eb)
+
+
+def test_cli_sparse_joints_rebuild_the_dense_file(tmp_path, example_paths):
+    """-js writes one line per joint (_joints_sparse.csv, O(joints) instead of O(rows^2));
+    joints_format.sparse_to_dense rebuilds the reference's dense _joints.csv from it and the
+    _prediction.csv byte for byte -- so correlation_from_joint.py reads it unchanged"""
+    from gfp_gaussian_process_amd import joints_format as J
+    csv = _small_csv(tmp_path / "small.csv", n_trees=8, rows=40)
+    pf = _param_file(tmp_path / "p.txt", {})
+    for tag, flag in (("dense", "-j"), ("sparse", "-js")):
+        _run(["-i", csv, "-b", pf, "-c", example_paths["config"], flag, "-o", str(tmp_path / tag)], tmp_path)
+    dense = (tmp_path / "dense" / "small_f_b_joints.csv").read_bytes()
+    sp = tmp_path / "sparse" / "small_f_b_joints_sparse.csv"
+    assert sp.exists() and not (tmp_path / "sparse" / "small_f_b_joints.csv").exists()
+    assert sp.stat().st_size < len(dense) / 2          # walks stay inside a tree (8 trees); dense: rows^2 fields
+    out = tmp_path / "rebuilt.csv"
+    J.sparse_to_dense(str(sp), str(tmp_path / "sparse" / "small_f_b_prediction.csv"), str(out))
+    assert out.read_bytes() == dense

@@ -261,3 +261,26 @@ def test_binary_dataset_roundtrip(tmp_path, example_paths):
         g.Dataset.load(p2)
     with pytest.raises(g.GGPError, match="GGPD0001"):
         g.Dataset.load(example_paths["params"])
+
+
+def test_sparse_joints_converter_handcrafted(tmp_path):
+    """joints_format.sparse_to_dense on a hand-made case: three rows, a duplicated (cell_id, time)
+    column pair (a joint lands in both, Joint_vector::add), rows without joints, the last add
+    winning, the dense header and blank blocks (correlation_tree.h:96-126)"""
+    from gfp_gaussian_process_amd import joints_format as J
+    pred = tmp_path / "p_prediction.csv"
+    pred.write_text("no,name\n0,x\n\ncell_id,parent_id,time,log_length,fp,rest\n"
+                    "1,0,0,0.5,9,z\n1,0,1,0.5,9,z\n2,1,5,0.6,8,z\n")
+    v = lambda k: ",".join(str(k * 100 + i) for i in range(44))   # noqa: E731
+    sp = tmp_path / "j_sparse.csv"
+    sp.write_text("no,name\n0,x\n\nstart_row,column,h" + "," * 43 + "\n"
+                  f"0,1,{v(1)}\n0,2,{v(2)}\n0,1,{v(3)}\n2,0,{v(4)}\n")
+    out = tmp_path / "dense.csv"
+    assert J.sparse_to_dense(str(sp), str(pred), str(out)) == 3
+    blank = "," * 44
+    want = ("no,name\n0,x\n\ncell_id,parent_id,time,1_0" + "," * 44 + "1_1" + "," * 44 + "2_5" + "," * 43 + "\n"
+            + "1,0,0" + blank + "," + v(3) + "," + v(2) + "\n"
+            + "1,0,1" + blank * 3 + "\n"
+            + "2,1,5," + v(4) + blank * 2 + "\n")
+    assert out.read_text() == want
+    assert J.read_sparse(str(sp))[(0, 1)][0] == 300.0
