@@ -60,6 +60,16 @@ GGP_DEV void load_dawson_table(double *s_tab, int lane)
     for (int k = lane; k < kDawsonTab; k += 64) s_tab[k] = ggp_dawson_coef[k];
 }
 
+// the wave schedule's copy: rows padded to ggp::wave::kDawsonRow doubles (128-bit reads)
+constexpr int kDawsonTabP = GGP_DAWSON_NINT * ggp::wave::kDawsonRow;
+GGP_DEV void load_dawson_table_padded(double *s_tab, int lane)
+{
+    for (int k = lane; k < kDawsonTabP; k += 64) {
+        const int row = k / ggp::wave::kDawsonRow, j = k % ggp::wave::kDawsonRow;
+        s_tab[k] = j < GGP_DAWSON_NCOEF ? ggp_dawson_coef[GGP_DAWSON_NCOEF * row + j] : 0.0;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Cell prologue shared by both schedules: init_sc_distribution (predictions.h:63-82).
 // Root: mean + diagonal from init_cells_f and the parameters; the off-diagonals keep this
@@ -456,11 +466,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     namespace W = ggp::wave;
     constexpr int CPW = 8;   // stamp slot 3 (GGP_STAMPS builds only)
     __shared__ double lds[W::kLds];
-    __shared__ double s_tab[kDawsonTab];
+    __shared__ __attribute__((aligned(16))) double s_tab[kDawsonTabP];
     __shared__ double ring_q[64], ring_s[4][64], ring_t[64];
     __shared__ double row_l[64], row_f[64], row_t[65];   // this 64-row chunk's data (+ next time)
     const int lane = threadIdx.x;
-    load_dawson_table(s_tab, lane);
+    load_dawson_table_padded(s_tab, lane);
     const int i = blockIdx.x;
     double *Xl = lds + W::L_X, *Dl = lds + W::L_D, *Pl = lds + W::L_P;
     double *Bv = lds + W::L_BV, *Vl = lds + W::L_V;
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             }
             GGP_STAMP(1);
             {   // stage B: one exponential, one Dawson value, one power per lane
-                const double ev = exp(W::exp_arg(S, T));
+                const double ev = W::exp_ocml(W::exp_arg(S, T));
                 const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
                 const double pw = W::pow_bf(S, T.p);
                 const double rpw = W::rpow_bf(S, T.p);
@@ -1084,12 +1094,14 @@ __global__ __launch_bounds__(64) void k_debug_dawson(const double *__restrict__ 
                                                      double *__restrict__ out)
 {
     __shared__ double s_tab[kDawsonTab];
+    __shared__ __attribute__((aligned(16))) double s_tabp[kDawsonTabP];
     load_dawson_table(s_tab, threadIdx.x);
+    load_dawson_table_padded(s_tabp, threadIdx.x);
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     const double v = i < n ? x[i] : 0.0;
     // every lane of the wave takes part (the wave form's ballots are wave-wide)
-    const double r = variant == 0 ? ggp_dawson_tab(v, s_tab) : ggp::wave::dawson_bf(v, s_tab);
+    const double r = variant == 0 ? ggp_dawson_tab(v, s_tab) : ggp::wave::dawson_bf(v, s_tabp);
     if (i < n) out[i] = r;
 }
 

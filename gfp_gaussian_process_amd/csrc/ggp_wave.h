@@ -191,8 +191,47 @@ GGP_DEV double dawson_arg(const Step &S, const LaneTasks &T)
     return rdiv(T.d_it == 0 ? B : zt, S.two_sa, S.r_two_sa);
 }
 
+// exp(x) exactly as ocml's __ocml_exp_f64 computes it (the same constants, fma chain and
+// ldexp; bitwise the same value), with every Horner step one VOP3 v_fma_f64: the compiler's own
+// form is a v_mov_b64 of the loop-invariant coefficient plus a tied v_fmac_f64 per step
+GGP_DEV double fma3(const double a, const double b, const double c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
+
+GGP_DEV double exp_ocml(const double x)
+{
+    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
+    double t = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, x);
+    t = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, t);
+    double p = fma3(t, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+    p = fma3(t, p, 0x1.71dee623fde64p-19);
+    p = fma3(t, p, 0x1.a01997c89e6b0p-16);
+    p = fma3(t, p, 0x1.a01a014761f6ep-13);
+    p = fma3(t, p, 0x1.6c16c1852b7b0p-10);
+    p = fma3(t, p, 0x1.1111111122322p-7);
+    p = fma3(t, p, 0x1.55555555502a1p-5);
+    p = fma3(t, p, 0x1.5555555555511p-3);
+    p = fma3(t, p, 0x1.000000000000bp-1);
+    p = __builtin_fma(t, p, 1.0);
+    p = __builtin_fma(t, p, 1.0);
+    const double r = __builtin_ldexp(p, (int)dn);
+    const double o = x > 1024.0 ? __builtin_huge_val() : r;
+    return x < -1075.0 ? 0.0 : o;
+}
+
 // ggp_dawson_tab without branches: one division for the continued fraction, a NaN falls
-// through the polynomial (same values as ggp_dawson_tab)
+// through the polynomial (same values as ggp_dawson_tab).  tab: rows of kDawsonRow doubles
+// (the 9 coefficients, zero-padded to 10), 16-B aligned: five 128-bit LDS reads per value;
+// Horner with fused multiply-adds (<= 1 ulp from the separate-rounding form; the device
+// Dawson stays within the reference's bound, tests/test_gpu_device_math.py)
+constexpr int kDawsonRow = 10;
 GGP_DEV double dawson_bf(const double x, const double *tab)
 {
     const double ax = fabs(x);
@@ -200,10 +239,17 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     const double y100 = rdiv(100.0, d1, frcp(d1));   // IEEE 100 / (1 + ax) for finite ax
     const double yk = y100 >= 0.0 ? y100 : 0.0;
     const int k = min((int)yk, GGP_DAWSON_NINT - 1);
-    const double *c = tab + GGP_DAWSON_NCOEF * k;
+    const double2 *c2 = reinterpret_cast<const double2 *>(tab + kDawsonRow * k);
+    const double2 a01 = c2[0], a23 = c2[1], a45 = c2[2], a67 = c2[3], a89 = c2[4];
     const double t = 2.0 * y100 - (double)(2 * k + 1);
-    const double poly =
-        pin(c[0] + (c[1] + (c[2] + (c[3] + (c[4] + (c[5] + (c[6] + (c[7] + c[8] * t) * t) * t) * t) * t) * t) * t) * t);
+    double h = __builtin_fma(a89.x, t, a67.y);
+    h = __builtin_fma(h, t, a67.x);
+    h = __builtin_fma(h, t, a45.y);
+    h = __builtin_fma(h, t, a45.x);
+    h = __builtin_fma(h, t, a23.y);
+    h = __builtin_fma(h, t, a23.x);
+    h = __builtin_fma(h, t, a01.y);
+    const double poly = pin(__builtin_fma(h, t, a01.x));
     // the Taylor and continued-fraction branches are rare (|x| < ~0.03, |x| > 45): formed only
     // when some lane of the wave needs them (a wave-uniform branch; NaN takes neither)
     const bool use_taylor = y100 >= (double)GGP_DAWSON_NINT, use_cf = ax > 45.0;

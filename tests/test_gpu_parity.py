@@ -236,7 +236,9 @@ def test_baseline_size_properties():
     c2 = g.HostForest.synthetic(1000, 200)
     assert _rel(g.Forest(c2).total_likelihood(P), O.OracleForest(c2.a).total_likelihood(P)[0]) < REL
     c3 = g.HostForest.synthetic(10000, 200)
-    f3 = g.Forest(c3)
+    # one schedule for the whole and the halves (auto would run the halves' 5000-cell levels on
+    # the wave schedule and the whole's 10000-cell levels on the lane schedule: ~1e-10 apart)
+    f3 = g.Forest(c3, kernel="lane")
     v = f3.total_likelihood(P)
     assert math.isfinite(v)
     lo, hi = g.HostForest.synthetic(5000, 200), g.HostForest.synthetic(5000, 200, first_tree=5000)
@@ -244,7 +246,7 @@ def test_baseline_size_properties():
     for h in (lo, hi):
         for k in ("root_mean_xg", "root_var_xg", "leaf_mean_xg", "leaf_var_xg"):
             h.a[k] = c3.a[k]
-    s = g.Forest(lo).total_likelihood(P) + g.Forest(hi).total_likelihood(P)
+    s = g.Forest(lo, kernel="lane").total_likelihood(P) + g.Forest(hi, kernel="lane").total_likelihood(P)
     assert _rel(s, v) < 1e-12
 
 
