@@ -1039,7 +1039,8 @@ __global__ __launch_bounds__(kRedMax) void k_reduce_blocks(int64_t n_cells, cons
                                                             const int32_t *__restrict__ gdfs, int n_lblocks,
                                                             double *__restrict__ out_sum, int64_t *__restrict__ out_nan,
                                                             unsigned *__restrict__ done, int64_t *__restrict__ out_seq,
-                                                            int64_t seq)
+                                                            int64_t seq, double *__restrict__ host_sum,
+                                                            int64_t *__restrict__ host_nan)
 {
     __shared__ double s_sum[kRedMax];
     __shared__ long long s_nan[kRedMax];
@@ -1067,20 +1068,33 @@ __global__ __launch_bounds__(kRedMax) void k_reduce_blocks(int64_t n_cells, cons
         }
         __syncthreads();
     }
+    __shared__ bool s_last;
     if (tid == 0) {
         out_sum[pt * n_lblocks + j] = s_sum[0];
         out_nan[pt * n_lblocks + j] = s_nan[0];
+        s_last = false;
         if (out_seq) {
-            // the last workgroup to finish publishes the call's sequence number (the host polls
-            // it, ggp_loglik_result); every block's result is fenced before its count
-            __threadfence_system();
+            // device-scope fence, then count: the last workgroup to finish sees every block
+            __threadfence();
             const unsigned prev = atomicAdd(done, 1u);
-            if (prev + 1 == gridDim.x * gridDim.y) {
-                *done = 0u;                    // ready for the next call (stream ordered)
-                __threadfence_system();
-                __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            s_last = prev + 1 == gridDim.x * gridDim.y;
         }
+    }
+    if (!out_seq) return;
+    __syncthreads();
+    if (!s_last) return;
+    // the last workgroup copies the block results to the mapped host slots in one burst, then
+    // publishes the call's sequence number (the host polls it, ggp_loglik_result)
+    __threadfence();
+    for (int k = tid; k < n_lblocks; k += nt) {
+        host_sum[k] = __hip_atomic_load(out_sum + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        host_nan[k] = __hip_atomic_load(out_nan + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        *done = 0u;                            // ready for the next call (stream ordered)
+        __threadfence_system();
+        __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1242,6 +1256,8 @@ struct Shard {
     int64_t *d_tree_dfs = nullptr;
     int32_t *d_blk_t0 = nullptr, *d_blk_nt = nullptr, *d_gdfs = nullptr;
     unsigned *d_done = nullptr;
+    double *d_blk_sum = nullptr;       // this evaluation's block results (device), before the
+    int64_t *d_blk_nan = nullptr;      // last workgroup copies them to the mapped host slots
     std::vector<int64_t> blk_global;   // local block -> global block
     // the result: pinned, mapped host memory k_reduce_blocks writes directly (no copy back):
     // block sums [n_lblocks], first-NaN codes [n_lblocks], then the call's sequence number
@@ -1374,7 +1390,7 @@ int shard_launch(Shard *s, const ggp_params &P)
     ++s->seq;
     hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, 1), dim3(s->red_threads), 0, s->stream,
                        s->n_cells, s->d_cell_ll, s->d_cell_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt, s->d_gdfs,
-                       (int)s->n_lblocks, s->m_sum, s->m_nan, s->d_done, s->m_seq, s->seq);
+                       (int)s->n_lblocks, s->d_blk_sum, s->d_blk_nan, s->d_done, s->m_seq, s->seq, s->m_sum, s->m_nan);
     s->seq_pending = true;
     HIPCHK(hipGetLastError());
     return GGP_OK;
@@ -1457,6 +1473,7 @@ void shard_destroy(Shard *f)
                     (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell,
                     (void *)f->d_state, (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_tree_dfs,
                     (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
+                    (void *)f->d_blk_sum, (void *)f->d_blk_nan,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -1638,6 +1655,8 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         check(dev_upload(&f->d_blk_t0, t0.data(), t0.size()));
         check(dev_upload(&f->d_blk_nt, blk_ntrees.data(), blk_ntrees.size()));
         check(dev_upload<unsigned>(&f->d_done, nullptr, 1));
+        check(dev_upload<double>(&f->d_blk_sum, nullptr, (size_t)std::max<int64_t>(1, f->n_lblocks)));
+        check(dev_upload<int64_t>(&f->d_blk_nan, nullptr, (size_t)std::max<int64_t>(1, f->n_lblocks)));
         if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
@@ -2229,7 +2248,7 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
             hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,
                                s->stream, nc, s->d_b_ll, s->d_b_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt,
                                s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
-                               (int64_t *)nullptr, (int64_t)0);
+                               (int64_t *)nullptr, (int64_t)0, (double *)nullptr, (int64_t *)nullptr);
             HIPCHK(hipGetLastError());
             sums[k].resize((size_t)np * s->n_lblocks);
             codes[k].resize((size_t)np * s->n_lblocks);
