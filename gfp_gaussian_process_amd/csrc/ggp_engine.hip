@@ -433,27 +433,36 @@ GGP_DEV double readlane_f64(const double v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-// ll terms of rows [base, base + n) from the LDS ring into cl, in row order (ggp_ll_term:
-// q - 0.5 log(det S) - 2 log(2 pi)); false at the first NaN (nan_row set)
-GGP_DEV bool wave_flush_ll(const double *ring_q, const double (*ring_s)[64], double *ring_t, const int n,
+// ll terms of rows [base, base + n) from the LDS ring (x0, x1, S00, S01, S11 per row) into cl,
+// in row order (ggp_ll_term: q - 0.5 log(det S) - 2 log(2 pi)); false at the first NaN (nan_row set)
+GGP_DEV bool wave_flush_ll(const double (*ring_x)[64], const double (*ring_s)[64], double *ring_t, const int n,
                            const int64_t base, const double two_log_2pi, const int lane, double &cl, int &nan_row)
 {
     __syncthreads();
-    if (lane < n)
-        ring_t[lane] = ring_q[lane] -
-                       0.5 * log(ggp_det_pplu(ring_s[0][lane], ring_s[1][lane], ring_s[2][lane], ring_s[3][lane])) -
-                       two_log_2pi;
+    if (lane < n) {
+        const double s00 = ring_s[0][lane], s01 = ring_s[1][lane], s11 = ring_s[2][lane];
+        ring_t[lane] = ggp::wave::ll_quad(ring_x[0][lane], ring_x[1][lane], s00, s01, s11) -
+                       0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - two_log_2pi;
+    }
     __syncthreads();
     bool ok = true;
     if (lane == 0) {
-        for (int k = 0; k < n; ++k) {
-            cl += ring_t[k];
-            if (cl != cl) {
-                nan_row = (int)(base + k);
-                ok = false;
-                break;
+        // the same adds in the same order; the scan for the first NaN row only when the chunk's
+        // sum is NaN (no compare and branch per row on the common path)
+        double acc = cl;
+        for (int k = 0; k < n; ++k) acc += ring_t[k];
+        if (acc != acc) {
+            acc = cl;
+            for (int k = 0; k < n; ++k) {
+                acc += ring_t[k];
+                if (acc != acc) {
+                    nan_row = (int)(base + k);
+                    ok = false;
+                    break;
+                }
             }
         }
+        cl = acc;
     }
     // every lane returns lane 0's verdict
     return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
@@ -464,19 +473,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                                                     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
 {
     namespace W = ggp::wave;
-    constexpr int CPW = 8;   // stamp slot 3 (GGP_STAMPS builds only)
+    const int CPW = gridDim.x <= 1024 ? 8 : 4;   // stamp slot 3: <= 1 wave per SIMD, 2: more (GGP_STAMPS builds only)
     __shared__ double lds[W::kLds];
     __shared__ __attribute__((aligned(16))) double s_tab[kDawsonTabP];
-    __shared__ double ring_q[64], ring_s[4][64], ring_t[64];
+    __shared__ double ring_x[2][64], ring_s[3][64], ring_t[64];
     __shared__ double row_l[64], row_f[64], row_t[65];   // this 64-row chunk's data (+ next time)
     const int lane = threadIdx.x;
     load_dawson_table_padded(s_tab, lane);
     const int i = blockIdx.x;
     double *Xl = lds + W::L_X, *Dl = lds + W::L_D, *Pl = lds + W::L_P;
     double *Bv = lds + W::L_BV, *Vl = lds + W::L_V;
-    const W::LaneTasks T = W::lane_tasks(lane);   // this lane's tasks, registers for the launch
     const double *p = P.p;
     const ggp::OU ou = W::pin_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
+    const W::LaneTasks T = W::lane_tasks(lane, ou);   // this lane's tasks, registers for the launch
     const double var_x = W::pin(p[7]), var_g = W::pin(p[8]), var_dx = W::pin(p[9]), var_dg = W::pin(p[10]);
     double kap[ggp::kOutL];
     ggp::OutTerm tt[ggp::kOutL];
@@ -529,20 +538,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     double dt_cached = __longlong_as_double(0x7ff8000000000000LL);  // NaN: nothing cached yet
     bool live = valid;
     GGP_STAMP_DECL;
-    while (live) {   // the whole workgroup is one cell: uniform
+    // One step (one row).  The first step of the cell is peeled (FIRST): only it can skip the
+    // propagation (a root's first row) or apply the division map (a daughter's), so the steady
+    // loop has neither branch -- nor the register copies the compiler put at their joins.
+    // Every later step propagates: the loop continues only while rows remain.  false = stop
+    // (a NaN term; nan_row set).
+    auto step = [&](auto first) -> bool {
+        constexpr bool FIRST = decltype(first)::value;
         GGP_STAMP(0);
         GGP_STAMP_STEP();
         const double y_l = row_l[slot], y_f = row_f[slot];
         const double t_next = r + 1 < r1 ? row_t[slot + 1] : 0.0;
-        if (pending) {
-            ggp::Step S;
-            ggp::step_init(S, m, C, dt, ou);   // every lane: the same step scalars, in registers
-            if (lane == 0) W::store_v(S, Vl);
+        if (!FIRST || pending) {
+            const W::WStep S = W::wstep(m, C, dt, ou.b);   // every lane: the same step scalars, in registers
+            if (lane == 0) W::store_v(m, C, dt, ou, Vl);
             if (__builtin_amdgcn_readfirstlane(dt == dt_cached ? 0 : 1)) {
                 // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
-                lds[T.xs_dst] = exp(ggp::pickSV(S, T.sv) * S.t);
+                lds[T.xs_dst] = exp(W::sv_of(ou, T.sv) * dt);
                 __syncthreads();
-                lds[T.dv_dst] = ggp::derived_generic(T.dv, Xl, ou.gl, S.t);
+                lds[T.dv_dst] = ggp::derived_generic(T.dv, Xl, ou.gl, dt);
                 __syncthreads();
                 dt_cached = dt;
             }
@@ -570,7 +584,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 vv[q][1] = Vl[tt[q].v2];
                 vv[q][2] = Vl[tt[q].v3];
             }
-            lds[T.i_dst] = W::tau_bf(S, T.it, T.i_km, T.i_ks, Xl, Dl, Pl);   // stage C: one integral per lane
+            lds[T.i_dst] = W::tau_bf(S, T, Xl, Dl, Pl);   // stage C: one integral per lane
             double kv[ggp::kOutL];
 #pragma unroll
             for (int q = 0; q < ggp::kOutL; ++q) kv[q] = ((kap[q] * vv[q][0]) * vv[q][1]) * vv[q][2];
@@ -599,28 +613,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             double o[ggp::kOutN];
 #pragma unroll
             for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
-            ggp::out_finish([&](int k) { return o[k]; }, o);
+#pragma unroll
+            for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j, one rounding
+                if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
             ggp::out_store(o, m, C);
-            if (divide) {
-                ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
-                divide = false;
-            }
+            if (FIRST && divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
             GGP_STAMP(8);
         }
         const double x0 = y_l - m[0];
         const double x1 = y_f - m[1];
-        ggp_innov v;
-        ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
-        {   // the ll term without its determinant and log (ggp_ll_term), into the ring
-            const double h0 = -0.5 * x0, h1 = -0.5 * x1;
-            const double q = (h0 * v.si00 + h1 * v.si10) * x0 + (h0 * v.si01 + h1 * v.si11) * x1;
-            if (lane == 0) {
-                ring_q[slot] = q;
-                ring_s[0][slot] = v.S00;
-                ring_s[1][slot] = v.S01;
-                ring_s[2][slot] = v.S10;
-                ring_s[3][slot] = v.S11;
-            }
+        const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
+        if (lane == 0) {   // the ll term's inputs into the ring (its q, det and log at the flush)
+            ring_x[0][slot] = x0;
+            ring_x[1][slot] = x1;
+            ring_s[0][slot] = v.S00;
+            ring_s[1][slot] = v.S01;
+            ring_s[2][slot] = v.S11;
         }
         ++slot;
         W::posterior(m, C, x0, x1, v, r + 1 == r1);   // lower triangle only on the cell's last row
@@ -631,14 +639,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         live = r < r1;
         GGP_STAMP(9);
         if (slot == 64 || !live) {
-            if (!wave_flush_ll(ring_q, ring_s, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
-                break;
+            if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
+                return false;
             slot = 0;
             if (live) load_chunk(r);
         }
-        __syncthreads();   // LDS slots are rewritten by the next step
         GGP_STAMP(10);
-    }
+        __syncthreads();   // LDS slots are rewritten by the next step
+        GGP_STAMP(11);
+        return true;
+    };
+    if (live && step(std::true_type{}))
+        while (live && step(std::false_type{})) {
+        }
     GGP_STAMP_FLUSH();
     if (valid && lane == 0) {
         double *st = state + (size_t)20 * c;

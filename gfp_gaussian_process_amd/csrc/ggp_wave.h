@@ -82,38 +82,110 @@ enum {
     kLds = L_DUMMY + 64
 };
 
+// ---- the step scalars every lane holds (wave-uniform values, formed from the state) ------
+// Only what the lanes' tasks read: a = Cll/2 and its roots and reciprocals, b + bl, Cxl, and
+// the two bases of the c values.  sqrt(a) is ocml's own iteration (bitwise its value for
+// a >= 2^-767, where ocml does not rescale); its Goldschmidt half-reciprocal is the rdiv
+// seed 1/(2 sqrt a), and its square the seed 1/(4a) (seeds only: rdiv's residual correction
+// makes the quotient independent of an ulp in them).
+struct WStep {
+    double t, a, two_a, four_a, four_aa, two_sa, m2sa, r_two_sa, r_four_a, bbl, Cxl, bx, Cxx;
+};
+
+GGP_DEV WStep wstep(const double *m, const double *C, const double t, const double b)
+{
+    WStep S;
+    S.t = t;
+    const double a = C[10] / 2.;
+    S.a = a;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double r = __builtin_amdgcn_rsq(a);
+#else
+    const double r = 1.0 / sqrt(a);
+#endif
+    double h = 0.5 * r, s = a * r;
+    const double e = __builtin_fma(-h, s, 0.5);
+    s = __builtin_fma(s, e, s);
+    h = __builtin_fma(h, e, h);
+    double d = __builtin_fma(-s, s, a);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, a);
+    s = __builtin_fma(d, h, s);
+    s = (a == 0.0 || a == __builtin_huge_val()) ? a : s;   // ocml: sqrt(+-0, +inf) = the input
+    S.two_sa = 2. * s;
+    S.m2sa = -2. * s;
+    S.r_two_sa = h;
+    S.r_four_a = h * h;
+    S.two_a = 2. * a;
+    S.four_a = 4. * a;
+    S.four_aa = 4 * (a * a);
+    S.bbl = b + m[2];
+    S.Cxl = C[2];
+    S.bx = m[0];
+    S.Cxx = C[0];
+    return S;
+}
+
 // ---- one lane's tasks (registers for the whole launch) ---------------------------------
+// Operands are formed from lane constants instead of select chains:
+//   B  = fma(Cxl, km, b + bl) + gq ks   (km in {1, 2} makes the fma exact: step_init's B bitwise)
+//   ti = t * tau                        (tau in {0, 1, 2}: 0, t, 2t exactly)
+//   c  = fma(kc, t, fma(Cxx, m2, bx m1)) (m1, m2 = 1, 1/2 or 2, 2: the base bx + Cxx/2 or
+//        2 (bx + Cxx) exactly; kc t folds step_init's -b t - gl t ... into one rounding)
 struct LaneTasks {
-    int x_dst, x_kind, x_ic, x_it;
-    double x_km, x_ks;
-    int d_dst, d_it;
-    double d_km, d_ks;
+    int x_dst, x_isE, x_isA;
+    double x_tau, x_km, x_gqks, x_m1, x_m2, x_kc;
+    int d_dst;
+    double d_tau, d_km, d_gqks;
     int p, p_dst0, p_dst1;
     int prod_dst, mult_off;
     ITask it;
-    double i_km, i_ks;
+    double i_tau0, i_tau1, i_km, i_gqks;
     int i_dst;
     int sv, xs_dst, dv_dst;
     DTaskB dv;
     int out_dst;
 };
 
-GGP_DEV LaneTasks lane_tasks(const int lane)
+// kc of c value ic (step_init's c0..c9 as base + kc t)
+GGP_DEV double c_slope(const int ic, const OU &P)
+{
+    const double b = P.b, gl = P.gl, gq = P.gq;
+    switch (ic) {
+    case cA: return -b;
+    case cB: return -b - gl;
+    case cJ: return -b - gq;
+    case cG: return -2 * b;
+    case cC: return -2 * b;
+    case cD: return -(2 * b + gq);
+    case cE: return -2 * b;
+    case cF: return -2 * b + gq;
+    case cI: return -b - gq;
+    default: return -2 * b - 2 * gq;   // cH
+    }
+}
+
+GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
 {
     LaneTasks L;
     const int xj = kXW.j[lane];
     const XTask xt = kXT[xj];
     L.x_dst = L_X + xj;
-    L.x_kind = xt.kind;
-    L.x_ic = xt.ic;
-    L.x_it = xt.it;
-    L.x_km = kKm[xt.iB < 6 ? xt.iB : 0];
-    L.x_ks = kKs[xt.iB < 6 ? xt.iB : 0];
+    L.x_isE = xt.kind == KX_E;
+    L.x_isA = xt.kind == KX_A;
+    L.x_tau = (double)xt.it;
+    const int xb = xt.iB < 6 ? xt.iB : 0;
+    L.x_km = kKm[xb];
+    L.x_gqks = P.gq * kKs[xb];
+    const bool half = xt.ic == cA || xt.ic == cB || xt.ic == cJ || xt.ic == cG || xt.ic == cI;
+    L.x_m1 = half ? 1.0 : 2.0;
+    L.x_m2 = half ? 0.5 : 2.0;
+    L.x_kc = c_slope(xt.ic, P);
     const DTask dk = kDT[lane < ND ? lane : 0];
     L.d_dst = lane < ND ? L_D + lane : L_DUMMY + lane;
-    L.d_it = dk.it;
+    L.d_tau = (double)dk.it;
     L.d_km = kKm[dk.iB];
-    L.d_ks = kKs[dk.iB];
+    L.d_gqks = P.gq * kKs[dk.iB];
     L.p = lane < 3 ? lane : 0;
     L.p_dst0 = lane < 3 ? L_P + lane : L_DUMMY + lane;
     L.p_dst1 = lane < 3 ? L_P + 3 + lane : L_DUMMY + lane;
@@ -124,8 +196,10 @@ GGP_DEV LaneTasks lane_tasks(const int lane)
     L.prod_dst = lane < 4 ? L_X + prod_slot : L_DUMMY + lane;
     L.mult_off = lane < 4 ? mult : L_X + X_ONE;
     L.it = kIT[lane < NI ? lane : 0];
+    L.i_tau0 = (double)L.it.it0;
+    L.i_tau1 = (double)L.it.it1;
     L.i_km = kKm[L.it.iB];
-    L.i_ks = kKs[L.it.iB];
+    L.i_gqks = P.gq * kKs[L.it.iB];
     L.i_dst = lane < NI ? L_BV + BV_I + lane : L_DUMMY + lane;
     L.sv = lane < 6 ? lane : 0;
     L.xs_dst = lane < 6 ? L_X + XS_bt + lane : L_DUMMY + lane;
@@ -139,56 +213,37 @@ GGP_DEV LaneTasks lane_tasks(const int lane)
     return L;
 }
 
-// ---- operand selection from the step scalars (every lane holds the whole Step) ---------
-GGP_DEV double bsel(const Step &S, const double km, const double ks)
+// the exponents s of exp(s t) (pickSV, ggp_prop.h)
+GGP_DEV double sv_of(const OU &P, const int s)
 {
-    return ((S.b + S.bl) + S.Cxl * km) + S.gq * ks;
+    return s == 0 ? P.b : s == 1 ? P.b + P.gl : s == 2 ? 2 * P.b : s == 3 ? P.b + P.gq : s == 4 ? -P.gl : -P.gq;
 }
 
-GGP_DEV double csel(const Step &S, const int ic)
+GGP_DEV double bval(const WStep &S, const double km, const double gqks)
 {
-    const double c0 = pin(S.c0), c1 = pin(S.c1), c2 = pin(S.c2), c3 = pin(S.c3), c4 = pin(S.c4);
-    const double c5 = pin(S.c5), c6 = pin(S.c6), c7 = pin(S.c7), c8 = pin(S.c8), c9 = pin(S.c9);
-    double c = c9;
-    c = ic == 8 ? c8 : c;
-    c = ic == 7 ? c7 : c;
-    c = ic == 6 ? c6 : c;
-    c = ic == 5 ? c5 : c;
-    c = ic == 4 ? c4 : c;
-    c = ic == 3 ? c3 : c;
-    c = ic == 2 ? c2 : c;
-    c = ic == 1 ? c1 : c;
-    c = ic == 0 ? c0 : c;
-    return c;
+    return __builtin_fma(S.Cxl, km, S.bbl) + gqks;
 }
 
-GGP_DEV double tsel(const Step &S, const int it)
+// the argument of exponential task x (exp_body, ggp_prop.h): exp(c) is the Z form at ti = 0
+// (a 0 + B 0 + c == c)
+GGP_DEV double exp_arg(const WStep &S, const LaneTasks &T)
 {
-    const double t = pin(S.t), t2 = pin(S.t2);
-    return it == 0 ? 0.0 : it == 1 ? t : t2;
-}
-
-// the argument of exponential task x (exp_body, ggp_prop.h)
-GGP_DEV double exp_arg(const Step &S, const LaneTasks &T)
-{
-    const double ti = tsel(S, T.x_it);
-    const double B = pin(bsel(S, T.x_km, T.x_ks));
-    const double c = csel(S, T.x_ic);
+    const double ti = S.t * T.x_tau;
+    const double B = pin(bval(S, T.x_km, T.x_gqks));
+    const double c = pin(__builtin_fma(T.x_kc, S.t, __builtin_fma(S.Cxx, T.x_m2, S.bx * T.x_m1)));
     const double n = pin(rdiv(-(B * B), S.four_a, S.r_four_a));
-    const double zt = pin(B + S.two_a * ti);
-    const double z = rdiv(T.x_it == 0 ? B : zt, S.two_sa, S.r_two_sa);
+    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
     const double argA = pin(ti * (B + S.a * ti));
     const double argE = pin(n + c + z * z);
     const double argZ = pin(S.a * (ti * ti) + B * ti + c);
-    return T.x_kind == KX_C ? c : T.x_kind == KX_A ? argA : T.x_kind == KX_E ? argE : argZ;
+    return T.x_isE ? argE : T.x_isA ? argA : argZ;
 }
 
-// the argument of Dawson task d (zval, ggp_prop.h)
-GGP_DEV double dawson_arg(const Step &S, const LaneTasks &T)
+// the argument of Dawson task d (zval, ggp_prop.h; ti = 0: B + 0 == B)
+GGP_DEV double dawson_arg(const WStep &S, const LaneTasks &T)
 {
-    const double B = pin(bsel(S, T.d_km, T.d_ks));
-    const double zt = pin(B + S.two_a * tsel(S, T.d_it));
-    return rdiv(T.d_it == 0 ? B : zt, S.two_sa, S.r_two_sa);
+    const double B = bval(S, T.d_km, T.d_gqks);
+    return rdiv(B + S.two_a * (S.t * T.d_tau), S.two_sa, S.r_two_sa);
 }
 
 // exp(x) exactly as ocml's __ocml_exp_f64 computes it (the same constants, fma chain and
@@ -269,8 +324,8 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     return GGP_SPI2 * (x < 0.0 ? -w : w);
 }
 
-// pow_task without branches
-GGP_DEV double pow_bf(const Step &S, const int p)
+// pow_task without branches (sqrt(a) = two_sa / 2 exactly)
+GGP_DEV double pow_bf(const WStep &S, const int p)
 {
     const double sa = S.two_sa * 0.5, a = S.a;
     const double p0 = pin(4. * (a * sa)), p1 = pin(8. * ((a * a) * sa)), p2 = pin(16. * (((a * a) * a) * sa));
@@ -281,7 +336,7 @@ GGP_DEV double pow_bf(const Step &S, const int p)
 // 2 r4a r2sa, then each next power one factor 2 r4a = 1/(2a) more.  They only seed rdiv
 // (q = x r, then one residual correction against the exact divisor), whose quotient does not
 // depend on a few ulp in r: one division per step less than 1.0 / pow.
-GGP_DEV double rpow_bf(const Step &S, const int p)
+GGP_DEV double rpow_bf(const WStep &S, const int p)
 {
     const double r0 = pin(2. * (S.r_four_a * S.r_two_sa));
     const double r1 = pin(2. * (S.r_four_a * r0));
@@ -290,17 +345,17 @@ GGP_DEV double rpow_bf(const Step &S, const int p)
 }
 
 // tau_unified without branches (X, Dw, PW: the LDS arrays)
-GGP_DEV double tau_bf(const Step &S, const ITask T, const double km, const double ks, const double *X,
-                      const double *Dw, const double *PW)
+GGP_DEV double tau_bf(const WStep &S, const LaneTasks &L, const double *X, const double *Dw, const double *PW)
 {
+    const ITask T = L.it;
     const double D0 = Dw[T.d0], D1 = Dw[T.d1];
     const double E0 = X[T.x0], E1 = X[T.x1];
     const double ec = X[T.xc], ea0 = X[T.xa0], ea1 = X[T.xa1];
     const int k = T.k;
     const int kk = k == 0 ? 0 : k - 1;
     const double pd = PW[kk], pr = PW[3 + kk];
-    const double B = pin(bsel(S, km, ks));
-    const double t0 = tsel(S, T.it0), t1 = tsel(S, T.it1);
+    const double B = pin(bval(S, L.i_km, L.i_gqks));
+    const double t0 = S.t * L.i_tau0, t1 = S.t * L.i_tau1;
     const double BB = pin(B * B);
     const double al3 = pin(BB - 2. * S.two_a);
     const double al = k == 1 ? 1.0 : k == 2 ? B : al3;
@@ -318,10 +373,34 @@ GGP_DEV double tau_bf(const Step &S, const ITask T, const double km, const doubl
     return rdiv(x, den, rden);
 }
 
-// ggp_posterior with the lower triangle of C formed only on the cell's last row: on every
-// other row the next propagation reads the upper triangle (step_init) and then overwrites
-// all of C (out_store), so those six entries are dead.  Same expressions, same bits.
-GGP_DEV void posterior(double *m, double *C, const double x0, const double x1, const ggp_innov &v, const bool last)
+// The measurement step of the wave schedule (ggp_innovation + ggp_posterior, likelihood.h:53-69,
+// predictions.h:84-89) with fused multiply-adds in the gain and the update: C_ij - (a + b)
+// keeps the reference's association (a + b by one fma), so the posterior agrees with the
+// lane schedule's to the last bits of each entry (the wave schedule is not bitwise equal to
+// it anyway, DESIGN.md "Parity").  S10 == S01 here (out_store writes C[4] = C[1]), so
+// si10 == si01.  The lower triangle of C is formed only on the cell's last row: on every
+// other row the next propagation reads the upper triangle and overwrites all of C.
+struct WInnov {
+    double S00, S01, S11, si00, si01, si11;
+};
+
+GGP_DEV WInnov innovation(const double *m, const double *C, const double var_x, const double var_g, const int scaled,
+                          const double fp_auto)
+{
+    WInnov v;
+    const double d11 = scaled ? var_g * (m[1] + fp_auto) : var_g;
+    v.S00 = C[0] + var_x;
+    v.S01 = C[1] + 0.0;
+    v.S11 = C[5] + d11;
+    const double det = v.S00 * v.S11 - v.S01 * v.S01;   // Eigen fixed 2x2 determinant (S10 == S01)
+    const double invdet = 1.0 / det;
+    v.si00 = v.S11 * invdet;
+    v.si01 = -v.S01 * invdet;
+    v.si11 = v.S00 * invdet;
+    return v;
+}
+
+GGP_DEV void posterior(double *m, double *C, const double x0, const double x1, const WInnov &v, const bool last)
 {
     double K[8];
 #pragma unroll
@@ -329,28 +408,38 @@ GGP_DEV void posterior(double *m, double *C, const double x0, const double x1, c
     double KS0[4], KS1[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        KS0[i] = K[i] * v.si00 + K[4 + i] * v.si10;
-        KS1[i] = K[i] * v.si01 + K[4 + i] * v.si11;
+        KS0[i] = __builtin_fma(K[4 + i], v.si01, K[i] * v.si00);
+        KS1[i] = __builtin_fma(K[4 + i], v.si11, K[i] * v.si01);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) m[i] = m[i] + (KS0[i] * x0 + KS1[i] * x1);
+    for (int i = 0; i < 4; ++i) m[i] = m[i] + __builtin_fma(KS1[i], x1, KS0[i] * x0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = i; j < 4; ++j) C[4 * i + j] = C[4 * i + j] - (KS0[i] * K[j] + KS1[i] * K[4 + j]);
+        for (int j = i; j < 4; ++j) C[4 * i + j] = C[4 * i + j] - __builtin_fma(KS1[i], K[4 + j], KS0[i] * K[j]);
     if (last) {   // wave-uniform (one cell per wave)
 #pragma unroll
         for (int i = 1; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < i; ++j) C[4 * i + j] = C[4 * i + j] - (KS0[i] * K[j] + KS1[i] * K[4 + j]);
+            for (int j = 0; j < i; ++j) C[4 * i + j] = C[4 * i + j] - __builtin_fma(KS1[i], K[4 + j], KS0[i] * K[j]);
     }
 }
 
-// the outputs' variables V (ggp_outtab.h): lane 0 stores them, stage D reads them
-GGP_DEV void store_v(const Step &S, double *V)
+// the ll term's quadratic form (ggp_ll_term's q, likelihood.h:26-32) from the ring's row values
+GGP_DEV double ll_quad(const double x0, const double x1, const double S00, const double S01, const double S11)
 {
-    const double v[V_N - 1] = {S.bx,  S.bg,  S.bl - S.ml, S.bq - S.mq, S.Cxx, S.Cxg, S.Cxl, S.Cxq,
-                               S.Cgg, S.Cgl, S.Cgq,       S.Cll,       S.Clq, S.Cqq, S.t};
+    const double det = S00 * S11 - S01 * S01;
+    const double invdet = 1.0 / det;
+    const double si00 = S11 * invdet, si01 = -S01 * invdet, si11 = S00 * invdet;
+    const double h0 = -0.5 * x0, h1 = -0.5 * x1;
+    return (h0 * si00 + h1 * si01) * x0 + (h0 * si01 + h1 * si11) * x1;
+}
+
+// the outputs' variables V (ggp_outtab.h): lane 0 stores them, stage D reads them
+GGP_DEV void store_v(const double *m, const double *C, const double t, const OU &P, double *V)
+{
+    const double v[V_N - 1] = {m[0], m[1], m[2] - P.ml, m[3] - P.mq, C[0], C[1], C[2], C[3],
+                               C[5], C[6], C[7], C[10], C[11], C[15], t};
 #pragma unroll
     for (int k = 0; k < V_N - 1; ++k) V[1 + k] = v[k];
 }

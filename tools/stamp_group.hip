@@ -35,19 +35,20 @@ int main(int argc, char **argv)
     (void)hipMemcpyFromSymbol(all, HIP_SYMBOL(g_stamp), sizeof all);
     const char *gnames[8] = {"prefetch+step_init", "B exp/dawson/pow", "barrier 1", "C integrals",
                              "barrier 2", "D outputs+division", "update", "barrier 3"};
-    const char *wnames[10] = {"step_init+V+dt cache", "B exp/dawson/pow", "barrier B", "C integrals",
+    const char *wnames[11] = {"step_init+V+dt cache", "B exp/dawson/pow", "barrier B", "C integrals",
                               "barrier C", "D output terms", "E butterfly", "readlane+division", "update",
-                              "ll flush+barrier"};
+                              "ll flush (every 64)", "end-of-step barrier"};
     for (int slot = 0; slot < 4; ++slot) {
         const unsigned long long *acc = all + 16 * slot;
         const double steps = (double)acc[15];
         if (steps == 0) continue;
         const bool wave = kernel == 3;
-        const int ns = wave ? 10 : 8;
+        const int ns = wave ? 11 : 8;
         unsigned long long tot = 0;
         for (int k = 0; k < ns; ++k) tot += acc[k];
         printf("trees=%lld %s ll=%.10g wave-steps=%.0f cycles/step=%.0f\n", (long long)trees,
-               wave ? "wave" : (slot == 0 ? "G=64" : "G=32"), ll, steps, tot / steps);
+               wave ? (slot == 3 ? "wave, levels <= 1024 cells" : "wave, levels > 1024 cells")
+                    : (slot == 0 ? "G=64" : "G=32"), ll, steps, tot / steps);
         for (int k = 0; k < ns; ++k)
             printf("  %-22s %8.0f  (%4.1f%%)\n", wave ? wnames[k] : gnames[k], acc[k] / steps, 100.0 * acc[k] / tot);
     }
