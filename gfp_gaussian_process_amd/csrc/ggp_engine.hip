@@ -53,21 +53,36 @@ struct DevForest {
 constexpr int kNanNone = 0x7fffffff;
 
 // Dawson coefficient table copied to LDS once per workgroup (LDS gather ~100 cycles vs an
-// L2 round trip per coefficient from constant memory)
+// L2 round trip per coefficient from constant memory).  Every lane issues all its global loads
+// before the first LDS store (one memory latency per launch, not one per 64 coefficients:
+// the loop form waited for each load, ~8 us of a level launch's fixed cost).
 constexpr int kDawsonTab = GGP_DAWSON_NINT * GGP_DAWSON_NCOEF;
+template <int N, class SRC>
+GGP_DEV void lds_fill(double *dst, const int lane, const SRC &src)
+{
+    constexpr int R = (N + 63) / 64;
+    double v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = src(min(lane + 64 * j, N - 1));
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (lane + 64 * j < N) dst[lane + 64 * j] = v[j];
+}
+
 GGP_DEV void load_dawson_table(double *s_tab, int lane)
 {
-    for (int k = lane; k < kDawsonTab; k += 64) s_tab[k] = ggp_dawson_coef[k];
+    lds_fill<kDawsonTab>(s_tab, lane, [](const int k) { return ggp_dawson_coef[k]; });
 }
 
 // the wave schedule's copy: rows padded to ggp::wave::kDawsonRow doubles (128-bit reads)
 constexpr int kDawsonTabP = GGP_DAWSON_NINT * ggp::wave::kDawsonRow;
 GGP_DEV void load_dawson_table_padded(double *s_tab, int lane)
 {
-    for (int k = lane; k < kDawsonTabP; k += 64) {
+    lds_fill<kDawsonTabP>(s_tab, lane, [](const int k) {
         const int row = k / ggp::wave::kDawsonRow, j = k % ggp::wave::kDawsonRow;
-        s_tab[k] = j < GGP_DAWSON_NCOEF ? ggp_dawson_coef[GGP_DAWSON_NCOEF * row + j] : 0.0;
-    }
+        const double c = ggp_dawson_coef[GGP_DAWSON_NCOEF * row + min(j, GGP_DAWSON_NCOEF - 1)];
+        return j < GGP_DAWSON_NCOEF ? c : 0.0;
+    });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -218,6 +233,18 @@ __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + sta
         st_prev = st_now;                                                                  \
     } while (0)
 #define GGP_STAMP_STEP() ++st_steps
+// phases of a launch (wave schedule): everything issued so far completes, then the stamp
+__device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], [.][8] = launches
+#define GGP_PSTAMP_DECL unsigned long long pst[8] = {0}
+#define GGP_PSTAMP(k) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(pst[k])::"memory")
+#define GGP_PSTAMP_FLUSH()                                                                 \
+    do {                                                                                   \
+        if (threadIdx.x == 0) {                                                            \
+            const int s_ = gridDim.x <= 1024 ? 0 : 1;                                      \
+            for (int k_ = 1; k_ < 8; ++k_) atomicAdd(&g_pstamp[s_][k_], pst[k_] - pst[k_ - 1]); \
+            atomicAdd(&g_pstamp[s_][8], 1ull);                                             \
+        }                                                                                  \
+    } while (0)
 #define GGP_STAMP_FLUSH()                                                                  \
     do {                                                                                   \
         if (threadIdx.x == 0) {                                                            \
@@ -231,6 +258,9 @@ __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + sta
 #define GGP_STAMP(k)
 #define GGP_STAMP_STEP()
 #define GGP_STAMP_FLUSH()
+#define GGP_PSTAMP_DECL
+#define GGP_PSTAMP(k)
+#define GGP_PSTAMP_FLUSH()
 #endif
 
 constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI + ggp::SB_N;   // doubles of LDS per cell
@@ -468,19 +498,165 @@ GGP_DEV bool wave_flush_ll(const double (*ring_x)[64], const double (*ring_s)[64
     return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
 }
 
+// Level launches: block b runs cell cells[b].  Path launches (one launch for a whole forest
+// whose levels all take the wave schedule): block b runs the path cells[seq[b] .. seq[b+1]),
+// a root or second daughter followed by first daughters down to a leaf; each cell after the
+// first inherits its parent's posterior in registers.  The Dawson table and the lane tasks
+// are set up once per block.  A path's first cell, if a second daughter, waits for its
+// parent's done flag (this evaluation's epoch; relaxed polls, then an agent-scope acquire);
+// a cell with a second daughter publishes its state and then its flag (agent-scope release).
+// Paths are ordered by the depth of their first cell, so a parent's path has a lower block
+// index: blocks are dispatched in index order, a waiting block only waits on a lower one, and
+// the lowest unfinished path never waits -- no deadlock, whatever the occupancy.
+// chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c}.
+constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling: a broken chain ends as NaN, not a hang
+
+// The state a second daughter takes over crosses XCDs: agent-scope atomic (sc1) stores and
+// loads, coherent without the L2 writeback / invalidate of a release / acquire (a writeback per
+// finishing parent cost more than the launch gap the path launch saves).  The writer waits for
+// its stores to complete before the flag store; the reader loads after seeing the flag.
+GGP_DEV void chain_publish(double *st, const double *m, const double *C, unsigned *flag, const unsigned epoch)
+{
+    unsigned long long *q = reinterpret_cast<unsigned long long *>(st);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        __hip_atomic_store(q + k, (unsigned long long)__double_as_longlong(m[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        __hip_atomic_store(q + 4 + k, (unsigned long long)__double_as_longlong(C[k]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0): the state is at the coherence point
+    __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// In-launch reduction of a path launch (replaces k_reduce_blocks there, with the same sums):
+// the last path of a tree to finish forms the tree sum (DFS order), the last tree of a block
+// the block sum (k_reduce_blocks' 64-wide LDS tree, emulated on the block's <= 8 trees: a path
+// launch has at most as many leaves as the device holds wave blocks, so B <= 8), and the last
+// block copies the block results to the mapped host slots and publishes the call's sequence
+// number.  Counters are agent-scope atomics with a handful of arrivals each (tree: its paths,
+// block: its trees, done: the blocks); the last arrival resets its counter for the next call.
+struct ChainRed {
+    const int32_t *path_tree;     // local tree of each path (nullptr: level launches, no reduction)
+    const int32_t *tree_npaths;   // paths per local tree
+    const int32_t *tree_blk;      // local block of each local tree
+    const int64_t *tree_dfs;      // DFS start of each local tree, then the end
+    const int32_t *blk_t0, *blk_nt, *gdfs;
+    unsigned *cnt_tree, *cnt_blk, *done;
+    double *tree_sum;
+    long long *tree_nan;
+    double *out_sum;
+    long long *out_nan;
+    int64_t *out_seq;
+    double *host_sum;
+    long long *host_nan;
+    int n_lblocks;
+};
+constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
+
+GGP_DEV unsigned add_agent(unsigned *p) { return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+GGP_DEV void zero_agent(unsigned *p) { __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+GGP_DEV double ld_agent(const double *p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+GGP_DEV void st_agent(double *p, const double v)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+GGP_DEV T ld_agent_i(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+GGP_DEV void st_agent_i(T *p, const T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+GGP_DEV void chain_reduce(const ChainRed &R, const int64_t seq, const int b, const int lane, const double *cell_ll,
+                          const int32_t *cell_nan)
+{
+    int last = 0;
+    if (lane == 0) {
+        __builtin_amdgcn_s_waitcnt(0);   // this path's cell results are at the coherence point
+        const int t = R.path_tree[b];
+        if (add_agent(R.cnt_tree + t) + 1 == (unsigned)R.tree_npaths[t]) {
+            zero_agent(R.cnt_tree + t);
+            double v = 0.0;
+            long long code = kChainNoNan;
+            for (int64_t i = R.tree_dfs[t]; i < R.tree_dfs[t + 1]; ++i) {
+                v += ld_agent(cell_ll + i);
+                const int nr = ld_agent_i(cell_nan + i);
+                if (nr != kNanNone && code == kChainNoNan) code = ((long long)R.gdfs[i] << 24) | (long long)nr;
+            }
+            st_agent(R.tree_sum + t, v);
+            st_agent_i(R.tree_nan + t, code);
+            __builtin_amdgcn_s_waitcnt(0);
+            const int j = R.tree_blk[t];
+            if (add_agent(R.cnt_blk + j) + 1 == (unsigned)R.blk_nt[j]) {
+                zero_agent(R.cnt_blk + j);
+                const int t0 = R.blk_t0[j], nb = R.blk_nt[j];
+                double sv[8];
+                long long sn[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    sv[k] = k < nb ? ld_agent(R.tree_sum + t0 + k) : 0.0;
+                    sn[k] = k < nb ? ld_agent_i(R.tree_nan + t0 + k) : kChainNoNan;
+                }
+#pragma unroll
+                for (int w = 32; w >= 1; w >>= 1)   // k_reduce_blocks' tree over 64 slots; slots >= 8 hold 0
+#pragma unroll
+                    for (int k = 0; k < 8 && k < w; ++k) {
+                        sv[k] = sv[k] + (k + w < 8 ? sv[(k + w) & 7] : 0.0);
+                        sn[k] = min(sn[k], k + w < 8 ? sn[(k + w) & 7] : kChainNoNan);
+                    }
+                st_agent(R.out_sum + j, sv[0]);
+                st_agent_i(R.out_nan + j, sn[0]);
+                __builtin_amdgcn_s_waitcnt(0);
+                if (add_agent(R.done) + 1 == (unsigned)R.n_lblocks) {
+                    zero_agent(R.done);
+                    last = 1;
+                }
+            }
+        }
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    // the last block: every block result to the mapped host slots in one burst, then the seq
+    for (int k = lane; k < R.n_lblocks; k += 64) {
+        R.host_sum[k] = ld_agent(R.out_sum + k);
+        R.host_nan[k] = ld_agent_i(R.out_nan + k);
+    }
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+GGP_DEV void chain_take(const double *st, double *m, double *C)
+{
+    const unsigned long long *q = reinterpret_cast<const unsigned long long *>(st);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        m[k] = __longlong_as_double((long long)__hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        C[k] = __longlong_as_double((long long)__hip_atomic_load(q + 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
                                                     int n, double *__restrict__ state,
-                                                    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
+                                                    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan,
+                                                    const int2 *__restrict__ chain, unsigned *cell_done,
+                                                    const unsigned epoch, const int32_t *__restrict__ seq,
+                                                    const ChainRed *__restrict__ red, const int64_t call_seq)
 {
     namespace W = ggp::wave;
-    const int CPW = gridDim.x <= 1024 ? 8 : 4;   // stamp slot 3: <= 1 wave per SIMD, 2: more (GGP_STAMPS builds only)
+    [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // stamp slot 3: <= 1 wave per SIMD, 2: more (GGP_STAMPS builds only)
     __shared__ double lds[W::kLds];
     __shared__ __attribute__((aligned(16))) double s_tab[kDawsonTabP];
     __shared__ double ring_x[2][64], ring_s[3][64], ring_t[64];
     __shared__ double row_l[64], row_f[64], row_t[65];   // this 64-row chunk's data (+ next time)
     const int lane = threadIdx.x;
+    GGP_PSTAMP_DECL;
+    GGP_PSTAMP(0);
     load_dawson_table_padded(s_tab, lane);
-    const int i = blockIdx.x;
+    GGP_PSTAMP(1);
     double *Xl = lds + W::L_X, *Dl = lds + W::L_D, *Pl = lds + W::L_P;
     double *Bv = lds + W::L_BV, *Vl = lds + W::L_V;
     const double *p = P.p;
@@ -495,21 +671,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         kap[q] = ggp::out_kappa(ou, tt[q].kap);
     }
     const int bs = ggp::kOutBlock[lane];
+    GGP_PSTAMP(2);
+    if (lane == 0) {
+        Xl[ggp::X_ONE] = 1.0;
+        Bv[ggp::BV_ONE] = 1.0;
+        Vl[ggp::V_ONE] = 1.0;
+    }
+    // the exp(s t) block in LDS depends on the parameters and dt only: it stays valid from one
+    // cell of this wave to the next
+    double dt_cached = __longlong_as_double(0x7ff8000000000000LL);  // NaN: nothing cached yet
+    GGP_STAMP_DECL;
+    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
+    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
+    int64_t prev_last = -1;   // the previous cell's last row (its daughter's division interval)
+    for (int i = i_lo; i < i_hi; ++i) {
     int c = 0;
     int64_t r = 0, r1 = 0, r0 = 0;
     double dt = 0.0, t_cur = 0.0;
     bool pending = false, divide = false;
-    const bool valid = i < n;
+    const bool valid = true;
+    int2 ch = {-1, 0};
+    bool chain_broken = false;
     if (valid) {
         c = cells[i];
+        ch = chain[c];
+        if (ch.x >= 0) {   // the parent runs in this launch: wait for its state
+            unsigned spins = 0;
+            while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                __builtin_amdgcn_s_sleep(8);
+                if (++spins > kChainSpinMax) {
+                    chain_broken = true;
+                    break;
+                }
+            }
+        }
         r0 = F.row_off[c];
         r1 = F.row_off[c + 1];
         r = r0;
-        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in m, C
+            pending = true;
+            dt = F.time[r0] - F.time[prev_last];
+        } else if (ch.x >= 0) {   // a second daughter of a cell in another path
+            chain_take(state + (size_t)20 * ch.x, m, C);
+            pending = true;
+            dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
+        } else {
+            pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        }
         divide = pending;
         t_cur = F.time[r0];
+        prev_last = r1 - 1;
     }
+    GGP_PSTAMP(3);
     // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane), so
     // the step loop issues no global loads and never waits on one
     auto load_chunk = [&](const int64_t base) {
@@ -526,18 +740,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         if (lane == 0) row_t[64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
     };
     if (valid) load_chunk(r0);
-    if (lane == 0) {
-        Xl[ggp::X_ONE] = 1.0;
-        Bv[ggp::BV_ONE] = 1.0;
-        Vl[ggp::V_ONE] = 1.0;
-    }
     __syncthreads();
     double cl = 0.0;
     int nan_row = kNanNone;
     int slot = 0;                                                   // rows in the ll ring = row - chunk base
-    double dt_cached = __longlong_as_double(0x7ff8000000000000LL);  // NaN: nothing cached yet
-    bool live = valid;
-    GGP_STAMP_DECL;
+    bool live = valid && !chain_broken;
+    if (chain_broken) {
+        cl = __longlong_as_double(0x7ff8000000000000LL);
+        nan_row = 0;
+    }
     // One step (one row).  The first step of the cell is peeled (FIRST): only it can skip the
     // propagation (a root's first row) or apply the division map (a daughter's), so the steady
     // loop has neither branch -- nor the register copies the compiler put at their joins.
@@ -561,15 +772,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 dt_cached = dt;
             }
             GGP_STAMP(1);
-            {   // stage B: one exponential, one Dawson value, one power per lane
+            {   // stage B: one exponential and one Dawson value per lane; lane 0: the denominators
                 const double ev = W::exp_ocml(W::exp_arg(S, T));
                 const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
-                const double pw = W::pow_bf(S, T.p);
-                const double rpw = W::rpow_bf(S, T.p);
+                if (lane == 0) W::store_pw(S, Pl);
                 lds[T.x_dst] = ev;
                 lds[T.d_dst] = dv;
-                lds[T.p_dst0] = pw;
-                lds[T.p_dst1] = rpw;
                 lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
             }
             GGP_STAMP(2);
@@ -596,9 +804,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             for (int q = 0; q < ggp::kOutL; ++q) bv[q] = Bv[tt[q].basis];
             asm volatile("" ::"v"(bv[0]), "v"(bv[1]), "v"(bv[2]), "v"(bv[3]));
             static_assert(ggp::kOutL == 4, "stage D issues kOutL reads together");
-            double acc = 0.0;
+            double acc = kv[0] * bv[0];   // the lane's terms, fused (the table's sums, not bitwise ggp::outputs)
 #pragma unroll
-            for (int q = 0; q < ggp::kOutL; ++q) acc = acc + kv[q] * bv[q];
+            for (int q = 1; q < ggp::kOutL; ++q) acc = __builtin_fma(kv[q], bv[q], acc);
             GGP_STAMP(6);
             {   // block sums: DPP butterfly (ggp::out_partner)
                 double w;
@@ -649,19 +857,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         GGP_STAMP(11);
         return true;
     };
-    if (live && step(std::true_type{}))
+    GGP_PSTAMP(4);
+    const bool more = live && step(std::true_type{});
+    GGP_PSTAMP(5);
+    if (more)
         while (live && step(std::false_type{})) {
         }
-    GGP_STAMP_FLUSH();
+    GGP_PSTAMP(6);
     if (valid && lane == 0) {
         double *st = state + (size_t)20 * c;
+        st_agent(cell_ll + F.dfs_rank[c], cl);          // coherent: a path launch sums them in-launch
+        st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
+        if (ch.y) {
+            chain_publish(st, m, C, cell_done + c, epoch);   // for the second daughter
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st[k] = m[k];
+            for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-        cell_ll[F.dfs_rank[c]] = cl;
-        cell_nan[F.dfs_rank[c]] = nan_row;
+            for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+        }
     }
+    GGP_PSTAMP(7);
+    __syncthreads();   // the LDS rows and ring are the next cell's
+    }
+    GGP_STAMP_FLUSH();
+    GGP_PSTAMP_FLUSH();
+    if (red) chain_reduce(*red, call_seq, blockIdx.x, lane, cell_ll, cell_nan);
 }
 
 
@@ -1263,6 +1484,22 @@ struct Shard {
     int32_t *d_row_cell = nullptr;    // -j: cell of every row
     double *d_state = nullptr, *d_cell_ll = nullptr;
     int32_t *d_cell_nan = nullptr;
+    // chained wave launches (k_loglik_wave): per cell {parent to wait for, has a waiting daughter},
+    // done flags holding the epoch of the evaluation that finished the cell
+    int2 *d_chain = nullptr;
+    unsigned *d_cell_done = nullptr;
+    unsigned epoch = 0;
+    int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
+    int32_t *d_path_cells = nullptr, *d_path_seq = nullptr;   // path launch: cells, [n_paths + 1] starts
+    int64_t n_paths = 0;               // 0: level launches
+    // path launch's in-launch reduction (ChainRed): path -> tree, paths per tree, tree -> block,
+    // arrival counters, per-tree partial results
+    int32_t *d_path_tree = nullptr, *d_tree_npaths = nullptr, *d_tree_blk = nullptr;
+    unsigned *d_cnt_tree = nullptr, *d_cnt_blk = nullptr;
+    double *d_tree_sum = nullptr;
+    int64_t *d_tree_nan = nullptr;
+    void *d_red = nullptr;             // the ChainRed of the path launch (device copy)
+    std::vector<int32_t> level_kind;   // GGP_KERNEL_* each level runs
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
     int64_t n_trees = 0, n_lblocks = 0;
     int red_threads = 64;
@@ -1330,32 +1567,62 @@ namespace {
 // trees, cpw 64 fastest everywhere).
 int lane_cpw(const Shard *f) { return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : 64; }
 
+// the schedule of a level of n cells: the handle's choice, or auto (measured,
+// profiles/r08_schedule_scan.txt): up to 5 cells per SIMD the wave schedule (GGP_AUTO_SMALL=group:
+// the bitwise-lane-equal one), up to 8 per SIMD the group schedule with 1-8 cells per wave,
+// above that the lane schedule
+int level_kind(const Shard *f, int64_t n)
+{
+    return f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
+           : n <= f->wave_max_cells          ? f->auto_small
+           : n <= f->group_max_cells         ? GGP_KERNEL_GROUP
+                                             : GGP_KERNEL_LANE;
+}
+
 int launch_levels(Shard *f, const ggp_params &P)
 {
     const int n_levels = (int)f->level_start.size() - 1;
     f->n_prof = 0;
+    ++f->epoch;
+    auto prof_begin = [&]() -> hipError_t {
+        if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) return hipEventRecord(f->ev[2 * f->n_prof], f->stream);
+        return hipSuccess;
+    };
+    auto prof_end = [&](int64_t rows) -> hipError_t {
+        if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
+            const hipError_t e = hipEventRecord(f->ev[2 * f->n_prof + 1], f->stream);
+            f->ev_kernel[f->n_prof] = f->last_code;
+            f->ev_rows_launch[f->n_prof] = rows;
+            f->n_prof++;
+            return e;
+        }
+        return hipSuccess;
+    };
+    if (f->n_paths > 0) {   // every level on the wave schedule: one launch, one block per path
+        HIPCHK(prof_begin());
+        hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
+                           f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
+                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq);
+        HIPCHK(hipGetLastError());
+        f->kernel_used = GGP_KERNEL_WAVE;
+        f->last_code = GGP_KERNEL_WAVE << 8 | 64;
+        HIPCHK(prof_end(f->n_rows));
+        return GGP_OK;
+    }
     for (int L = 0; L < n_levels; ++L) {
         const int64_t a = f->level_start[L], b = f->level_start[L + 1];
         const int n = (int)(b - a);
         if (n <= 0) continue;
-        if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
-            HIPCHK(hipEventRecord(f->ev[2 * f->n_prof], f->stream));
-        }
+        HIPCHK(prof_begin());
         const int64_t n_simd = (int64_t)f->n_cu * 4;
-        // auto (measured, profiles/r08_schedule_scan.txt): up to 5 cells per SIMD the wave
-        // schedule (GGP_AUTO_SMALL=group: the bitwise-lane-equal one), up to 8 per SIMD the
-        // group schedule with 1-8 cells per wave, above that the lane schedule
-        const int kind = f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
-                         : n <= f->wave_max_cells          ? f->auto_small
-                         : n <= f->group_max_cells         ? GGP_KERNEL_GROUP
-                                                           : GGP_KERNEL_LANE;
-        const bool group = kind == GGP_KERNEL_GROUP;
+        const int kind = f->level_kind[L];
         if (kind == GGP_KERNEL_WAVE) {
             hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                               f->d_state, f->d_cell_ll, f->d_cell_nan);
+                               f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
+                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
-        } else if (group) {
+        } else if (kind == GGP_KERNEL_GROUP) {
             // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
             int cpw = 1;
@@ -1383,12 +1650,7 @@ int launch_levels(Shard *f, const ggp_params &P)
             f->last_code = GGP_KERNEL_LANE << 8 | 1;
         }
         HIPCHK(hipGetLastError());
-        if (f->profile && 2 * (f->n_prof + 1) <= (int)f->ev.size()) {
-            HIPCHK(hipEventRecord(f->ev[2 * f->n_prof + 1], f->stream));
-            f->ev_kernel[f->n_prof] = f->last_code;
-            f->ev_rows_launch[f->n_prof] = f->ev_rows[L];
-            f->n_prof++;
-        }
+        HIPCHK(prof_end(f->ev_rows[L]));
     }
     return GGP_OK;
 }
@@ -1398,9 +1660,13 @@ int shard_launch(Shard *s, const ggp_params &P)
 {
     if (s->n_cells == 0) return GGP_OK;
     HIPCHK(hipSetDevice(s->device));
+    ++s->seq;
     const int rc = launch_levels(s, P);
     if (rc != GGP_OK) return rc;
-    ++s->seq;
+    if (s->n_paths > 0) {   // the path launch reduced in-launch
+        s->seq_pending = true;
+        return GGP_OK;
+    }
     hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, 1), dim3(s->red_threads), 0, s->stream,
                        s->n_cells, s->d_cell_ll, s->d_cell_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt, s->d_gdfs,
                        (int)s->n_lblocks, s->d_blk_sum, s->d_blk_nan, s->d_done, s->m_seq, s->seq, s->m_sum, s->m_nan);
@@ -1486,7 +1752,10 @@ void shard_destroy(Shard *f)
                     (void *)f->d_level_cells, (void *)f->d_dfs_rank, (void *)f->d_prior_seg, (void *)f->d_row_cell,
                     (void *)f->d_state, (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_tree_dfs,
                     (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
-                    (void *)f->d_blk_sum, (void *)f->d_blk_nan,
+                    (void *)f->d_blk_sum, (void *)f->d_blk_nan, (void *)f->d_chain, (void *)f->d_cell_done,
+                    (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_tree,
+                    (void *)f->d_tree_npaths, (void *)f->d_tree_blk, (void *)f->d_cnt_tree, (void *)f->d_cnt_blk,
+                    (void *)f->d_tree_sum, (void *)f->d_tree_nan, f->d_red,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -1706,6 +1975,110 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     F.log2 = std::log(2.);
     F.scaled = d->noise_scaled ? 1 : 0;
     F.binomial = d->division_binomial ? 1 : 0;
+    // schedule per level; when every level takes the wave schedule and the forest has at most as
+    // many leaves as the device holds wave blocks, one path launch (k_loglik_wave): paths
+    // (a root or second daughter, then first daughters to a leaf) ordered by the depth of
+    // their first cell, and the chain table of the second daughters' waits
+    {
+        const int n_levels = (int)f->level_start.size() - 1;
+        f->level_kind.assign(std::max(0, n_levels), GGP_KERNEL_LANE);
+        bool all_wave = n_levels > 0;
+        for (int L = 0; L < n_levels; ++L) {
+            f->level_kind[L] = level_kind(f, f->level_start[L + 1] - f->level_start[L]);
+            all_wave = all_wave && f->level_kind[L] == GGP_KERNEL_WAVE;
+        }
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0) == hipSuccess && per_cu > 0)
+            f->wave_resident = per_cu * f->n_cu;
+        if (const char *e = getenv("GGP_WAVE_PATHS_MAX")) f->wave_resident = atoi(e);
+        std::vector<int2> ch(nc, int2{-1, 0});
+        std::vector<int32_t> heads, pcells, pseq;
+        auto next_of = [&](int32_t c) { return d->daughter1[c] >= 0 ? d->daughter1[c] : d->daughter2[c]; };
+        if (all_wave) {
+            for (int64_t c = 0; c < nc; ++c) {
+                const int32_t pa = d->parent[c];
+                if (pa < 0 || next_of(pa) != c) heads.push_back((int32_t)c);
+            }
+            std::stable_sort(heads.begin(), heads.end(), [&](int32_t a2, int32_t b2) { return depth[a2] < depth[b2]; });
+        }
+        // the in-launch reduction emulates k_reduce_blocks' 64-wide tree on <= 8 trees per block
+        bool small_blocks = f->red_threads == 64;
+        for (int32_t v : blk_ntrees) small_blocks = small_blocks && v <= 8;
+        if (all_wave && small_blocks && (int64_t)heads.size() <= f->wave_resident) {
+            pseq.push_back(0);
+            for (int32_t h : heads) {
+                for (int32_t c = h; c >= 0 && (int64_t)pcells.size() <= nc; c = next_of(c)) pcells.push_back(c);
+                pseq.push_back((int32_t)pcells.size());
+                const int32_t pa = d->parent[h];
+                if (pa >= 0) {
+                    ch[h].x = pa;
+                    ch[pa].y = 1;
+                }
+            }
+            if ((int64_t)pcells.size() != nc && rc == GGP_OK) {
+                g_last_err = "path decomposition does not cover the forest";
+                rc = GGP_EINVAL;
+            }
+            f->n_paths = (int64_t)heads.size();
+            check(dev_upload(&f->d_path_cells, pcells.data(), pcells.size()));
+            check(dev_upload(&f->d_path_seq, pseq.data(), pseq.size()));
+            // reduction tables: the tree of each path (by its first cell's DFS position), paths
+            // per tree, the block of each tree
+            std::vector<int32_t> rank(nc);
+            for (int64_t k = 0; k < nc; ++k) rank[dfs[k]] = (int32_t)k;
+            const int64_t ntr = (int64_t)tree_start.size() - 1;
+            std::vector<int32_t> ptree(heads.size()), npaths(std::max<int64_t>(1, ntr), 0), tblk(std::max<int64_t>(1, ntr), 0);
+            for (size_t q = 0; q < heads.size(); ++q) {
+                const int64_t k = rank[heads[q]];
+                const int32_t t = (int32_t)(std::upper_bound(tree_start.begin(), tree_start.end(), k) - tree_start.begin() - 1);
+                ptree[q] = t;
+                npaths[t]++;
+            }
+            for (int64_t j = 0, t = 0; j < (int64_t)blk_ntrees.size(); ++j)
+                for (int32_t u = 0; u < blk_ntrees[j]; ++u, ++t) tblk[t] = (int32_t)j;
+            check(dev_upload(&f->d_path_tree, ptree.data(), ptree.size()));
+            check(dev_upload(&f->d_tree_npaths, npaths.data(), npaths.size()));
+            check(dev_upload(&f->d_tree_blk, tblk.data(), tblk.size()));
+            check(dev_upload<unsigned>(&f->d_cnt_tree, nullptr, npaths.size()));
+            check(dev_upload<unsigned>(&f->d_cnt_blk, nullptr, std::max<size_t>(1, blk_ntrees.size())));
+            check(dev_upload<double>(&f->d_tree_sum, nullptr, npaths.size()));
+            check(dev_upload<int64_t>(&f->d_tree_nan, nullptr, npaths.size()));
+            if (rc == GGP_OK && (hipMemset(f->d_cnt_tree, 0, npaths.size() * sizeof(unsigned)) != hipSuccess ||
+                                 hipMemset(f->d_cnt_blk, 0, std::max<size_t>(1, blk_ntrees.size()) * sizeof(unsigned)) != hipSuccess))
+                rc = GGP_EDEV;
+            if (rc == GGP_OK) {
+                ChainRed R{};
+                R.path_tree = f->d_path_tree;
+                R.tree_npaths = f->d_tree_npaths;
+                R.tree_blk = f->d_tree_blk;
+                R.tree_dfs = f->d_tree_dfs;
+                R.blk_t0 = f->d_blk_t0;
+                R.blk_nt = f->d_blk_nt;
+                R.gdfs = f->d_gdfs;
+                R.cnt_tree = f->d_cnt_tree;
+                R.cnt_blk = f->d_cnt_blk;
+                R.done = f->d_done;
+                R.tree_sum = f->d_tree_sum;
+                R.tree_nan = (long long *)f->d_tree_nan;
+                R.out_sum = f->d_blk_sum;
+                R.out_nan = (long long *)f->d_blk_nan;
+                R.out_seq = f->m_seq;
+                R.host_sum = f->m_sum;
+                R.host_nan = (long long *)f->m_nan;
+                R.n_lblocks = (int)f->n_lblocks;
+                ChainRed *dr = nullptr;
+                check(dev_upload(&dr, &R, 1));
+                f->d_red = dr;
+            }
+        }
+        check(dev_upload(&f->d_chain, ch.data(), nc));
+        check(dev_upload<unsigned>(&f->d_cell_done, nullptr, nc));
+        if (rc == GGP_OK && nc > 0 && hipMemset(f->d_cell_done, 0, (size_t)nc * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
+        if (rc != GGP_OK) {
+            shard_destroy(f);
+            return rc;
+        }
+    }
     // per-level rows for the roofline bookkeeping
     f->ev_rows.assign(f->level_start.size() - 1, 0);
     for (size_t L = 0; L + 1 < f->level_start.size(); ++L)

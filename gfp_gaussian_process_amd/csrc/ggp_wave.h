@@ -2,8 +2,9 @@
 // one 64-lane wave per cell; in every stage of a step each lane runs ONE task:
 //
 //   stage B   lane l: exponential kXW[l] (64 state-dependent exponentials), Dawson value l
-//             (l < 14), power l (l < 3); then lanes 0..3 form exp(c_B), exp(c_J), exp(c_G),
-//             exp(c_I) as exp(c_A) times a cached exponential
+//             (l < 14); lane 0 stores the tauint denominators and their reciprocals; then
+//             lanes 0..3 form exp(c_B), exp(c_J), exp(c_G), exp(c_I) as exp(c_A) times a
+//             cached exponential
 //   stage C   lane l: integral l (l < 45)
 //   per dt    exp(s t) (6) and the 18 exp-derived basis values of the outputs depend on the
 //             parameters and dt only: formed when dt changes, kept in LDS
@@ -74,8 +75,8 @@ constexpr double kKs[6] = {0., -1., 0., -1., 1., 1.};
 enum {
     L_X = 0,                  // exponentials (NX, incl. X_ONE = 1)
     L_D = L_X + NX,           // Dawson values
-    L_P = L_D + ND,           // 4 a^1.5, 8 a^2.5, 16 a^3.5, reciprocals
-    L_BV = L_P + NPW,         // outputs basis: 1, the 45 integrals, 18 exp-derived values
+    L_P = L_D + ND,           // tauint denominators 2 sqrt a, 4 a^1.5, 8 a^2.5, 16 a^3.5, then reciprocals
+    L_BV = L_P + 8,           // outputs basis: 1, the 45 integrals, 18 exp-derived values
     L_V = L_BV + BV_N,        // outputs variables: 1, state, t
     L_OUT = L_V + V_N,        // the step's 14 outputs (block sums, written by the lead lanes)
     L_DUMMY = L_OUT + kOutN,  // one slot per lane for stores of lanes without a task
@@ -137,10 +138,9 @@ struct LaneTasks {
     double x_tau, x_km, x_gqks, x_m1, x_m2, x_kc;
     int d_dst;
     double d_tau, d_km, d_gqks;
-    int p, p_dst0, p_dst1;
     int prod_dst, mult_off;
     ITask it;
-    double i_tau0, i_tau1, i_km, i_gqks;
+    double i_tau0, i_tau1, i_km, i_gqks, i_s1;
     int i_dst;
     int sv, xs_dst, dv_dst;
     DTaskB dv;
@@ -186,9 +186,6 @@ GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
     L.d_tau = (double)dk.it;
     L.d_km = kKm[dk.iB];
     L.d_gqks = P.gq * kKs[dk.iB];
-    L.p = lane < 3 ? lane : 0;
-    L.p_dst0 = lane < 3 ? L_P + lane : L_DUMMY + lane;
-    L.p_dst1 = lane < 3 ? L_P + 3 + lane : L_DUMMY + lane;
     // exp(c_B) = exp(c_A) exp(-gl t), exp(c_J) = exp(c_I) = exp(c_A) exp(-gq t),
     // exp(c_G) = exp(c_A) / exp(b t)   (c_* of step_init)
     const int prod_slot = lane == 0 ? XC_B : lane == 1 ? XC_J : lane == 2 ? XC_G : XC_I;
@@ -196,6 +193,7 @@ GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
     L.prod_dst = lane < 4 ? L_X + prod_slot : L_DUMMY + lane;
     L.mult_off = lane < 4 ? mult : L_X + X_ONE;
     L.it = kIT[lane < NI ? lane : 0];
+    L.i_s1 = L.it.k == 2 ? 1.0 : -1.0;
     L.i_tau0 = (double)L.it.it0;
     L.i_tau1 = (double)L.it.it1;
     L.i_km = kKm[L.it.iB];
@@ -276,9 +274,10 @@ GGP_DEV double exp_ocml(const double x)
     p = fma3(t, p, 0x1.000000000000bp-1);
     p = __builtin_fma(t, p, 1.0);
     p = __builtin_fma(t, p, 1.0);
-    const double r = __builtin_ldexp(p, (int)dn);
-    const double o = x > 1024.0 ? __builtin_huge_val() : r;
-    return x < -1075.0 ? 0.0 : o;
+    // ocml's range checks (x > 1024 -> inf, x < -1075 -> 0) are left out: v_ldexp_f64 already
+    // overflows to inf and underflows to 0 for every finite x that far out (the int conversion
+    // saturates); only x = +-inf (a non-finite state) gives NaN here instead of inf / 0
+    return __builtin_ldexp(p, (int)dn);
 }
 
 // ggp_dawson_tab without branches: one division for the continued fraction, a NaN falls
@@ -292,9 +291,15 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     const double ax = fabs(x);
     const double d1 = 1.0 + ax;
     const double y100 = rdiv(100.0, d1, frcp(d1));   // IEEE 100 / (1 + ax) for finite ax
-    const double yk = y100 >= 0.0 ? y100 : 0.0;
-    const int k = min((int)yk, GGP_DAWSON_NINT - 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+    int kt;   // v_cvt_i32_f64: NaN -> 0 (then t and the value are NaN), no guard needed
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(kt) : "v"(y100));
+    const int k = min(kt, GGP_DAWSON_NINT - 1);
+    const double2 *c2 = reinterpret_cast<const double2 *>(tab + __mul24(k, kDawsonRow));
+#else
+    const int k = min((int)(y100 >= 0.0 ? y100 : 0.0), GGP_DAWSON_NINT - 1);
     const double2 *c2 = reinterpret_cast<const double2 *>(tab + kDawsonRow * k);
+#endif
     const double2 a01 = c2[0], a23 = c2[1], a45 = c2[2], a67 = c2[3], a89 = c2[4];
     const double t = 2.0 * y100 - (double)(2 * k + 1);
     double h = __builtin_fma(a89.x, t, a67.y);
@@ -304,44 +309,45 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     h = __builtin_fma(h, t, a23.y);
     h = __builtin_fma(h, t, a23.x);
     h = __builtin_fma(h, t, a01.y);
-    const double poly = pin(__builtin_fma(h, t, a01.x));
-    // the Taylor and continued-fraction branches are rare (|x| < ~0.03, |x| > 45): formed only
-    // when some lane of the wave needs them (a wave-uniform branch; NaN takes neither)
+    double w = pin(__builtin_fma(h, t, a01.x));
+    // the Taylor and continued-fraction branches are rare (|x| < ~0.03, |x| > 45; exclusive):
+    // formed, and selected, only when some lane of the wave needs them (a wave-uniform branch;
+    // NaN takes neither)
     const bool use_taylor = y100 >= (double)GGP_DAWSON_NINT, use_cf = ax > 45.0;
-    double taylor = 0.0, cf = 0.0;
     if (__builtin_amdgcn_ballot_w64(use_taylor)) {
         const double x2 = ax * ax;
         const double *tc = ggp_dawson_taylor;
-        taylor = pin(ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4])))));
+        const double taylor = pin(ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4])))));
+        w = use_taylor ? taylor : w;
     }
     if (__builtin_amdgcn_ballot_w64(use_cf)) {
         const bool far = ax > 5e7;
         const double num = far ? GGP_ISPI : pin(GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2));
         const double den = far ? ax : pin(ax * ((ax * ax) * (ax * ax - 5) + 3.75));
-        cf = pin(num / den);
+        const double cf = pin(num / den);
+        w = use_cf ? cf : w;
     }
-    const double w = use_cf ? cf : (use_taylor ? taylor : poly);
     return GGP_SPI2 * (x < 0.0 ? -w : w);
 }
 
-// pow_task without branches (sqrt(a) = two_sa / 2 exactly)
-GGP_DEV double pow_bf(const WStep &S, const int p)
+// The tauint denominators of k = 0..3 (2 sqrt a, then pow_task's 4 a^1.5, 8 a^2.5, 16 a^3.5)
+// and their rdiv seeds (r_two_sa, then 1/(4 a^1.5) = 2 r4a r2sa and each next power one factor
+// 2 r4a = 1/(2a) more: seeds only, rdiv's residual correction makes the quotient independent of
+// a few ulp in them).  Uniform values: lane 0 stores them (no per-lane select).
+GGP_DEV void store_pw(const WStep &S, double *PW)
 {
-    const double sa = S.two_sa * 0.5, a = S.a;
-    const double p0 = pin(4. * (a * sa)), p1 = pin(8. * ((a * a) * sa)), p2 = pin(16. * (((a * a) * a) * sa));
-    return p == 0 ? p0 : p == 1 ? p1 : p2;
-}
-
-// reciprocals of the powers from the step's 1/(4a) and 1/(2 sqrt a): 1/(4 a^1.5) =
-// 2 r4a r2sa, then each next power one factor 2 r4a = 1/(2a) more.  They only seed rdiv
-// (q = x r, then one residual correction against the exact divisor), whose quotient does not
-// depend on a few ulp in r: one division per step less than 1.0 / pow.
-GGP_DEV double rpow_bf(const WStep &S, const int p)
-{
-    const double r0 = pin(2. * (S.r_four_a * S.r_two_sa));
-    const double r1 = pin(2. * (S.r_four_a * r0));
-    const double r2 = pin(2. * (S.r_four_a * r1));
-    return p == 0 ? r0 : p == 1 ? r1 : r2;
+    const double sa = S.two_sa * 0.5, a = S.a;   // sqrt(a) exactly
+    const double r0 = 2. * (S.r_four_a * S.r_two_sa);
+    const double r1 = 2. * (S.r_four_a * r0);
+    const double r2 = 2. * (S.r_four_a * r1);
+    PW[0] = S.two_sa;
+    PW[1] = 4. * (a * sa);
+    PW[2] = 8. * ((a * a) * sa);
+    PW[3] = 16. * (((a * a) * a) * sa);
+    PW[4] = S.r_two_sa;
+    PW[5] = r0;
+    PW[6] = r1;
+    PW[7] = r2;
 }
 
 // tau_unified without branches (X, Dw, PW: the LDS arrays)
@@ -352,8 +358,7 @@ GGP_DEV double tau_bf(const WStep &S, const LaneTasks &L, const double *X, const
     const double E0 = X[T.x0], E1 = X[T.x1];
     const double ec = X[T.xc], ea0 = X[T.xa0], ea1 = X[T.xa1];
     const int k = T.k;
-    const int kk = k == 0 ? 0 : k - 1;
-    const double pd = PW[kk], pr = PW[3 + kk];
+    const double den = PW[k], rden = PW[4 + k];
     const double B = pin(bval(S, L.i_km, L.i_gqks));
     const double t0 = S.t * L.i_tau0, t1 = S.t * L.i_tau1;
     const double BB = pin(B * B);
@@ -365,11 +370,10 @@ GGP_DEV double tau_bf(const WStep &S, const LaneTasks &L, const double *X, const
     const double P0 = al + t0 * (be + ga * t0), P1 = al + t1 * (be + ga * t1);
     const double q1 = pin(B * 2.), q2 = pin((S.two_a - BB) * 2.), q3 = pin(B * (-6. * S.a + BB) * 2.);
     const double Q = k == 0 ? -2.0 : k == 1 ? q1 : k == 2 ? q2 : q3;
-    const double S1 = k == 2 ? S.two_sa : S.m2sa;
+    const double S1 = S.two_sa * L.i_s1;   // 2 sqrt a (k = 2) or -2 sqrt a
     const double dterm = pin(Q * (E0 * D0 - E1 * D1));
     const double xfull = pin(S1 * ec * (ea0 * P0 - ea1 * P1) + dterm);
     const double x = k == 0 ? dterm : xfull;
-    const double den = k == 0 ? S.two_sa : pd, rden = k == 0 ? S.r_two_sa : pr;
     return rdiv(x, den, rden);
 }
 

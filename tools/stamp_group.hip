@@ -52,6 +52,17 @@ int main(int argc, char **argv)
         for (int k = 0; k < ns; ++k)
             printf("  %-22s %8.0f  (%4.1f%%)\n", wave ? wnames[k] : gnames[k], acc[k] / steps, 100.0 * acc[k] / tot);
     }
+    if (kernel == 3) {
+        unsigned long long ps[2][9];
+        (void)hipMemcpyFromSymbol(ps, HIP_SYMBOL(g_pstamp), sizeof ps);
+        const char *pn[8] = {"", "dawson table", "lane tasks+kappa", "cell prologue", "row chunk+barrier",
+                             "first step", "steady steps", "state stores"};
+        for (int s = 0; s < 2; ++s) {
+            if (!ps[s][8]) continue;
+            printf("launch phases, levels %s 1024 cells (%llu blocks), cycles per block:\n", s ? ">" : "<=", ps[s][8]);
+            for (int k = 1; k < 8; ++k) printf("  %-20s %10.0f\n", pn[k], (double)ps[s][k] / ps[s][8]);
+        }
+    }
     ggp_forest_destroy(f);
     ggp_host_forest_free(hf);
     return 0;
