@@ -530,23 +530,18 @@ GGP_DEV void chain_publish(double *st, const double *m, const double *C, unsigne
 }
 
 // In-launch reduction of a path launch (replaces k_reduce_blocks there, with the same sums):
-// the last path of a tree to finish forms the tree sum (DFS order), the last tree of a block
-// the block sum (k_reduce_blocks' 64-wide LDS tree, emulated on the block's <= 8 trees: a path
-// launch has at most as many leaves as the device holds wave blocks, so B <= 8), and the last
-// block copies the block results to the mapped host slots and publishes the call's sequence
-// number.  Counters are agent-scope atomics with a handful of arrivals each (tree: its paths,
-// block: its trees, done: the blocks); the last arrival resets its counter for the next call.
+// the last path of a reduction block to finish forms the block's tree sums (each in DFS order)
+// and its block sum (k_reduce_blocks' 64-wide LDS tree, emulated on the block's <= 8 trees: a
+// path launch has at most as many leaves as the device holds wave blocks, so B <= 8), writes
+// the block result straight to its mapped host slots and counts the block; the last block
+// publishes the call's sequence number.  Counters are agent-scope atomics with few arrivals
+// (a block: its paths; done: the blocks); the last arrival resets its counter for the next call.
 struct ChainRed {
-    const int32_t *path_tree;     // local tree of each path (nullptr: level launches, no reduction)
-    const int32_t *tree_npaths;   // paths per local tree
-    const int32_t *tree_blk;      // local block of each local tree
+    const int32_t *path_blk;      // local block of each path
+    const int32_t *blk_npaths;    // paths per local block
     const int64_t *tree_dfs;      // DFS start of each local tree, then the end
     const int32_t *blk_t0, *blk_nt, *gdfs;
-    unsigned *cnt_tree, *cnt_blk, *done;
-    double *tree_sum;
-    long long *tree_nan;
-    double *out_sum;
-    long long *out_nan;
+    unsigned *cnt_blk, *done;
     int64_t *out_seq;
     double *host_sum;
     long long *host_nan;
@@ -574,58 +569,43 @@ GGP_DEV void st_agent_i(T *p, const T v) { __hip_atomic_store(p, v, __ATOMIC_REL
 GGP_DEV void chain_reduce(const ChainRed &R, const int64_t seq, const int b, const int lane, const double *cell_ll,
                           const int32_t *cell_nan)
 {
-    int last = 0;
-    if (lane == 0) {
-        __builtin_amdgcn_s_waitcnt(0);   // this path's cell results are at the coherence point
-        const int t = R.path_tree[b];
-        if (add_agent(R.cnt_tree + t) + 1 == (unsigned)R.tree_npaths[t]) {
-            zero_agent(R.cnt_tree + t);
-            double v = 0.0;
-            long long code = kChainNoNan;
-            for (int64_t i = R.tree_dfs[t]; i < R.tree_dfs[t + 1]; ++i) {
+    if (lane != 0) return;
+    __builtin_amdgcn_s_waitcnt(0);   // this path's cell results are at the coherence point
+    const int j = R.path_blk[b];
+    if (add_agent(R.cnt_blk + j) + 1 != (unsigned)R.blk_npaths[j]) return;
+    zero_agent(R.cnt_blk + j);
+    const int t0 = R.blk_t0[j], nb = R.blk_nt[j];
+    double sv[8];
+    long long sn[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // tree sums, each in DFS order (k_reduce_blocks' per-thread loop)
+        double v = 0.0;
+        long long code = kChainNoNan;
+        if (k < nb)
+            for (int64_t i = R.tree_dfs[t0 + k]; i < R.tree_dfs[t0 + k + 1]; ++i) {
                 v += ld_agent(cell_ll + i);
                 const int nr = ld_agent_i(cell_nan + i);
                 if (nr != kNanNone && code == kChainNoNan) code = ((long long)R.gdfs[i] << 24) | (long long)nr;
             }
-            st_agent(R.tree_sum + t, v);
-            st_agent_i(R.tree_nan + t, code);
-            __builtin_amdgcn_s_waitcnt(0);
-            const int j = R.tree_blk[t];
-            if (add_agent(R.cnt_blk + j) + 1 == (unsigned)R.blk_nt[j]) {
-                zero_agent(R.cnt_blk + j);
-                const int t0 = R.blk_t0[j], nb = R.blk_nt[j];
-                double sv[8];
-                long long sn[8];
+        sv[k] = v;
+        sn[k] = code;
+    }
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    sv[k] = k < nb ? ld_agent(R.tree_sum + t0 + k) : 0.0;
-                    sn[k] = k < nb ? ld_agent_i(R.tree_nan + t0 + k) : kChainNoNan;
-                }
+    for (int w = 32; w >= 1; w >>= 1)   // k_reduce_blocks' tree over 64 slots; slots >= 8 hold 0
 #pragma unroll
-                for (int w = 32; w >= 1; w >>= 1)   // k_reduce_blocks' tree over 64 slots; slots >= 8 hold 0
-#pragma unroll
-                    for (int k = 0; k < 8 && k < w; ++k) {
-                        sv[k] = sv[k] + (k + w < 8 ? sv[(k + w) & 7] : 0.0);
-                        sn[k] = min(sn[k], k + w < 8 ? sn[(k + w) & 7] : kChainNoNan);
-                    }
-                st_agent(R.out_sum + j, sv[0]);
-                st_agent_i(R.out_nan + j, sn[0]);
-                __builtin_amdgcn_s_waitcnt(0);
-                if (add_agent(R.done) + 1 == (unsigned)R.n_lblocks) {
-                    zero_agent(R.done);
-                    last = 1;
-                }
-            }
+        for (int k = 0; k < 8 && k < w; ++k) {
+            sv[k] = sv[k] + (k + w < 8 ? sv[(k + w) & 7] : 0.0);
+            sn[k] = min(sn[k], k + w < 8 ? sn[(k + w) & 7] : kChainNoNan);
         }
-    }
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
-    // the last block: every block result to the mapped host slots in one burst, then the seq
-    for (int k = lane; k < R.n_lblocks; k += 64) {
-        R.host_sum[k] = ld_agent(R.out_sum + k);
-        R.host_nan[k] = ld_agent_i(R.out_nan + k);
-    }
-    __threadfence_system();
-    if (lane == 0) __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the block result to its mapped host slots (system-coherent stores), complete before the count
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(R.host_sum + j), (unsigned long long)__double_as_longlong(sv[0]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(R.host_nan + j, sn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (add_agent(R.done) + 1 != (unsigned)R.n_lblocks) return;
+    zero_agent(R.done);
+    // every block's slots were written before its count: the sequence number last (the host polls it)
+    __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 GGP_DEV void chain_take(const double *st, double *m, double *C)
@@ -1492,12 +1472,10 @@ struct Shard {
     int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
     int32_t *d_path_cells = nullptr, *d_path_seq = nullptr;   // path launch: cells, [n_paths + 1] starts
     int64_t n_paths = 0;               // 0: level launches
-    // path launch's in-launch reduction (ChainRed): path -> tree, paths per tree, tree -> block,
-    // arrival counters, per-tree partial results
-    int32_t *d_path_tree = nullptr, *d_tree_npaths = nullptr, *d_tree_blk = nullptr;
-    unsigned *d_cnt_tree = nullptr, *d_cnt_blk = nullptr;
-    double *d_tree_sum = nullptr;
-    int64_t *d_tree_nan = nullptr;
+    // path launch's in-launch reduction (ChainRed): path -> block, paths per block, the blocks'
+    // arrival counters
+    int32_t *d_path_blk = nullptr, *d_blk_npaths = nullptr;
+    unsigned *d_cnt_blk = nullptr;
     void *d_red = nullptr;             // the ChainRed of the path launch (device copy)
     std::vector<int32_t> level_kind;   // GGP_KERNEL_* each level runs
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
@@ -1753,9 +1731,8 @@ void shard_destroy(Shard *f)
                     (void *)f->d_state, (void *)f->d_cell_ll, (void *)f->d_cell_nan, (void *)f->d_tree_dfs,
                     (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
                     (void *)f->d_blk_sum, (void *)f->d_blk_nan, (void *)f->d_chain, (void *)f->d_cell_done,
-                    (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_tree,
-                    (void *)f->d_tree_npaths, (void *)f->d_tree_blk, (void *)f->d_cnt_tree, (void *)f->d_cnt_blk,
-                    (void *)f->d_tree_sum, (void *)f->d_tree_nan, f->d_red,
+                    (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_blk,
+                    (void *)f->d_blk_npaths, (void *)f->d_cnt_blk, f->d_red,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -2022,46 +1999,35 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->n_paths = (int64_t)heads.size();
             check(dev_upload(&f->d_path_cells, pcells.data(), pcells.size()));
             check(dev_upload(&f->d_path_seq, pseq.data(), pseq.size()));
-            // reduction tables: the tree of each path (by its first cell's DFS position), paths
-            // per tree, the block of each tree
+            // reduction tables: the block of each path (by its first cell's DFS position and
+            // that tree's block), paths per block
             std::vector<int32_t> rank(nc);
             for (int64_t k = 0; k < nc; ++k) rank[dfs[k]] = (int32_t)k;
             const int64_t ntr = (int64_t)tree_start.size() - 1;
-            std::vector<int32_t> ptree(heads.size()), npaths(std::max<int64_t>(1, ntr), 0), tblk(std::max<int64_t>(1, ntr), 0);
+            std::vector<int32_t> tblk(std::max<int64_t>(1, ntr), 0);
+            for (int64_t j = 0, t = 0; j < (int64_t)blk_ntrees.size(); ++j)
+                for (int32_t u = 0; u < blk_ntrees[j]; ++u, ++t) tblk[t] = (int32_t)j;
+            std::vector<int32_t> pblk(heads.size()), bnp(std::max<size_t>(1, blk_ntrees.size()), 0);
             for (size_t q = 0; q < heads.size(); ++q) {
                 const int64_t k = rank[heads[q]];
                 const int32_t t = (int32_t)(std::upper_bound(tree_start.begin(), tree_start.end(), k) - tree_start.begin() - 1);
-                ptree[q] = t;
-                npaths[t]++;
+                pblk[q] = tblk[t];
+                bnp[tblk[t]]++;
             }
-            for (int64_t j = 0, t = 0; j < (int64_t)blk_ntrees.size(); ++j)
-                for (int32_t u = 0; u < blk_ntrees[j]; ++u, ++t) tblk[t] = (int32_t)j;
-            check(dev_upload(&f->d_path_tree, ptree.data(), ptree.size()));
-            check(dev_upload(&f->d_tree_npaths, npaths.data(), npaths.size()));
-            check(dev_upload(&f->d_tree_blk, tblk.data(), tblk.size()));
-            check(dev_upload<unsigned>(&f->d_cnt_tree, nullptr, npaths.size()));
-            check(dev_upload<unsigned>(&f->d_cnt_blk, nullptr, std::max<size_t>(1, blk_ntrees.size())));
-            check(dev_upload<double>(&f->d_tree_sum, nullptr, npaths.size()));
-            check(dev_upload<int64_t>(&f->d_tree_nan, nullptr, npaths.size()));
-            if (rc == GGP_OK && (hipMemset(f->d_cnt_tree, 0, npaths.size() * sizeof(unsigned)) != hipSuccess ||
-                                 hipMemset(f->d_cnt_blk, 0, std::max<size_t>(1, blk_ntrees.size()) * sizeof(unsigned)) != hipSuccess))
-                rc = GGP_EDEV;
+            check(dev_upload(&f->d_path_blk, pblk.data(), pblk.size()));
+            check(dev_upload(&f->d_blk_npaths, bnp.data(), bnp.size()));
+            check(dev_upload<unsigned>(&f->d_cnt_blk, nullptr, bnp.size()));
+            if (rc == GGP_OK && hipMemset(f->d_cnt_blk, 0, bnp.size() * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
             if (rc == GGP_OK) {
                 ChainRed R{};
-                R.path_tree = f->d_path_tree;
-                R.tree_npaths = f->d_tree_npaths;
-                R.tree_blk = f->d_tree_blk;
+                R.path_blk = f->d_path_blk;
+                R.blk_npaths = f->d_blk_npaths;
                 R.tree_dfs = f->d_tree_dfs;
                 R.blk_t0 = f->d_blk_t0;
                 R.blk_nt = f->d_blk_nt;
                 R.gdfs = f->d_gdfs;
-                R.cnt_tree = f->d_cnt_tree;
                 R.cnt_blk = f->d_cnt_blk;
                 R.done = f->d_done;
-                R.tree_sum = f->d_tree_sum;
-                R.tree_nan = (long long *)f->d_tree_nan;
-                R.out_sum = f->d_blk_sum;
-                R.out_nan = (long long *)f->d_blk_nan;
                 R.out_seq = f->m_seq;
                 R.host_sum = f->m_sum;
                 R.host_nan = (long long *)f->m_nan;
