@@ -510,6 +510,7 @@ GGP_DEV bool wave_flush_ll(const double (*ring_x)[64], const double (*ring_s)[64
 // the lowest unfinished path never waits -- no deadlock, whatever the occupancy.
 // chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c}.
 constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling: a broken chain ends as NaN, not a hang
+constexpr unsigned kChainQuietPerRow = 1100;    // s_memtime units (~0.5 us) of unpolled sleep per parent row
 
 // The state a second daughter takes over crosses XCDs: agent-scope atomic (sc1) stores and
 // loads, coherent without the L2 writeback / invalidate of a release / acquire (a writeback per
@@ -642,7 +643,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const double *p = P.p;
     const ggp::OU ou = W::pin_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
     const W::LaneTasks T = W::lane_tasks(lane, ou);   // this lane's tasks, registers for the launch
-    const double var_x = W::pin(p[7]), var_g = W::pin(p[8]), var_dx = W::pin(p[9]), var_dg = W::pin(p[10]);
+    const double var_x = W::pin(p[7]), var_g = W::pin(p[8]);
+    const double var_dx = p[9], var_dg = p[10];   // first step of a daughter only: not pinned
     double kap[ggp::kOutL];
     ggp::OutTerm tt[ggp::kOutL];
 #pragma unroll
@@ -658,8 +660,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         Vl[ggp::V_ONE] = 1.0;
     }
     // the exp(s t) block in LDS depends on the parameters and dt only: it stays valid from one
-    // cell of this wave to the next
-    double dt_cached = __longlong_as_double(0x7ff8000000000000LL);  // NaN: nothing cached yet
+    // cell of this wave to the next.  dt is wave-uniform: compared by its bits in scalar
+    // registers (a NaN pattern no time difference produces: nothing cached yet)
+    unsigned long long dt_cached = 0x7ff4dead0000beefULL;
     GGP_STAMP_DECL;
     const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
     const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     int64_t prev_last = -1;   // the previous cell's last row (its daughter's division interval)
     for (int i = i_lo; i < i_hi; ++i) {
     int c = 0;
-    int64_t r = 0, r1 = 0, r0 = 0;
+    int64_t r1 = 0, r0 = 0;
     double dt = 0.0, t_cur = 0.0;
     bool pending = false, divide = false;
     const bool valid = true;
@@ -676,7 +679,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     if (valid) {
         c = cells[i];
         ch = chain[c];
-        if (ch.x >= 0) {   // the parent runs in this launch: wait for its state
+        if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            // the parent runs in this launch and is not done: it needs >= ~1.3 us per row, so
+            // sleep through half a microsecond per parent row without polling (each poll is a
+            // memory read past the L2), then poll
+            const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+            const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
+            while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
             unsigned spins = 0;
             while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
                 __builtin_amdgcn_s_sleep(8);
@@ -688,7 +697,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         r0 = F.row_off[c];
         r1 = F.row_off[c + 1];
-        r = r0;
         if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in m, C
             pending = true;
             dt = F.time[r0] - F.time[prev_last];
@@ -724,6 +732,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     double cl = 0.0;
     int nan_row = kNanNone;
     int slot = 0;                                                   // rows in the ll ring = row - chunk base
+    const int nrows = (int)(r1 - r0);
+    int left = nrows;                                               // rows from the current one on
     bool live = valid && !chain_broken;
     if (chain_broken) {
         cl = __longlong_as_double(0x7ff8000000000000LL);
@@ -739,23 +749,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         GGP_STAMP(0);
         GGP_STAMP_STEP();
         const double y_l = row_l[slot], y_f = row_f[slot];
-        const double t_next = r + 1 < r1 ? row_t[slot + 1] : 0.0;
+        const double t_next = left > 1 ? row_t[slot + 1] : 0.0;
         if (!FIRST || pending) {
             const W::WStep S = W::wstep(m, C, dt, ou.b);   // every lane: the same step scalars, in registers
-            if (lane == 0) W::store_v(m, C, dt, ou, Vl);
-            if (__builtin_amdgcn_readfirstlane(dt == dt_cached ? 0 : 1)) {
+            if (lane == 0) {   // stage D's variables and stage C's denominators, one masked region
+                W::store_v(m, C, dt, ou, Vl);
+                W::store_pw(S, Pl);
+            }
+            const long long db = __double_as_longlong(dt);
+            const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
+                                             (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
+            if (dbits != dt_cached) {
                 // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
-                lds[T.xs_dst] = exp(W::sv_of(ou, T.sv) * dt);
+                lds[W::xs_dst_of(lane)] = exp(W::sv_of(ou, lane < 6 ? lane : 0) * dt);
                 __syncthreads();
-                lds[T.dv_dst] = ggp::derived_generic(T.dv, Xl, ou.gl, dt);
+                lds[W::dv_dst_of(lane)] = ggp::derived_generic(W::dv_of(lane), Xl, ou.gl, dt);
                 __syncthreads();
-                dt_cached = dt;
+                dt_cached = dbits;
             }
             GGP_STAMP(1);
-            {   // stage B: one exponential and one Dawson value per lane; lane 0: the denominators
+            {   // stage B: one exponential and one Dawson value per lane
                 const double ev = W::exp_ocml(W::exp_arg(S, T));
                 const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
-                if (lane == 0) W::store_pw(S, Pl);
                 lds[T.x_dst] = ev;
                 lds[T.d_dst] = dv;
                 lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
@@ -819,18 +834,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             ring_s[2][slot] = v.S11;
         }
         ++slot;
-        W::posterior(m, C, x0, x1, v, r + 1 == r1);   // lower triangle only on the cell's last row
-        pending = r + 1 < r1;
+        W::posterior(m, C, x0, x1, v, left == 1);   // lower triangle only on the cell's last row
+        pending = left > 1;
         if (pending) dt = t_next - t_cur;
         t_cur = t_next;
-        ++r;
-        live = r < r1;
+        --left;
+        live = left > 0;
         GGP_STAMP(9);
         if (slot == 64 || !live) {
-            if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, r - slot - r0, F.two_log_2pi, lane, cl, nan_row))
+            const int done = nrows - left;
+            if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, done - slot, F.two_log_2pi, lane, cl, nan_row))
                 return false;
             slot = 0;
-            if (live) load_chunk(r);
+            if (live) load_chunk(r0 + done);
         }
         GGP_STAMP(10);
         __syncthreads();   // LDS slots are rewritten by the next step

@@ -142,8 +142,6 @@ struct LaneTasks {
     ITask it;
     double i_tau0, i_tau1, i_km, i_gqks, i_s1;
     int i_dst;
-    int sv, xs_dst, dv_dst;
-    DTaskB dv;
     int out_dst;
 };
 
@@ -199,10 +197,6 @@ GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
     L.i_km = kKm[L.it.iB];
     L.i_gqks = P.gq * kKs[L.it.iB];
     L.i_dst = lane < NI ? L_BV + BV_I + lane : L_DUMMY + lane;
-    L.sv = lane < 6 ? lane : 0;
-    L.xs_dst = lane < 6 ? L_X + XS_bt + lane : L_DUMMY + lane;
-    L.dv = kDerived[lane < kNDerived ? lane : 0];
-    L.dv_dst = lane < kNDerived ? L_BV + BV_R_EBT + lane : L_DUMMY + lane;
     // the lead lane of output k's block stores the block sum
     int out = L_DUMMY + lane;
 #pragma unroll
@@ -210,6 +204,12 @@ GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
     L.out_dst = out;
     return L;
 }
+
+// The per-dt block (exp(s t) and the exp-derived basis of the outputs, formed when dt changes):
+// its lane tasks are formed there from the lane number, not kept in registers for the launch
+GGP_DEV int xs_dst_of(const int lane) { return lane < 6 ? L_X + XS_bt + lane : L_DUMMY + lane; }
+GGP_DEV int dv_dst_of(const int lane) { return lane < kNDerived ? L_BV + BV_R_EBT + lane : L_DUMMY + lane; }
+GGP_DEV DTaskB dv_of(const int lane) { return kDerived[lane < kNDerived ? lane : 0]; }
 
 // the exponents s of exp(s t) (pickSV, ggp_prop.h)
 GGP_DEV double sv_of(const OU &P, const int s)

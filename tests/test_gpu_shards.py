@@ -168,3 +168,32 @@ def test_cli_outputs_identical_for_any_device_list(tmp_path, example_paths):
         assert sorted(n for n in os.listdir(runs[tag]) if not n.endswith(".log")) == names
         for n in names:
             assert filecmp.cmp(runs["one"] / n, runs[tag] / n, shallow=False), (tag, n)
+
+
+def test_path_launch_bitwise_equal_to_level_launches(monkeypatch):
+    """the path launch (one launch per evaluation, in-launch reduction) against
+    level launches + k_reduce_blocks (GGP_WAVE_PATHS_MAX=0 at handle creation): the same bits
+    for the chain, the carried state, the NaN location and batch points"""
+    import gfp_gaussian_process_amd as g
+    hf = _forest(200, 60)
+    paths = g.Forest(hf, kernel="wave")
+    monkeypatch.setenv("GGP_WAVE_PATHS_MAX", "0")
+    levels = g.Forest(hf, kernel="wave")
+    monkeypatch.delenv("GGP_WAVE_PATHS_MAX")
+    P = list(INIT)
+    for call in range(3):
+        assert paths.total_likelihood(P) == levels.total_likelihood(P), call
+    assert np.array_equal(paths.state(), levels.state())
+    paths.enable_profile()
+    levels.enable_profile()
+    paths.total_likelihood(P)
+    levels.total_likelihood(P)
+    assert len(paths.launch_profile()[0]) == 1 and len(levels.launch_profile()[0]) >= 2
+    bad = list(INIT)
+    bad[2] = -1.0
+    got = []
+    for f in (paths, levels):
+        with pytest.raises(g.LikelihoodIsNan) as e:
+            f.total_likelihood(bad)
+        got.append((e.value.cell, e.value.row))
+    assert got[0] == got[1]
