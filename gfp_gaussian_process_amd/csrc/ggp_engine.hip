@@ -430,19 +430,21 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 
 // ------------------------------------------------------------------------------------------
 // WAVE schedule: one 64-lane wave per cell, every stage of a step spread over the lanes
-// (ggp_wave.h): one exponential, one Dawson value and one power per lane, then one integral
-// per lane, then the outputs as the sparse trilinear form of ggp_outtab.h (59 lanes x 4
-// terms, summed by a DPP butterfly inside power-of-two lane blocks and broadcast through
-// LDS); the Kalman update runs redundantly in all lanes (the state stays in registers).
+// (ggp_wave.h): one exponential and one Dawson value per lane (lane 0: the tauint
+// denominators), then one integral per lane, then the outputs as the sparse trilinear form of
+// ggp_outtab.h (59 lanes x 4 terms, summed by a DPP butterfly inside power-of-two lane blocks
+// and broadcast through LDS); the Kalman update runs redundantly in all lanes (the state stays
+// in registers).  A step costs about its instruction count (one per ~4 shader cycles per
+// wave), so every stage is kept to the fewest instructions.
 // Every stage is straight-line code (ggp_wave.h says why).  What depends on the parameters
 // and dt only -- exp(s t) and the 18 exp-derived basis values of the outputs -- is formed
 // when dt changes and kept in LDS.  The determinant and log of the ll term are off the
-// critical path: q and S go to an LDS ring, and every 64 rows (or at the cell's end) 64
-// lanes take the determinants and logs at once and one lane adds the terms in row order
-// (the reference's summation order; the first NaN row is found there).
-// The outputs are the same polynomial as ggp::outputs summed in another order, and four
-// exp(c) are products of exponentials, so results agree with the lane/group schedules to
-// ~1e-10 relative on the total, not bitwise (DESIGN.md "Parity").
+// critical path: x and S go to an LDS ring, and every 64 rows (or at the cell's end) 64
+// lanes take the quadratic forms, determinants and logs at once and one lane adds the terms in
+// row order (the reference's summation order; the first NaN row is found there).
+// The outputs are the same polynomial as ggp::outputs summed in another order, four exp(c)
+// are products of exponentials, and the update uses fused multiply-adds, so results agree with
+// the lane/group schedules to ~1e-10 relative on the total, not bitwise (DESIGN.md "Parity").
 // ------------------------------------------------------------------------------------------
 template <int CTRL>
 GGP_DEV double dpp_f64(const double v)
@@ -669,212 +671,211 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
     int64_t prev_last = -1;   // the previous cell's last row (its daughter's division interval)
     for (int i = i_lo; i < i_hi; ++i) {
-    int c = 0;
-    int64_t r1 = 0, r0 = 0;
-    double dt = 0.0, t_cur = 0.0;
-    bool pending = false, divide = false;
-    const bool valid = true;
-    int2 ch = {-1, 0};
-    bool chain_broken = false;
-    if (valid) {
-        c = cells[i];
-        ch = chain[c];
-        if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            // the parent runs in this launch and is not done: it needs >= ~1.3 us per row, so
-            // sleep through half a microsecond per parent row without polling (each poll is a
-            // memory read past the L2), then poll
-            const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-            const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
-            while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
-            unsigned spins = 0;
-            while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-                __builtin_amdgcn_s_sleep(8);
-                if (++spins > kChainSpinMax) {
-                    chain_broken = true;
-                    break;
+        int c = 0;
+        int64_t r1 = 0, r0 = 0;
+        double dt = 0.0, t_cur = 0.0;
+        bool pending = false, divide = false;
+        int2 ch = {-1, 0};
+        bool chain_broken = false;
+        {
+            c = cells[i];
+            ch = chain[c];
+            if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                // the parent runs in this launch and is not done: it needs >= ~1.3 us per row, so
+                // sleep through half a microsecond per parent row without polling (each poll is a
+                // memory read past the L2), then poll
+                const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+                const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
+                while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
+                unsigned spins = 0;
+                while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                    __builtin_amdgcn_s_sleep(8);
+                    if (++spins > kChainSpinMax) {
+                        chain_broken = true;
+                        break;
+                    }
                 }
             }
-        }
-        r0 = F.row_off[c];
-        r1 = F.row_off[c + 1];
-        if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in m, C
-            pending = true;
-            dt = F.time[r0] - F.time[prev_last];
-        } else if (ch.x >= 0) {   // a second daughter of a cell in another path
-            chain_take(state + (size_t)20 * ch.x, m, C);
-            pending = true;
-            dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
-        } else {
-            pending = cell_prologue(F, p, state, c, r0, m, C, dt);
-        }
-        divide = pending;
-        t_cur = F.time[r0];
-        prev_last = r1 - 1;
-    }
-    GGP_PSTAMP(3);
-    // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane), so
-    // the step loop issues no global loads and never waits on one
-    auto load_chunk = [&](const int64_t base) {
-        const int64_t rr = base + lane;
-        double a = 0.0, b = 0.0, t = 0.0;
-        if (rr < r1) {
-            a = F.logl[rr];
-            b = F.fp[rr];
-            t = F.time[rr];
-        }
-        row_l[lane] = a;
-        row_f[lane] = b;
-        row_t[lane] = t;
-        if (lane == 0) row_t[64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
-    };
-    if (valid) load_chunk(r0);
-    __syncthreads();
-    double cl = 0.0;
-    int nan_row = kNanNone;
-    int slot = 0;                                                   // rows in the ll ring = row - chunk base
-    const int nrows = (int)(r1 - r0);
-    int left = nrows;                                               // rows from the current one on
-    bool live = valid && !chain_broken;
-    if (chain_broken) {
-        cl = __longlong_as_double(0x7ff8000000000000LL);
-        nan_row = 0;
-    }
-    // One step (one row).  The first step of the cell is peeled (FIRST): only it can skip the
-    // propagation (a root's first row) or apply the division map (a daughter's), so the steady
-    // loop has neither branch -- nor the register copies the compiler put at their joins.
-    // Every later step propagates: the loop continues only while rows remain.  false = stop
-    // (a NaN term; nan_row set).
-    auto step = [&](auto first) -> bool {
-        constexpr bool FIRST = decltype(first)::value;
-        GGP_STAMP(0);
-        GGP_STAMP_STEP();
-        const double y_l = row_l[slot], y_f = row_f[slot];
-        const double t_next = left > 1 ? row_t[slot + 1] : 0.0;
-        if (!FIRST || pending) {
-            const W::WStep S = W::wstep(m, C, dt, ou.b);   // every lane: the same step scalars, in registers
-            if (lane == 0) {   // stage D's variables and stage C's denominators, one masked region
-                W::store_v(m, C, dt, ou, Vl);
-                W::store_pw(S, Pl);
+            r0 = F.row_off[c];
+            r1 = F.row_off[c + 1];
+            if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in m, C
+                pending = true;
+                dt = F.time[r0] - F.time[prev_last];
+            } else if (ch.x >= 0) {   // a second daughter of a cell in another path
+                chain_take(state + (size_t)20 * ch.x, m, C);
+                pending = true;
+                dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
+            } else {
+                pending = cell_prologue(F, p, state, c, r0, m, C, dt);
             }
-            const long long db = __double_as_longlong(dt);
-            const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
-                                             (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
-            if (dbits != dt_cached) {
-                // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
-                lds[W::xs_dst_of(lane)] = exp(W::sv_of(ou, lane < 6 ? lane : 0) * dt);
+            divide = pending;
+            t_cur = F.time[r0];
+            prev_last = r1 - 1;
+        }
+        GGP_PSTAMP(3);
+        // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane), so
+        // the step loop issues no global loads and never waits on one
+        auto load_chunk = [&](const int64_t base) {
+            const int64_t rr = base + lane;
+            double a = 0.0, b = 0.0, t = 0.0;
+            if (rr < r1) {
+                a = F.logl[rr];
+                b = F.fp[rr];
+                t = F.time[rr];
+            }
+            row_l[lane] = a;
+            row_f[lane] = b;
+            row_t[lane] = t;
+            if (lane == 0) row_t[64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
+        };
+        load_chunk(r0);
+        __syncthreads();
+        double cl = 0.0;
+        int nan_row = kNanNone;
+        int slot = 0;                                                   // rows in the ll ring = row - chunk base
+        const int nrows = (int)(r1 - r0);
+        int left = nrows;                                               // rows from the current one on
+        bool live = !chain_broken;
+        if (chain_broken) {
+            cl = __longlong_as_double(0x7ff8000000000000LL);
+            nan_row = 0;
+        }
+        // One step (one row).  The first step of the cell is peeled (FIRST): only it can skip the
+        // propagation (a root's first row) or apply the division map (a daughter's), so the steady
+        // loop has neither branch -- nor the register copies the compiler put at their joins.
+        // Every later step propagates: the loop continues only while rows remain.  false = stop
+        // (a NaN term; nan_row set).
+        auto step = [&](auto first) -> bool {
+            constexpr bool FIRST = decltype(first)::value;
+            GGP_STAMP(0);
+            GGP_STAMP_STEP();
+            const double y_l = row_l[slot], y_f = row_f[slot];
+            const double t_next = left > 1 ? row_t[slot + 1] : 0.0;
+            if (!FIRST || pending) {
+                const W::WStep S = W::wstep(m, C, dt, ou.b);   // every lane: the same step scalars, in registers
+                if (lane == 0) {   // stage D's variables and stage C's denominators, one masked region
+                    W::store_v(m, C, dt, ou, Vl);
+                    W::store_pw(S, Pl);
+                }
+                const long long db = __double_as_longlong(dt);
+                const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
+                                                 (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
+                if (dbits != dt_cached) {
+                    // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
+                    lds[W::xs_dst_of(lane)] = exp(W::sv_of(ou, lane < 6 ? lane : 0) * dt);
+                    __syncthreads();
+                    lds[W::dv_dst_of(lane)] = ggp::derived_generic(W::dv_of(lane), Xl, ou.gl, dt);
+                    __syncthreads();
+                    dt_cached = dbits;
+                }
+                GGP_STAMP(1);
+                {   // stage B: one exponential and one Dawson value per lane
+                    const double ev = W::exp_ocml(W::exp_arg(S, T));
+                    const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
+                    lds[T.x_dst] = ev;
+                    lds[T.d_dst] = dv;
+                    lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
+                }
+                GGP_STAMP(2);
                 __syncthreads();
-                lds[W::dv_dst_of(lane)] = ggp::derived_generic(W::dv_of(lane), Xl, ou.gl, dt);
+                GGP_STAMP(3);
+                // stage D's state monomials kappa V1 V2 V3 need no stage-C value: their 12 LDS reads
+                // are issued here, beside stage C, and the products formed after it
+                double vv[ggp::kOutL][3];
+#pragma unroll
+                for (int q = 0; q < ggp::kOutL; ++q) {
+                    vv[q][0] = Vl[tt[q].v1];
+                    vv[q][1] = Vl[tt[q].v2];
+                    vv[q][2] = Vl[tt[q].v3];
+                }
+                lds[T.i_dst] = W::tau_bf(S, T, Xl, Dl, Pl);   // stage C: one integral per lane
+                double kv[ggp::kOutL];
+#pragma unroll
+                for (int q = 0; q < ggp::kOutL; ++q) kv[q] = ((kap[q] * vv[q][0]) * vv[q][1]) * vv[q][2];
+                GGP_STAMP(4);
                 __syncthreads();
-                dt_cached = dbits;
+                GGP_STAMP(5);
+                double bv[ggp::kOutL];   // stage D: this lane's output terms; the four reads issue together
+#pragma unroll
+                for (int q = 0; q < ggp::kOutL; ++q) bv[q] = Bv[tt[q].basis];
+                asm volatile("" ::"v"(bv[0]), "v"(bv[1]), "v"(bv[2]), "v"(bv[3]));
+                static_assert(ggp::kOutL == 4, "stage D issues kOutL reads together");
+                double acc = kv[0] * bv[0];   // the lane's terms, fused (the table's sums, not bitwise ggp::outputs)
+#pragma unroll
+                for (int q = 1; q < ggp::kOutL; ++q) acc = __builtin_fma(kv[q], bv[q], acc);
+                GGP_STAMP(6);
+                {   // block sums: DPP butterfly (ggp::out_partner)
+                    double w;
+                    w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
+                    w = dpp_f64<0x4E>(acc);  acc = bs > 2 ? acc + w : acc;
+                    w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
+                    w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
+                }
+                lds[T.out_dst] = acc;   // block sums to LDS, read back by every lane
+                GGP_STAMP(7);
+                __syncthreads();
+                double o[ggp::kOutN];
+#pragma unroll
+                for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
+#pragma unroll
+                for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j, one rounding
+                    if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
+                ggp::out_store(o, m, C);
+                if (FIRST && divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
+                GGP_STAMP(8);
             }
-            GGP_STAMP(1);
-            {   // stage B: one exponential and one Dawson value per lane
-                const double ev = W::exp_ocml(W::exp_arg(S, T));
-                const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
-                lds[T.x_dst] = ev;
-                lds[T.d_dst] = dv;
-                lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
+            const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
+            if (lane == 0) {   // the ll term's inputs into the ring (its q, det and log at the flush)
+                ring_x[0][slot] = x0;
+                ring_x[1][slot] = x1;
+                ring_s[0][slot] = v.S00;
+                ring_s[1][slot] = v.S01;
+                ring_s[2][slot] = v.S11;
             }
-            GGP_STAMP(2);
-            __syncthreads();
-            GGP_STAMP(3);
-            // stage D's state monomials kappa V1 V2 V3 need no stage-C value: their 12 LDS reads
-            // are issued here, beside stage C, and the products formed after it
-            double vv[ggp::kOutL][3];
-#pragma unroll
-            for (int q = 0; q < ggp::kOutL; ++q) {
-                vv[q][0] = Vl[tt[q].v1];
-                vv[q][1] = Vl[tt[q].v2];
-                vv[q][2] = Vl[tt[q].v3];
+            ++slot;
+            W::posterior(m, C, x0, x1, v, left == 1);   // lower triangle only on the cell's last row
+            pending = left > 1;
+            if (pending) dt = t_next - t_cur;
+            t_cur = t_next;
+            --left;
+            live = left > 0;
+            GGP_STAMP(9);
+            if (slot == 64 || !live) {
+                const int done = nrows - left;
+                if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, done - slot, F.two_log_2pi, lane, cl, nan_row))
+                    return false;
+                slot = 0;
+                if (live) load_chunk(r0 + done);
             }
-            lds[T.i_dst] = W::tau_bf(S, T, Xl, Dl, Pl);   // stage C: one integral per lane
-            double kv[ggp::kOutL];
-#pragma unroll
-            for (int q = 0; q < ggp::kOutL; ++q) kv[q] = ((kap[q] * vv[q][0]) * vv[q][1]) * vv[q][2];
-            GGP_STAMP(4);
-            __syncthreads();
-            GGP_STAMP(5);
-            double bv[ggp::kOutL];   // stage D: this lane's output terms; the four reads issue together
-#pragma unroll
-            for (int q = 0; q < ggp::kOutL; ++q) bv[q] = Bv[tt[q].basis];
-            asm volatile("" ::"v"(bv[0]), "v"(bv[1]), "v"(bv[2]), "v"(bv[3]));
-            static_assert(ggp::kOutL == 4, "stage D issues kOutL reads together");
-            double acc = kv[0] * bv[0];   // the lane's terms, fused (the table's sums, not bitwise ggp::outputs)
-#pragma unroll
-            for (int q = 1; q < ggp::kOutL; ++q) acc = __builtin_fma(kv[q], bv[q], acc);
-            GGP_STAMP(6);
-            {   // block sums: DPP butterfly (ggp::out_partner)
-                double w;
-                w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
-                w = dpp_f64<0x4E>(acc);  acc = bs > 2 ? acc + w : acc;
-                w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
-                w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
+            GGP_STAMP(10);
+            __syncthreads();   // LDS slots are rewritten by the next step
+            GGP_STAMP(11);
+            return true;
+        };
+        GGP_PSTAMP(4);
+        const bool more = live && step(std::true_type{});
+        GGP_PSTAMP(5);
+        if (more)
+            while (live && step(std::false_type{})) {
             }
-            lds[T.out_dst] = acc;   // block sums to LDS, read back by every lane
-            GGP_STAMP(7);
-            __syncthreads();
-            double o[ggp::kOutN];
+        GGP_PSTAMP(6);
+        if (lane == 0) {
+            double *st = state + (size_t)20 * c;
+            st_agent(cell_ll + F.dfs_rank[c], cl);          // coherent: a path launch sums them in-launch
+            st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
+            if (ch.y) {
+                chain_publish(st, m, C, cell_done + c, epoch);   // for the second daughter
+            } else {
 #pragma unroll
-            for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
+                for (int k = 0; k < 4; ++k) st[k] = m[k];
 #pragma unroll
-            for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j, one rounding
-                if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
-            ggp::out_store(o, m, C);
-            if (FIRST && divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
-            GGP_STAMP(8);
+                for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+            }
         }
-        const double x0 = y_l - m[0];
-        const double x1 = y_f - m[1];
-        const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
-        if (lane == 0) {   // the ll term's inputs into the ring (its q, det and log at the flush)
-            ring_x[0][slot] = x0;
-            ring_x[1][slot] = x1;
-            ring_s[0][slot] = v.S00;
-            ring_s[1][slot] = v.S01;
-            ring_s[2][slot] = v.S11;
-        }
-        ++slot;
-        W::posterior(m, C, x0, x1, v, left == 1);   // lower triangle only on the cell's last row
-        pending = left > 1;
-        if (pending) dt = t_next - t_cur;
-        t_cur = t_next;
-        --left;
-        live = left > 0;
-        GGP_STAMP(9);
-        if (slot == 64 || !live) {
-            const int done = nrows - left;
-            if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, done - slot, F.two_log_2pi, lane, cl, nan_row))
-                return false;
-            slot = 0;
-            if (live) load_chunk(r0 + done);
-        }
-        GGP_STAMP(10);
-        __syncthreads();   // LDS slots are rewritten by the next step
-        GGP_STAMP(11);
-        return true;
-    };
-    GGP_PSTAMP(4);
-    const bool more = live && step(std::true_type{});
-    GGP_PSTAMP(5);
-    if (more)
-        while (live && step(std::false_type{})) {
-        }
-    GGP_PSTAMP(6);
-    if (valid && lane == 0) {
-        double *st = state + (size_t)20 * c;
-        st_agent(cell_ll + F.dfs_rank[c], cl);          // coherent: a path launch sums them in-launch
-        st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
-        if (ch.y) {
-            chain_publish(st, m, C, cell_done + c, epoch);   // for the second daughter
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) st[k] = m[k];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-        }
-    }
-    GGP_PSTAMP(7);
-    __syncthreads();   // the LDS rows and ring are the next cell's
+        GGP_PSTAMP(7);
+        __syncthreads();   // the LDS rows and ring are the next cell's
     }
     GGP_STAMP_FLUSH();
     GGP_PSTAMP_FLUSH();

@@ -102,6 +102,12 @@ typedef struct {
 #define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
 #define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);
                                  agrees with LANE/GROUP to ~1e-10, not bitwise        */
+/* Launch form (per shard, fixed at creation): when every level takes the wave schedule and the
+ * shard has at most as many leaves as the device holds wave blocks, an evaluation is ONE launch
+ * (a block per root-to-leaf path, the sum formed in-launch); otherwise one launch per level plus
+ * a reduction.  Both give the same bits.  Environment (read at creation, tuning only):
+ * GGP_WAVE_PATHS_MAX (paths allowed in one launch; 0 = always level launches),
+ * GGP_WAVE_MAX_CELLS / GGP_GROUP_MAX_CELLS (auto's thresholds), GGP_AUTO_SMALL=group. */
 
 int ggp_forest_create(const ggp_forest_desc *desc, ggp_forest **out);
 void ggp_forest_destroy(ggp_forest *f);
