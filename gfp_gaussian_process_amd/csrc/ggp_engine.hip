@@ -253,6 +253,14 @@ __device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], 
             atomicAdd(&g_stamp[o_ + 15], (unsigned long long)st_steps);                    \
         }                                                                                  \
     } while (0)
+#elif defined(GGP_MARKS)   // assembly comments at the stamp points (tools/isa_segments.py)
+#define GGP_STAMP_DECL
+#define GGP_STAMP(k) asm volatile(";@mark " #k)
+#define GGP_STAMP_STEP()
+#define GGP_STAMP_FLUSH()
+#define GGP_PSTAMP_DECL
+#define GGP_PSTAMP(k) asm volatile(";@pmark " #k)
+#define GGP_PSTAMP_FLUSH()
 #else
 #define GGP_STAMP_DECL
 #define GGP_STAMP(k)

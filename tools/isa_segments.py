@@ -1,5 +1,7 @@
 """Static instruction mix between s_memtime stamps of a kernel in a GGP_STAMPS assembly
-listing (diagnostic): python tools/isa_segments.py file.s kernel_symbol_substring"""
+listing (diagnostic): python tools/isa_segments.py file.s kernel_symbol_substring.
+A -DGGP_MARKS listing puts ";@mark k" comments at the same points without stamps (the
+shipped schedule, approximately: nothing pins instructions to the marks)."""
 import sys
 from collections import Counter
 
