@@ -778,8 +778,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 }
                 GGP_STAMP(1);
                 {   // stage B: one exponential and one Dawson value per lane
-                    const double ev = W::exp_ocml(W::exp_arg(S, T));
+                    const double xa = W::exp_arg(S, T);
+                    double ev = ggp::exp_ocml(xa);
                     const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
+                    if (__builtin_amdgcn_ballot_w64(!(fabs(xa) < ggp::kExpFastMax)))   // ocml's exp beyond 2^50 (rare)
+                        ev = fabs(xa) < ggp::kExpFastMax ? ev : exp(xa);
                     lds[T.x_dst] = ev;
                     lds[T.d_dst] = dv;
                     lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];

@@ -28,6 +28,46 @@ GGP_DEV double rdiv(double x, double d, double r)
     return __builtin_fma(e, r, q);
 }
 
+// exp(x) exactly as ocml's __ocml_exp_f64 computes it (the same constants, fma chain and
+// ldexp; bitwise the same value), with every Horner step one VOP3 v_fma_f64: the compiler's own
+// form is a v_mov_b64 of the loop-invariant coefficient plus a tied v_fmac_f64 per step
+GGP_DEV double fma3(const double a, const double b, const double c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
+
+GGP_DEV double exp_ocml(const double x)
+{
+    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
+    double t = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, x);
+    t = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, t);
+    double p = fma3(t, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+    p = fma3(t, p, 0x1.71dee623fde64p-19);
+    p = fma3(t, p, 0x1.a01997c89e6b0p-16);
+    p = fma3(t, p, 0x1.a01a014761f6ep-13);
+    p = fma3(t, p, 0x1.6c16c1852b7b0p-10);
+    p = fma3(t, p, 0x1.1111111122322p-7);
+    p = fma3(t, p, 0x1.55555555502a1p-5);
+    p = fma3(t, p, 0x1.5555555555511p-3);
+    p = fma3(t, p, 0x1.000000000000bp-1);
+    p = __builtin_fma(t, p, 1.0);
+    p = __builtin_fma(t, p, 1.0);
+    // ocml's range checks (x > 1024 -> inf, x < -1075 -> 0) are left out.  For |x| < 2^50,
+    // dn = rint(x log2 e) is within 0.7 of x log2 e, so |t| < 0.6 and p is finite: v_ldexp_f64
+    // then overflows to inf / underflows to 0 exactly where ocml's checks would (the int
+    // conversion saturates), and the value is ocml's bitwise.  Beyond 2^50 (+-inf included) t
+    // is not reduced and the value is not ocml's: callers bound |x| (kExpFastMax)
+    return __builtin_ldexp(p, (int)dn);
+}
+
+constexpr double kExpFastMax = 0x1p50;   // exp_ocml is ocml's exp for |x| below this
+
 // 1/d for finite nonzero d as v_rcp_f64 and two Newton steps (5 instructions against the ~11 of
 // the IEEE sequence).  Used where the value only seeds rdiv, whose residual correction makes
 // the quotient independent of an ulp in the seed.  d = 0 or inf gives NaN (IEEE: inf, 0);
@@ -361,7 +401,7 @@ GGP_DEV double zval(const ST &S, int iB, int it)
 }
 
 template <class ST>
-GGP_DEV double exp_body(const ST &S, const XTask T)
+GGP_DEV double exp_arg_body(const ST &S, const XTask T)
 {
     // branch-free: every candidate argument is formed from selected operands and the kind
     // picks one, so lanes holding different kinds do not serialise (group schedule)
@@ -376,10 +416,12 @@ GGP_DEV double exp_body(const ST &S, const XTask T)
     const double argS = sv * S.t;
     const double argE = n + c + z * z;
     const double argZ = S.a * (ti * ti) + B * ti + c;
-    const double arg = T.kind == KX_C ? c : T.kind == KX_A ? argA : T.kind == KX_S ? argS
-                     : T.kind == KX_E ? argE : argZ;
-    return exp(arg);
+    return T.kind == KX_C ? c : T.kind == KX_A ? argA : T.kind == KX_S ? argS
+         : T.kind == KX_E ? argE : argZ;
 }
+
+template <class ST>
+GGP_DEV double exp_body(const ST &S, const XTask T) { return exp(exp_arg_body(S, T)); }
 
 GGP_DEV double exp_task(const Step &S, int j) { return exp_body(S, kXT[j]); }
 

@@ -244,41 +244,7 @@ GGP_DEV double dawson_arg(const WStep &S, const LaneTasks &T)
     return rdiv(B + S.two_a * (S.t * T.d_tau), S.two_sa, S.r_two_sa);
 }
 
-// exp(x) exactly as ocml's __ocml_exp_f64 computes it (the same constants, fma chain and
-// ldexp; bitwise the same value), with every Horner step one VOP3 v_fma_f64: the compiler's own
-// form is a v_mov_b64 of the loop-invariant coefficient plus a tied v_fmac_f64 per step
-GGP_DEV double fma3(const double a, const double b, const double c)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-#else
-    return __builtin_fma(a, b, c);
-#endif
-}
-
-GGP_DEV double exp_ocml(const double x)
-{
-    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
-    double t = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, x);
-    t = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, t);
-    double p = fma3(t, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
-    p = fma3(t, p, 0x1.71dee623fde64p-19);
-    p = fma3(t, p, 0x1.a01997c89e6b0p-16);
-    p = fma3(t, p, 0x1.a01a014761f6ep-13);
-    p = fma3(t, p, 0x1.6c16c1852b7b0p-10);
-    p = fma3(t, p, 0x1.1111111122322p-7);
-    p = fma3(t, p, 0x1.55555555502a1p-5);
-    p = fma3(t, p, 0x1.5555555555511p-3);
-    p = fma3(t, p, 0x1.000000000000bp-1);
-    p = __builtin_fma(t, p, 1.0);
-    p = __builtin_fma(t, p, 1.0);
-    // ocml's range checks (x > 1024 -> inf, x < -1075 -> 0) are left out: v_ldexp_f64 already
-    // overflows to inf and underflows to 0 for every finite x that far out (the int conversion
-    // saturates); only x = +-inf (a non-finite state) gives NaN here instead of inf / 0
-    return __builtin_ldexp(p, (int)dn);
-}
+// exp_ocml: ggp_prop.h (shared with the lane schedule)
 
 // ggp_dawson_tab without branches: one division for the continued fraction, a NaN falls
 // through the polynomial (same values as ggp_dawson_tab).  tab: rows of kDawsonRow doubles
