@@ -130,6 +130,11 @@ def main() -> int:
                     help="also time the -p smoother on a C5-shard forest: trees per GPU (0 = skip)")
     ap.add_argument("--hessian", type=int, default=1, help="also time the batched 11-parameter Hessian (0 = skip)")
     ap.add_argument("--predict-rows", type=int, default=500, help="rows per tree of the -p forest")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo: rehearsal of the "
+                         "multi-rank path on one GPU, the per-call 16 B through host memory)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="HIP ordinal of this rank (default LOCAL_RANK; rehearsal: several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -142,9 +147,16 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.device is not None:
+        local = args.device
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    # the max-over-ranks of the timings: device tensors for RCCL, host tensors for gloo
+    red_dev = "cuda" if args.backend == "nccl" else "cpu"
 
     # ---- this rank's forest (weak scaling), resident on the GPU before timing ----
     hf = g.HostForest.synthetic(args.trees, args.rows, seed=SEED, first_tree=rank * args.trees)
@@ -168,7 +180,7 @@ def main() -> int:
     barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_rows = rows_rank * world * args.steps
@@ -267,7 +279,7 @@ def main() -> int:
         barrier()
         pel = (time.perf_counter() - t1) / reps
         if world > 1:
-            t = torch.tensor([pel], dtype=torch.float64, device="cuda")
+            t = torch.tensor([pel], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             pel = float(t.item())
         nr = hp.n_rows
@@ -300,7 +312,8 @@ def main() -> int:
                             f"(root {args.rows // 2} + 2 x {args.rows // 4} rows), single total-log-likelihood "
                             "evaluation per step, scaled noise + binomial division, example parameters",
                 "trees_per_gpu": args.trees, "rows_per_gpu": rows_rank, "levels": info["levels"],
-                "kernel": args.kernel, "parallelism": f"forest sharded by whole trees, {world} rank(s)",
+                "kernel": args.kernel, "parallelism": f"forest sharded by whole trees, {world} rank(s)"
+                                                      + ("" if world == 1 else f", {args.backend}"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -1,0 +1,120 @@
+"""Multi-rank runs of the HIP engine on the one-GPU box: several processes, one group.
+
+The driver's scaling run launches bench.py with one rank per GPU over RCCL (nccl).  A GPU
+box here has one card, and RCCL does not put two ranks on one device, so these tests
+rehearse the same code with the gloo backend and every rank on cuda:0:
+  - bench.py under torch.distributed.run with 2 ranks: the JSON line's whole-job value,
+    n_gpus and the gathered total (bitwise the rank-order sum of single-process evaluations);
+  - ShardedObjective over whole-tree shards of ONE forest (distributed.shard), each rank's
+    partial from the HIP engine: the sum against the whole forest and the oracle, and a NaN
+    on one rank raised on every rank.
+"""
+import json
+import math
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P0 = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_gloo_rehearsal():
+    """bench.py --gpus 2 as the driver launches it (torch.distributed.run, one process per
+    rank), gloo and both ranks on cuda:0"""
+    import gfp_gaussian_process_amd as g
+    sys.path.insert(0, ROOT)
+    import bench
+    trees, rows, steps, warm = 200, 200, 20, 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", str(warm),
+           "--trees", str(trees), "--rows", str(rows), "--no-cpu", "--large-trees", "0", "--predict-trees", "0",
+           "--hessian", "0", "--backend", "gloo", "--device", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]      # rank 0 prints ONE line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == steps and out["warmup"] == warm
+    assert out["config"]["rows_per_gpu"] == trees * rows
+    # whole-job value: rows of both ranks over the max-over-ranks time of the K steps
+    assert out["value"] == pytest.approx(2 * trees * rows / (out["ms_per_step"] * 1e-3), rel=1e-9)
+    # the gathered total after W + K chained calls: the rank-order sum of each rank's own chain
+    want = 0.0
+    for rank in range(2):
+        hf = g.HostForest.synthetic(trees, rows, seed=bench.SEED, first_tree=rank * trees)
+        f = g.Forest(hf, device=0)
+        for _ in range(warm + steps):
+            v = f.total_likelihood(bench.P_EXAMPLE)
+        f.close()
+        want = want + v
+    assert out["total_log_likelihood"] == want
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedObjective, shard
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        full = g.HostForest.synthetic(301, 120)
+        mine = shard(full, rank, world)
+        obj = ShardedObjective(g.Forest(mine, device=0))
+        vals = [obj.total_likelihood(P0) for _ in range(3)]
+        bad = list(P0)
+        bad[2] = -1.0
+        # a NaN on one rank only: rank 1 evaluates bad parameters, rank 0 good ones
+        obj2 = ShardedObjective(g.Forest(mine, device=0))
+        try:
+            obj2.total_likelihood(bad if rank == 1 else P0)
+            nan_ok = False
+        except g.LikelihoodIsNan:
+            nan_ok = True
+        q.put((rank, vals, mine.n_cells, nan_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_objective_hip_engine_two_ranks():
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = g.HostForest.synthetic(301, 120)
+    whole = g.Forest(full, device=0)
+    of = O.OracleForest(full.a)
+    want = [whole.total_likelihood(P0) for _ in range(3)]
+    ref = [of.total_likelihood(P0)[0] for _ in range(3)]
+    assert res[0][2] + res[1][2] == full.n_cells and min(res[0][2], res[1][2]) > 0
+    for rank, vals, ncells, nan_ok in res:
+        assert nan_ok                              # both ranks raise
+        for v, w, o in zip(vals, want, ref):
+            assert math.isfinite(v)
+            assert abs(v - w) <= 1e-12 * abs(w)    # another partition of the same sum
+            assert abs(v - o) <= 1e-9 * abs(o)     # the parity bar against the oracle
+    assert res[0][1] == res[1][1]                  # every rank holds the same total
