@@ -895,413 +895,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
 
 // ------------------------------------------------------------------------------------------
-// WAVE-G schedule (k_loglik_wg<G>): G lanes per cell, NC = 64/G cells per wave, four waves per
-// workgroup.  For mid-size levels (thousands to tens of thousands of cells): the wave schedule
-// keeps a SIMD busy with one cell (~480 wave-instructions per cell-step), the lane schedule
-// with 64 (~64 per cell-step, but ~4.1k in a row per step: a level of 12.5k cells runs at 0.2
-// waves per SIMD and waits on that latency).  Here every stage of the wave schedule is spread
-// over G lanes instead of 64: lane r of a cell runs the wave schedule's virtual lanes r, r + G,
-// ... (the same task bodies, ggp_wave.h; the tasks' constants come from an LDS table shared by
-// the workgroup), and the outputs' trilinear form runs over contiguous virtual lanes r·64/G ..
-// with the state monomials taken from a per-cell LDS table (kMono: the 60 distinct products
-// V1 V2 V3 of ggp_outtab.h's terms).  Waves of a workgroup share the Dawson table and the task
-// tables only; each wave's cells are independent, so stages are ordered by wave-local LDS
-// ordering (no workgroup barrier in the step loop).
-// Results: the wave schedule's expressions except the trilinear form's association
-// (kappa (V1 V2 V3) basis, block sums in another order): ~1e-10 from the lane schedule like
-// the wave schedule (DESIGN.md "Parity").  Cells of a wave run in lockstep; a finished cell's
-// lanes compute on its final state without storing.
-// ------------------------------------------------------------------------------------------
-namespace wg {
-constexpr int kWaves = 4;   // waves per workgroup
-
-struct MonoTab {
-    unsigned char a[64], b[64], c[64];   // V indices of monomial mu
-    unsigned char of[64][ggp::kOutL];    // monomial of term (virtual lane, q)
-    int n;
-};
-constexpr MonoTab make_mono()
-{
-    MonoTab M{};
-    for (int l = 0; l < 64; ++l)
-        for (int q = 0; q < ggp::kOutL; ++q) {
-            const ggp::OutTerm T = ggp::kOutTerm[l][q];
-            int x = T.v1, y = T.v2, z = T.v3;
-            if (T.kap == 255) x = y = z = 0;   // padding: kappa 0 times the monomial 1
-            if (x > y) { const int s = x; x = y; y = s; }
-            if (y > z) { const int s = y; y = z; z = s; }
-            if (x > y) { const int s = x; x = y; y = s; }
-            int k = 0;
-            while (k < M.n && !(M.a[k] == x && M.b[k] == y && M.c[k] == z)) ++k;
-            if (k == M.n) {
-                M.a[k] = (unsigned char)x;
-                M.b[k] = (unsigned char)y;
-                M.c[k] = (unsigned char)z;
-                ++M.n;
-            }
-            M.of[l][q] = (unsigned char)k;
-        }
-    return M;
-}
-constexpr MonoTab kMono = make_mono();
-static_assert(kMono.n <= 64, "monomials fit one slot per virtual lane");
-
-// per-cell LDS region: the wave schedule's layout (ggp_wave.h) up to its dummy slots (here one
-// per lane of the wave instead), then the monomials
-constexpr int C_MONO = ggp::wave::L_DUMMY;
-constexpr int kCell = C_MONO + 64;
-
-struct Term {   // one output term: kappa and the LDS offsets (doubles) of its monomial and basis
-    double kap;
-    int mono, basis;
-};
-
-// the wave's LDS stores before this point are visible to every lane of the wave after it (a
-// wave's LDS operations execute in order; this only keeps the compiler from moving them)
-GGP_DEV void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-GGP_DEV double shfl_f64(const double v, const int src)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffff));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-}  // namespace wg
-
-template <int G>
-__global__ __launch_bounds__(64 * wg::kWaves) void k_loglik_wg(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
-                                                              int n, double *__restrict__ state,
-                                                              double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
-{
-    namespace W = ggp::wave;
-    constexpr int NC = 64 / G;                          // cells per wave
-    constexpr int NV = 64 / G;                          // stage D: contiguous virtual lanes per lane
-    constexpr int NXS = 64 / G;                         // stage B: exponential slots (64 tasks)
-    constexpr int NDS = (ggp::ND + G - 1) / G;          // Dawson slots
-    constexpr int NIS = (ggp::NI + G - 1) / G;          // stage C: integral slots
-    constexpr int NMS = (wg::kMono.n + G - 1) / G;      // monomial slots
-    constexpr int NRS = (ggp::kNDerived + G - 1) / G;   // per-dt derived basis slots
-    static_assert(G >= 8 && G <= 32, "lanes 0..5 of a cell form exp(s t); virtual lanes 0..3 the products");
-    __shared__ __attribute__((aligned(16))) double s_tab[kDawsonTabP];
-    __shared__ W::LaneTasks s_task[64];
-    __shared__ wg::Term s_term[64][ggp::kOutL];
-    __shared__ int s_msrc[64][4];
-    __shared__ ggp::DTaskB s_dv[ggp::kNDerived];
-    __shared__ double s_cell[wg::kWaves * NC][wg::kCell];
-    __shared__ double s_dummy[wg::kWaves][64];
-    __shared__ double s_ring[wg::kWaves * NC][6][G];     // x0, x1, S00, S01, S11, the term
-    __shared__ double s_rows[wg::kWaves * NC][3][G + 1];  // this chunk's log length, fp, time (+ next time)
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int gi = lane / G, r = lane % G;
-    const int ci = wv * NC + gi;
-    double *Lc = s_cell[ci];
-    double *Dm = s_dummy[wv] + lane;   // this lane's slot for stores of tasks it does not own
-    const double *p = P.p;
-    const ggp::OU ou = W::pin_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
-    if (wv == 0) {
-        load_dawson_table_padded(s_tab, lane);
-        s_task[lane] = W::lane_tasks(lane, ou);
-#pragma unroll
-        for (int q = 0; q < ggp::kOutL; ++q) {
-            const ggp::OutTerm T = ggp::kOutTerm[lane][q];
-            s_term[lane][q] = wg::Term{ggp::out_kappa(ou, T.kap), wg::C_MONO + wg::kMono.of[lane][q], W::L_BV + T.basis};
-        }
-        const int mu = lane < wg::kMono.n ? lane : 0;
-        s_msrc[lane][0] = W::L_V + wg::kMono.a[mu];
-        s_msrc[lane][1] = W::L_V + wg::kMono.b[mu];
-        s_msrc[lane][2] = W::L_V + wg::kMono.c[mu];
-        s_msrc[lane][3] = lane < wg::kMono.n ? wg::C_MONO + lane : -1;
-        if (lane < ggp::kNDerived) s_dv[lane] = ggp::kDerived[lane];
-    }
-    // stage D constants of this lane's virtual lanes v = r NV + i: block sizes and destinations
-    int bsz[NV], ddst[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const int v = r * NV + i;
-        bsz[i] = ggp::kOutBlock[v];
-        int d = -1;
-#pragma unroll
-        for (int k = 0; k < ggp::kOutN; ++k) d = ggp::kOutLead[k] == v ? W::L_OUT + k : d;
-        ddst[i] = d;
-    }
-    const int lane_blk = bsz[0] >= NV ? bsz[0] / NV : 1;   // lanes a block spans (1: in-lane)
-    const double var_x = W::pin(p[7]), var_g = W::pin(p[8]);
-    const double var_dx = p[9], var_dg = p[10];
-    // the cell of this lane's group
-    const int i = (int)blockIdx.x * (wg::kWaves * NC) + ci;
-    const bool valid = i < n;
-    int c = 0;
-    int64_t r0 = 0;
-    int nrows = 0;
-    double m[4] = {0, 0, 0, 0}, C[16] = {0};
-    double dt = 0.0, t_cur = 0.0;
-    bool pending = false, divide = false;
-    if (valid) {
-        c = cells[i];
-        r0 = F.row_off[c];
-        nrows = (int)(F.row_off[c + 1] - r0);
-        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
-        divide = pending;
-        t_cur = F.time[r0];
-    }
-    // lanes without a cell compute on the wave's first cell's state (never stored): finite
-    // operands, so no rare branch is taken for them
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double v = wg::shfl_f64(m[k], 0);
-        m[k] = valid ? m[k] : v;
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const double v = wg::shfl_f64(C[k], 0);
-        C[k] = valid ? C[k] : v;
-    }
-    {
-        const double v = wg::shfl_f64(dt, 0);
-        dt = valid ? dt : v;
-    }
-    if (r == 0) {
-        Lc[W::L_X + ggp::X_ONE] = 1.0;
-        Lc[W::L_BV + ggp::BV_ONE] = 1.0;
-        Lc[W::L_V + ggp::V_ONE] = 1.0;
-    }
-    // the rows of chunk [k0, k0 + G) of every cell of the wave to LDS (one load per lane, waited
-    // for here: no global load is in flight during the steps)
-    double (*Rw)[G + 1] = s_rows[ci];
-    auto load_rows = [&](const int k0) {
-        double a = 0.0, b = 0.0, t = 0.0;
-        if (k0 + r < nrows) {
-            a = F.logl[r0 + k0 + r];
-            b = F.fp[r0 + k0 + r];
-            t = F.time[r0 + k0 + r];
-        }
-        Rw[0][r] = a;
-        Rw[1][r] = b;
-        Rw[2][r] = t;
-        if (r == 0) Rw[2][G] = k0 + G < nrows ? F.time[r0 + k0 + G] : 0.0;
-    };
-    load_rows(0);
-    __syncthreads();   // the tables (the only workgroup barrier)
-    unsigned long long dt_cached = 0x7ff4dead0000beefULL;
-    double cl = 0.0;
-    int nan_row = kNanNone;
-    int k = 0, nring = 0;
-    bool live = valid && nrows > 0;
-    while (__builtin_amdgcn_ballot_w64(live)) {
-        const int kr = k % G;   // the step's slot in the chunk and the ring (all cells in step)
-        const double y_l = Rw[0][kr], y_f = Rw[1][kr];
-        const double t_next = k + 1 < nrows ? Rw[2][kr + 1] : 0.0;
-        const bool prop = live && pending;
-        if (__builtin_amdgcn_ballot_w64(prop)) {
-            const W::WStep S = W::wstep(m, C, dt, ou.b);
-            if (r == 0) W::store_pw(S, Lc + W::L_P);
-            if (r == 1) W::store_v(m, C, dt, ou, Lc + W::L_V);
-            const unsigned long long dbits = (unsigned long long)__double_as_longlong(dt);
-            if (__builtin_amdgcn_ballot_w64(dbits != dt_cached)) {   // exp(s t) and the derived basis
-                if (r < 6) Lc[W::xs_dst_of(r)] = exp(W::sv_of(ou, r) * dt);
-                wg::wave_sync();
-#pragma unroll
-                for (int j = 0; j < NRS; ++j) {
-                    const int v = r + G * j;
-                    const double dvv = ggp::derived_generic(s_dv[v < ggp::kNDerived ? v : 0], Lc + W::L_X, ou.gl, dt);
-                    *(v < ggp::kNDerived ? Lc + W::L_BV + ggp::BV_R_EBT + v : Dm) = dvv;
-                }
-                wg::wave_sync();
-                dt_cached = dbits;
-            }
-            // stage B: exponentials (virtual lanes r + G j), Dawson values, the four products.
-            // Every slot's constants are read first, the values formed, the stores last (a store
-            // may alias a later read for the compiler: stores in between would serialise)
-            double xa[NXS], ev[NXS];
-            int xdst[NXS];
-#pragma unroll
-            for (int j = 0; j < NXS; ++j) {
-                const W::LaneTasks &T = s_task[r + G * j];
-                W::LaneTasks L;
-                L.x_tau = T.x_tau; L.x_km = T.x_km; L.x_gqks = T.x_gqks; L.x_m1 = T.x_m1; L.x_m2 = T.x_m2;
-                L.x_kc = T.x_kc; L.x_isE = T.x_isE; L.x_isA = T.x_isA;
-                xdst[j] = T.x_dst;
-                xa[j] = W::exp_arg(S, L);
-            }
-            double dz[NDS];
-#pragma unroll
-            for (int j = 0; j < NDS; ++j) {
-                const int v = r + G * j;
-                const W::LaneTasks &T = s_task[v < ggp::ND ? v : 0];
-                W::LaneTasks L;
-                L.d_tau = T.d_tau; L.d_km = T.d_km; L.d_gqks = T.d_gqks;
-                dz[j] = W::dawson_arg(S, L);
-            }
-            bool big = false;
-#pragma unroll
-            for (int j = 0; j < NXS; ++j) {
-                ev[j] = ggp::exp_ocml(xa[j]);
-                big = big || !(fabs(xa[j]) < ggp::kExpFastMax);
-            }
-            if (__builtin_amdgcn_ballot_w64(big)) {   // ocml's exp beyond 2^50 (rare)
-#pragma unroll
-                for (int j = 0; j < NXS; ++j) ev[j] = fabs(xa[j]) < ggp::kExpFastMax ? ev[j] : exp(xa[j]);
-            }
-            double dv[NDS];
-#pragma unroll
-            for (int j = 0; j < NDS; ++j) dv[j] = W::dawson_bf(dz[j], s_tab);
-            const double ea = wg::shfl_f64(ev[0], gi * G);   // exp(c_A): virtual lane 0 of the cell
-            int pdst = 0;
-            double pmul = 0.0;
-            if (r < 4) {
-                const W::LaneTasks &T = s_task[r];
-                pdst = T.prod_dst;
-                pmul = Lc[T.mult_off];
-            }
-#pragma unroll
-            for (int j = 0; j < NXS; ++j) Lc[xdst[j]] = ev[j];
-#pragma unroll
-            for (int j = 0; j < NDS; ++j) {
-                const int v = r + G * j;
-                *(v < ggp::ND ? Lc + W::L_D + v : Dm) = dv[j];
-            }
-            *(r < 4 ? Lc + pdst : Dm) = ea * pmul;   // exp(c_B), exp(c_J), exp(c_G), exp(c_I)
-            wg::wave_sync();
-            // monomials of the state (V, stored above) and stage C: integrals (virtual lanes r + G j)
-            double mv[NMS];
-            int mdst[NMS];
-#pragma unroll
-            for (int j = 0; j < NMS; ++j) {
-                const int mu = (r + G * j) & 63;
-                mv[j] = (Lc[s_msrc[mu][0]] * Lc[s_msrc[mu][1]]) * Lc[s_msrc[mu][2]];
-                mdst[j] = s_msrc[mu][3];
-            }
-            double iv[NIS];
-#pragma unroll
-            for (int j = 0; j < NIS; ++j) {
-                const int v = r + G * j;
-                iv[j] = W::tau_bf(S, s_task[v < ggp::NI ? v : 0], Lc + W::L_X, Lc + W::L_D, Lc + W::L_P);
-            }
-#pragma unroll
-            for (int j = 0; j < NMS; ++j) *(mdst[j] >= 0 ? Lc + mdst[j] : Dm) = mv[j];
-#pragma unroll
-            for (int j = 0; j < NIS; ++j) {
-                const int v = r + G * j;
-                *(v < ggp::NI ? Lc + W::L_BV + ggp::BV_I + v : Dm) = iv[j];
-            }
-            wg::wave_sync();
-            // stage D: the terms of virtual lanes r NV + i, block sums in-lane, then across lanes
-            double pv[NV];
-#pragma unroll
-            for (int ii = 0; ii < NV; ++ii) {
-                const int v = r * NV + ii;
-                double acc = 0.0;
-#pragma unroll
-                for (int q = 0; q < ggp::kOutL; ++q) {
-                    const wg::Term t = s_term[v][q];
-                    acc = __builtin_fma(t.kap * Lc[t.mono], Lc[t.basis], acc);
-                }
-                pv[ii] = acc;
-            }
-#pragma unroll
-            for (int s = 1; s < NV; s <<= 1) {
-                double nx[NV];
-#pragma unroll
-                for (int ii = 0; ii < NV; ++ii) nx[ii] = bsz[ii] > s ? pv[ii] + pv[ii ^ s] : pv[ii];
-#pragma unroll
-                for (int ii = 0; ii < NV; ++ii) pv[ii] = nx[ii];
-            }
-            {   // blocks wider than a lane: pv[0] holds the lane's part (all its pv are equal)
-                double x = pv[0], w;
-                // a block spans up to 16 / NV = G / 4 lanes of the cell's group
-                if (G >= 8) { w = dpp_f64<0xB1>(x); x = lane_blk > 1 ? x + w : x; }    // quad_perm xor 1
-                if (G >= 16) { w = dpp_f64<0x4E>(x); x = lane_blk > 2 ? x + w : x; }   // quad_perm xor 2
-                if (G >= 32) { w = dpp_f64<0x141>(x); x = lane_blk > 4 ? x + w : x; }  // row_half_mirror
-#pragma unroll
-                for (int ii = 0; ii < NV; ++ii) *(ddst[ii] >= 0 ? Lc + ddst[ii] : Dm) = lane_blk > 1 ? x : pv[ii];
-            }
-            wg::wave_sync();
-            if (prop) {
-                double o[ggp::kOutN];
-#pragma unroll
-                for (int kk = 0; kk < ggp::kOutN; ++kk) o[kk] = Lc[W::L_OUT + kk];
-#pragma unroll
-                for (int kk = 0; kk < ggp::kOutN; ++kk)
-                    if (ggp::kOutNm[kk][0] >= 0) o[kk] = __builtin_fma(-o[ggp::kOutNm[kk][0]], o[ggp::kOutNm[kk][1]], o[kk]);
-                ggp::out_store(o, m, C);
-                if (divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
-            }
-            wg::wave_sync();   // the outputs are read before the next step rewrites them
-        }
-        // the measurement step (likelihood.h:53-69): live cells only
-        const double x0 = y_l - m[0];
-        const double x1 = y_f - m[1];
-        const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
-        double *rg = &s_ring[ci][0][0];
-        if (live) {
-            if (r == 0) {
-                rg[0 * G + nring] = x0;
-                rg[1 * G + nring] = x1;
-                rg[2 * G + nring] = v.S00;
-                rg[3 * G + nring] = v.S01;
-                rg[4 * G + nring] = v.S11;
-            }
-            W::posterior(m, C, x0, x1, v, k + 1 == nrows);
-            pending = k + 1 < nrows;
-            if (pending) dt = t_next - t_cur;
-            t_cur = t_next;
-            divide = false;
-            ++nring;
-        }
-        ++k;   // every cell of the wave steps together (a finished cell's k runs past its rows)
-        const bool ended = live && k == nrows;
-        // ll terms of the ring (rows k - nring .. k - 1), in row order: when a ring is full (the
-        // chunk is done) or a cell has ended
-        if (__builtin_amdgcn_ballot_w64(nring == G || ended)) {
-            wg::wave_sync();
-            if (r < nring) {
-                const double s00 = rg[2 * G + r], s01 = rg[3 * G + r], s11 = rg[4 * G + r];
-                rg[5 * G + r] = ggp::wave::ll_quad(rg[0 * G + r], rg[1 * G + r], s00, s01, s11) -
-                                0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - F.two_log_2pi;
-            }
-            wg::wave_sync();
-            if (nring > 0) {   // every lane of the cell adds the terms in row order (same bits)
-                double acc = cl;
-                for (int q = 0; q < nring; ++q) acc += rg[5 * G + q];
-                if (acc != acc) {
-                    acc = cl;
-                    for (int q = 0; q < nring; ++q) {
-                        acc += rg[5 * G + q];
-                        if (acc != acc) {
-                            nan_row = k - nring + q;
-                            break;
-                        }
-                    }
-                    live = false;
-                }
-                cl = acc;
-            }
-            nring = 0;
-            wg::wave_sync();
-        }
-        live = live && k < nrows;
-        if (k % G == 0 && __builtin_amdgcn_ballot_w64(live)) {   // the next chunk of rows
-            load_rows(k);
-            wg::wave_sync();
-        }
-    }
-    if (valid && r == 0) {
-        double *st = state + (size_t)20 * c;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) st[kk] = m[kk];
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) st[4 + kk] = C[kk];
-        cell_ll[F.dfs_rank[c]] = cl;
-        cell_nan[F.dfs_rank[c]] = nan_row;
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // -p smoother kernels (lane schedule).  Parameters per row come from the segment table.
 // ------------------------------------------------------------------------------------------
 GGP_DEV const double *seg_params(const DevForest &F, const double *ptab, int n_seg, int64_t r)
@@ -1887,7 +1480,6 @@ struct Shard {
     int64_t wave_max_cells = 5120;    // auto: wave schedule for levels up to this size
     int64_t group_max_cells = 8192;   // auto: group schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
-    int tune_wg_g = 16;                          // GGP_WG_G: lanes per cell of the wave-G schedule
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -2036,20 +1628,6 @@ int launch_levels(Shard *f, const ggp_params &P)
                                (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
-        } else if (kind == GGP_KERNEL_WG) {
-            const int G = f->tune_wg_g;
-            const int cpb = wg::kWaves * (64 / G);   // cells per workgroup
-            const int blocks = (n + cpb - 1) / cpb;
-            switch (G) {
-            case 8: hipLaunchKernelGGL(k_loglik_wg<8>, dim3(blocks), dim3(64 * wg::kWaves), 0, f->stream, f->F, P,
-                                       f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
-            case 32: hipLaunchKernelGGL(k_loglik_wg<32>, dim3(blocks), dim3(64 * wg::kWaves), 0, f->stream, f->F, P,
-                                        f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
-            default: hipLaunchKernelGGL(k_loglik_wg<16>, dim3(blocks), dim3(64 * wg::kWaves), 0, f->stream, f->F, P,
-                                        f->d_level_cells + a, n, f->d_state, f->d_cell_ll, f->d_cell_nan); break;
-            }
-            f->kernel_used = GGP_KERNEL_WG;
-            f->last_code = GGP_KERNEL_WG << 8 | G;
         } else if (kind == GGP_KERNEL_GROUP) {
             // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
@@ -2283,10 +1861,6 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_WG_G")) {
-        const int v = atoi(e);
-        f->tune_wg_g = (v == 8 || v == 16 || v == 32) ? v : 16;
-    }
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);
@@ -2760,7 +2334,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
 {
     if (!d || !out) { g_last_err = "null argument"; return GGP_EINVAL; }
     *out = nullptr;
-    if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_WG) {
+    if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_WAVE) {
         g_last_err = "ggp_forest_create: unknown kernel policy";
         return GGP_EINVAL;
     }

@@ -365,8 +365,6 @@ def kernel_name(code: int) -> str:
         return "k_loglik_level"
     if kind == N.KERNELS["wave"]:
         return "k_loglik_wave"
-    if kind == N.KERNELS["wg"]:
-        return f"k_loglik_wg<{lanes}>"
     return f"k_loglik_group<{lanes}>"
 
 

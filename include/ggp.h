@@ -102,9 +102,6 @@ typedef struct {
 #define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
 #define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);
                                  agrees with LANE/GROUP to ~1e-10, not bitwise        */
-#define GGP_KERNEL_WG 4       /* G lanes per cell (GGP_WG_G = 8, 16, 32), the wave
-                                 schedule's tasks spread over G lanes (mid-size
-                                 levels); ~1e-10 from LANE, not bitwise               */
 /* Launch form (per shard, fixed at creation): when every level takes the wave schedule and the
  * shard has at most as many leaves as the device holds wave blocks, an evaluation is ONE launch
  * (a block per root-to-leaf path, the sum formed in-launch); otherwise one launch per level plus
