@@ -74,6 +74,10 @@ ENGINE_SYMBOLS = {
     "ggp_predict_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p]),
     "ggp_debug_dawson": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, c_double_p, ctypes.c_int64, c_double_p]),
     "ggp_debug_tauint": (ctypes.c_int, [ctypes.c_int32, c_double_p, ctypes.c_int64, c_double_p]),
+    "ggp_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "ggp_comm_attach": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_char_p]),
+    "ggp_comm_nan_rank": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),
     "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "ggp_version": (ctypes.c_char_p, []),

@@ -59,7 +59,7 @@ def build(verbose: bool = False, force: bool = False) -> dict:
             eng_deps.append(p)
     eng = os.path.join(LIB, "libggp.so")
     if force or not _newer(eng, eng_deps):
-        _run([HIPCC, *HIP_FLAGS, "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src], verbose)
+        _run([HIPCC, *HIP_FLAGS, "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src, "-ldl"], verbose)
     out["libggp"] = eng
     # --- host ingest ---
     host_src = os.path.join(CSRC, "host", "ggp_host.cpp")

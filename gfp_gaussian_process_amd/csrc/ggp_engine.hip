@@ -17,6 +17,8 @@
 // with a fixed reduction tree (bitwise reproducible) and finds the first NaN.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -1341,6 +1343,82 @@ __global__ __launch_bounds__(kRedMax) void k_reduce_blocks(int64_t n_cells, cons
 }
 
 // ------------------------------------------------------------------------------------------
+// Multi-process evaluation (ggp_comm_attach): this rank's partial, the RCCL all-gather, the
+// rank-order sum -- all on the shard's stream behind the evaluation.
+// k_rank_partial: ggp_loglik_result's total on the device: the block results (mapped host
+// memory, written by the reduction of this evaluation) zero-padded to np2 and summed by the same
+// fixed pairwise tree (v[i] = v[2i] + v[2i+1], level by level: top_sum's bits), and the flag of
+// a NaN partial (a first-NaN code, or a NaN sum: ggp_loglik_result's GGP_ENAN cases).
+// part = {sum, flag as a double}: the 16 B this rank sends.
+// ------------------------------------------------------------------------------------------
+constexpr int kPartMax = 4096;   // blocks a rank may hold (4096 x 1024 trees)
+
+__global__ __launch_bounds__(256) void k_rank_partial(const double *__restrict__ blk, const int64_t *__restrict__ code, int nb,
+                                                      int np2, double *__restrict__ part)
+{
+    __shared__ double v[kPartMax];
+    __shared__ long long cm[256];
+    const int t = threadIdx.x;
+    long long c = kNoNan;
+    for (int i = t; i < np2; i += 256) {
+        double x = 0.0;
+        if (i < nb) {   // fine-grained host memory: system-scope loads
+            x = __longlong_as_double(
+                (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(blk + i), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM));
+            c = min(c, (long long)__hip_atomic_load(code + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        }
+        v[i] = x;
+    }
+    cm[t] = c;
+    __syncthreads();
+    constexpr int R = kPartMax / 512;   // pairs per thread at the widest level
+    for (int n = np2; n > 1; n >>= 1) {
+        double x[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int i = t + 256 * j;
+            x[j] = i < n / 2 ? v[2 * i] + v[2 * i + 1] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int i = t + 256 * j;
+            if (i < n / 2) v[i] = x[j];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        long long mc = kNoNan;
+        for (int k = 0; k < 256; ++k) mc = min(mc, cm[k]);
+        const double s = v[0];
+        part[0] = s;
+        part[1] = (mc != kNoNan || s != s) ? 1.0 : 0.0;
+    }
+}
+
+// distributed.combine_partials on the gathered {sum, flag} of every rank: the first rank with a
+// flag decides (NaN), else 0.0 + p_0 + p_1 + ... in rank order; the result and that rank to the
+// mapped host slots, then the call's sequence number (system-scope release; the host spins on it)
+__global__ void k_rank_sum(const double *__restrict__ g, int nranks, double *out_sum, int64_t *out_rank, int64_t *out_seq,
+                           int64_t seq)
+{
+    if (threadIdx.x != 0) return;
+    double s = 0.0;
+    long long nr = -1;
+    for (int r = 0; r < nranks; ++r) {
+        if (nr < 0 && g[2 * r + 1] != 0.0) nr = r;
+        s = s + g[2 * r];
+    }
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(out_sum),
+                       (unsigned long long)__double_as_longlong(nr >= 0 ? __longlong_as_double(0x7ff8000000000000LL) : s),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out_rank, (int64_t)nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------------------------------
 // Test-only device entry points (tests/test_gpu_device_math.py): the device Dawson in both
 // forms the kernels use, and the four tauint integrals of mean_cov_model.h:9-67 built from
 // the same device primitives (rdiv, ocml exp, table Dawson, a^k sqrt(a)) in tau_body's
@@ -1557,12 +1635,44 @@ struct Shard {
     std::vector<double> j_params;      // the table the joint tables hold (empty: none)
 };
 
+// RCCL entry points, resolved at run time from the library the caller names (the one torch
+// loaded, so the process holds a single RCCL): rccl.h signatures, the unique id by value
+struct ggp_rccl_id {
+    char internal[128];
+};
+struct RcclApi {
+    void *lib = nullptr;
+    int (*get_unique_id)(ggp_rccl_id *) = nullptr;
+    int (*comm_init_rank)(void **, int, ggp_rccl_id, int) = nullptr;
+    int (*all_gather)(const void *, void *, size_t, int, void *, hipStream_t) = nullptr;
+    int (*comm_destroy)(void *) = nullptr;
+    const char *(*error_string)(int) = nullptr;
+};
+constexpr int kRcclUint8 = 1;   // ncclUint8 (rccl.h ncclDataType_t)
+
+// one rank of a group of one-GPU processes (ggp_comm_attach)
+struct Comm {
+    RcclApi api;
+    void *nc = nullptr;                // ncclComm_t
+    int nranks = 1, rank = 0;
+    double *d_part = nullptr;          // this rank's {sum, flag}
+    double *d_gath = nullptr;          // every rank's, in rank order
+    void *h_res = nullptr;             // mapped: the total, the first NaN rank, the sequence number
+    volatile double *h_sum = nullptr;
+    volatile int64_t *h_rank = nullptr, *h_seq = nullptr;
+    double *m_sum = nullptr;
+    int64_t *m_rank = nullptr, *m_seq = nullptr;
+    int64_t seq = 0;
+    int32_t last_nan_rank = -1;
+};
+
 struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0, n_trees = 0, blk_trees = 1, n_blocks = 0;
     std::vector<DeviceCtx *> devs;
     std::vector<Shard *> shards;
     std::vector<int32_t> dfs_order;    // global DFS position -> global cell
     std::vector<int64_t> row_off;      // global row_offset
+    Comm *comm = nullptr;              // multi-process mode (ggp_comm_attach)
 };
 
 namespace {
@@ -2307,6 +2417,102 @@ const char *ggp_strerror(int code)
 
 const char *ggp_version(void) { return GGP_VERSION; }
 
+static int rccl_load(const char *path, RcclApi &a)
+{
+    const char *lib = path && *path ? path : "librccl.so.1";
+    a.lib = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!a.lib) {
+        g_last_err = std::string("cannot load ") + lib + ": " + dlerror();
+        return GGP_EDEV;
+    }
+    a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(a.lib, "ncclGetUniqueId"));
+    a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(dlsym(a.lib, "ncclCommInitRank"));
+    a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(a.lib, "ncclAllGather"));
+    a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(a.lib, "ncclCommDestroy"));
+    a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(a.lib, "ncclGetErrorString"));
+    if (!a.get_unique_id || !a.comm_init_rank || !a.all_gather || !a.comm_destroy) {
+        g_last_err = std::string(lib) + " lacks the RCCL entry points";
+        return GGP_EDEV;
+    }
+    return GGP_OK;
+}
+
+int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id)
+{
+    if (!id) return GGP_EINVAL;
+    RcclApi a;
+    int rc = rccl_load(rccl_lib, a);
+    if (rc != GGP_OK) return rc;
+    ggp_rccl_id u;
+    const int e = a.get_unique_id(&u);
+    if (e != 0) {
+        g_last_err = std::string("ncclGetUniqueId: ") + (a.error_string ? a.error_string(e) : "error");
+        return GGP_EDEV;
+    }
+    std::memcpy(id, u.internal, sizeof u.internal);
+    return GGP_OK;
+}
+
+int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id)
+{
+    if (!f || !id || nranks < 1 || rank < 0 || rank >= nranks) return GGP_EINVAL;
+    if (f->comm) {
+        g_last_err = "ggp_comm_attach: the handle is already attached";
+        return GGP_EINVAL;
+    }
+    if (f->shards.size() != 1 || f->shards[0]->n_lblocks > kPartMax) {
+        g_last_err = "ggp_comm_attach: the handle must hold one shard (one device per process) of at most 4096 blocks";
+        return GGP_EINVAL;
+    }
+    Shard *s = f->shards[0];
+    Comm *c = new Comm;
+    c->nranks = nranks;
+    c->rank = rank;
+    int rc = rccl_load(rccl_lib, c->api);
+    auto fail = [&](int code) {
+        if (c->d_part) (void)hipFree(c->d_part);
+        if (c->d_gath) (void)hipFree(c->d_gath);
+        if (c->h_res) (void)hipHostFree(c->h_res);
+        if (c->nc) c->api.comm_destroy(c->nc);
+        delete c;
+        return code;
+    };
+    if (rc != GGP_OK) return fail(rc);
+    if (hipSetDevice(s->device) != hipSuccess || hipMalloc(&c->d_part, 2 * sizeof(double)) != hipSuccess ||
+        hipMalloc(&c->d_gath, 2 * sizeof(double) * (size_t)nranks) != hipSuccess) {
+        g_last_err = "ggp_comm_attach: device buffers";
+        return fail(GGP_ENOMEM);
+    }
+    void *m = nullptr;
+    if (hipHostMalloc(&c->h_res, 3 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&m, c->h_res, 0) != hipSuccess) {
+        g_last_err = "ggp_comm_attach: mapped result slots";
+        return fail(GGP_ENOMEM);
+    }
+    c->h_sum = (volatile double *)c->h_res;
+    c->h_rank = (volatile int64_t *)((char *)c->h_res + sizeof(double));
+    c->h_seq = (volatile int64_t *)((char *)c->h_res + 2 * sizeof(double));
+    *c->h_seq = 0;
+    c->m_sum = (double *)m;
+    c->m_rank = (int64_t *)((char *)m + sizeof(double));
+    c->m_seq = (int64_t *)((char *)m + 2 * sizeof(double));
+    ggp_rccl_id u;
+    std::memcpy(u.internal, id, sizeof u.internal);
+    const int e = c->api.comm_init_rank(&c->nc, nranks, u, rank);   // every rank of the group joins
+    if (e != 0) {
+        g_last_err = std::string("ncclCommInitRank: ") + (c->api.error_string ? c->api.error_string(e) : "error");
+        c->nc = nullptr;
+        return fail(GGP_EDEV);
+    }
+    f->comm = c;
+    return GGP_OK;
+}
+
+int32_t ggp_comm_nan_rank(const ggp_forest *f)
+{
+    return f && f->comm ? f->comm->last_nan_rank : -1;
+}
+
 int ggp_device_count(int32_t *n)
 {
     int c = 0;
@@ -2318,6 +2524,17 @@ int ggp_device_count(int32_t *n)
 void ggp_forest_destroy(ggp_forest *f)
 {
     if (!f) return;
+    if (Comm *c = f->comm) {
+        if (!f->shards.empty()) {
+            (void)hipSetDevice(f->shards[0]->device);
+            (void)hipStreamSynchronize(f->shards[0]->stream);
+        }
+        if (c->nc && c->api.comm_destroy) c->api.comm_destroy(c->nc);
+        if (c->d_part) (void)hipFree(c->d_part);
+        if (c->d_gath) (void)hipFree(c->d_gath);
+        if (c->h_res) (void)hipHostFree(c->h_res);
+        delete c;   // the RCCL library stays loaded (the process's other users hold it too)
+    }
     for (Shard *s : f->shards) shard_destroy(s);
     for (DeviceCtx *d : f->devs) {
         (void)hipSetDevice(d->id);
@@ -2523,12 +2740,68 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
         const int rc = shard_launch(s, P);
         if (rc != GGP_OK) return rc;
     }
+    if (Comm *c = f->comm) {   // behind the evaluation: partial, all-gather, rank-order sum
+        Shard *s = f->shards[0];
+        int np2 = 1;
+        while (np2 < s->n_lblocks) np2 *= 2;
+        hipLaunchKernelGGL(k_rank_partial, dim3(1), dim3(256), 0, s->stream, s->m_sum, s->m_nan, (int)s->n_lblocks, np2,
+                           c->d_part);
+        HIPCHK(hipGetLastError());
+        const int e = c->api.all_gather(c->d_part, c->d_gath, 2 * sizeof(double), kRcclUint8, c->nc, s->stream);
+        if (e != 0) {
+            g_last_err = std::string("RCCL all-gather: ") + (c->api.error_string ? c->api.error_string(e) : "error");
+            return GGP_EDEV;
+        }
+        ++c->seq;
+        hipLaunchKernelGGL(k_rank_sum, dim3(1), dim3(64), 0, s->stream, c->d_gath, c->nranks, c->m_sum, c->m_rank, c->m_seq,
+                           c->seq);
+        HIPCHK(hipGetLastError());
+    }
     return GGP_OK;
+}
+
+// multi-process result: spin on the sequence number k_rank_sum releases (hipStreamQuery as the
+// way out), then the shard's own block results for this rank's NaN location
+static int comm_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
+{
+    Comm *c = f->comm;
+    Shard *s = f->shards[0];
+    bool seen = false;
+    for (uint32_t it = 1;; ++it) {
+        if (*c->h_seq == c->seq) { seen = true; break; }
+        if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    s->seq_pending = false;
+    if (!seen || s->profile) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (*c->h_seq != c->seq) {
+            g_last_err = "multi-process evaluation did not complete";
+            return GGP_EDEV;
+        }
+    }
+    const double v = *c->h_sum;
+    c->last_nan_rank = (int32_t)*c->h_rank;
+    if (ll) *ll = v;
+    if (nan_cell) *nan_cell = -1;
+    if (nan_row) *nan_row = -1;
+    if (c->last_nan_rank < 0) return GGP_OK;
+    if (c->last_nan_rank == c->rank) {   // this rank's first NaN, as ggp_loglik_result finds it
+        long long code = kNoNan;
+        for (int64_t j = 0; j < s->n_lblocks; ++j) code = std::min<long long>(code, s->h_nan[j]);
+        if (code != kNoNan) {
+            if (nan_cell) *nan_cell = f->dfs_order[code >> 24];
+            if (nan_row) *nan_row = code & 0xffffff;
+        }
+    }
+    return GGP_ENAN;
 }
 
 int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
     if (!f) return GGP_EINVAL;
+    if (f->comm) return comm_result(f, ll, nan_cell, nan_row);
     std::vector<double> blocks((size_t)f->n_blocks, 0.0);
     long long code = kNoNan;
     for (Shard *s : f->shards) {

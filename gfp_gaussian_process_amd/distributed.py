@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import heapq
 import math
+import os
 
 import numpy as np
 
@@ -86,7 +87,8 @@ class ShardedObjective:
     device_forest: this rank's Forest (or any object with .total_likelihood(params)).
     """
 
-    def __init__(self, device_forest, group=None, device=None, always_gather: bool = False):
+    def __init__(self, device_forest, group=None, device=None, always_gather: bool = False,
+                 engine_comm: bool | None = None):
         import torch
         import torch.distributed as dist
         self.f = device_forest
@@ -96,6 +98,15 @@ class ShardedObjective:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.always_gather = always_gather          # tests: the collective path at world size 1
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        # RCCL inside the engine (include/ggp.h ggp_comm_attach): the all-gather is enqueued on the
+        # engine's stream behind the evaluation, no host round trip in between.  Default on for
+        # nccl groups whose per-rank objective is a HIP Forest (GGP_ENGINE_COMM=0: torch's path)
+        if engine_comm is None:
+            engine_comm = os.environ.get("GGP_ENGINE_COMM", "1") != "0"
+        self.engine = False
+        if (engine_comm and backend == "nccl" and (self.world > 1 or always_gather)
+                and isinstance(device_forest, Forest)):
+            self._attach_engine(torch, dist, group)
         self.dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
                                                       if backend == "nccl" else torch.device("cpu"))
         self._send = torch.zeros(2, dtype=torch.float64, device=self.dev)
@@ -110,6 +121,19 @@ class ShardedObjective:
         self._h_send_np = self._h_send.numpy()
         self._h_recv_np = self._h_recv.numpy()
 
+    def _attach_engine(self, torch, dist, group):
+        from .forest import comm_unique_id
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        lib = lib if os.path.exists(lib) else None      # the RCCL torch loaded: one RCCL per process
+        rank = dist.get_rank(group)
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(comm_unique_id(lib)), dtype=torch.uint8))
+        dist.broadcast(uid, src=src, group=group)
+        self.f.comm_attach(self.world, rank, bytes(uid.cpu().numpy().tobytes()), lib)
+        self.engine = True
+
     def local(self, params):
         try:
             return self.f.total_likelihood(params), False, None
@@ -117,6 +141,8 @@ class ShardedObjective:
             return math.nan, True, e
 
     def total_likelihood(self, params) -> float:
+        if self.engine:   # the engine returns the rank-order sum (or raises, on every rank)
+            return self.f.total_likelihood(params)
         v, isnan, err = self.local(params)
         if self.world == 1 and not self.always_gather:
             if isnan:

@@ -368,6 +368,16 @@ def kernel_name(code: int) -> str:
     return f"k_loglik_group<{lanes}>"
 
 
+def comm_unique_id(rccl_lib: str | None = None) -> bytes:
+    """the 128-byte RCCL unique id (ncclGetUniqueId) rank 0 makes for Forest.comm_attach"""
+    buf = ctypes.create_string_buffer(128)
+    lib = N.engine()
+    rc = lib.ggp_comm_unique_id(rccl_lib.encode() if rccl_lib else None, buf)
+    if rc != N.GGP_OK:
+        raise GGPError(lib.ggp_strerror(rc).decode())
+    return buf.raw
+
+
 class Forest:
     """Device-resident forest + carried state.  Owns a ggp_forest handle.
 
@@ -400,6 +410,9 @@ class Forest:
             raise GGPError(self._lib.ggp_strerror(rc).decode())
 
     def _nan(self, nc: int, nr: int):
+        r = self._lib.ggp_comm_nan_rank(self._h) if getattr(self, "_comm_rank", None) is not None else -1
+        if r >= 0 and r != self._comm_rank:   # another rank's NaN: this rank's state is intact
+            return LikelihoodIsNan(-1, -1, f"rank {r}")
         # after a NaN the carried state is unspecified (include/ggp.h "Errors"): the next
         # evaluation needs reset_state() or set_state() first
         self._poisoned = True
@@ -423,6 +436,17 @@ class Forest:
             raise self._nan(self._nc.value, self._nr.value)
         self._check(rc)
         return self._ll.value
+
+    # -- one process per GPU: the engine's own RCCL collective (include/ggp.h ggp_comm_attach) --
+    def comm_attach(self, nranks: int, rank: int, uid: bytes, rccl_lib: str | None = None) -> None:
+        """join a group of one-GPU processes: every later total_likelihood returns the total over
+        all ranks (this forest is this rank's whole-tree shard); `uid` from comm_unique_id() on
+        rank 0.  Every rank of the group must call it."""
+        if len(uid) != 128:
+            raise ValueError("uid must be the 128-byte id of comm_unique_id()")
+        self._check(self._lib.ggp_comm_attach(self._h, rccl_lib.encode() if rccl_lib else None, int(nranks),
+                                              int(rank), bytes(uid)))
+        self._comm_rank = int(rank)
 
     def submit(self, params) -> None:
         """enqueue one evaluation (ggp_total_loglik_async)"""

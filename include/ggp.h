@@ -185,6 +185,24 @@ int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *ke
 int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
                     int32_t *kernel_used);
 
+/* One process per GPU (north_star "a single RCCL collective per NLopt objective
+ * call"): the handle holds this process's whole-tree shard (one device), and after
+ * ggp_comm_attach every ggp_total_loglik / ggp_loglik_result returns the total over all ranks.
+ * The collective is enqueued by the engine on the shard's stream right behind the evaluation:
+ * a one-workgroup kernel forms this rank's partial (ggp_loglik_result's pairwise tree over its
+ * blocks, and its first-NaN flag), one RCCL all-gather moves 16 B per rank over xGMI, and a
+ * one-thread kernel sums the partials in rank order into mapped host memory (the host spins on
+ * it): the same bits as distributed.ShardedObjective's all_gather + combine_partials.  A NaN
+ * partial on any rank makes the call return GGP_ENAN on every rank; *nan_cell / *nan_row are
+ * this rank's first NaN, or -1 when the first NaN rank is another (ggp_comm_nan_rank).
+ *   rccl_lib: the RCCL library to use (the one torch already loaded, so the process holds one
+ *             RCCL; NULL = "librccl.so.1")
+ *   id: 128 bytes (ncclUniqueId) made by ggp_comm_unique_id on rank 0 and given to every rank
+ * The shard's device must be the process's current device for RCCL (one device per handle). */
+int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
+int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
+int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last call, -1 none */
+
 int ggp_device_count(int32_t *n);
 const char *ggp_strerror(int code);
 const char *ggp_version(void);

@@ -526,32 +526,38 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 P = PARAMS
 hf = g.HostForest.synthetic(1000, 200)
-a, b = g.Forest(hf), g.Forest(hf)
-obj = ShardedObjective(a, always_gather=True)
-same = all(obj.total_likelihood(P) == b.total_likelihood(P) for _ in range(3))
-for _ in range(5):   # fresh objectives: their first collective is ordered after the engine
-    a2, b2 = g.Forest(hf), g.Forest(hf)
-    same = same and ShardedObjective(a2, always_gather=True).total_likelihood(P) == b2.total_likelihood(P)
-bad = list(P); bad[2] = -1.0
-try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
-    ShardedObjective(g.Forest(hf), always_gather=True).total_likelihood(bad); nan_ok = False
-except g.LikelihoodIsNan:
-    nan_ok = True
-t = {}
-for name, fn in (("direct", b.total_likelihood), ("gather", obj.total_likelihood)):
-    for _ in range(20): fn(P)
-    t0 = time.perf_counter()
-    for _ in range(200): fn(P)
-    t[name] = 1e3 * (time.perf_counter() - t0) / 200
+same, nan_ok, t, mode = True, True, {}, {}
+b = g.Forest(hf)
+for name, ec in (("engine", True), ("torch", False)):   # RCCL inside the engine; torch's all_gather
+    a = g.Forest(hf)
+    obj = ShardedObjective(a, always_gather=True, engine_comm=ec)
+    mode[name] = obj.engine
+    b.reset_state()
+    same = same and all(obj.total_likelihood(P) == b.total_likelihood(P) for _ in range(3))
+    for _ in range(5):   # fresh objectives: their first collective is ordered after the engine
+        a2, b2 = g.Forest(hf), g.Forest(hf)
+        same = same and ShardedObjective(a2, always_gather=True, engine_comm=ec).total_likelihood(P) == b2.total_likelihood(P)
+    bad = list(P); bad[2] = -1.0
+    try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
+        ShardedObjective(g.Forest(hf), always_gather=True, engine_comm=ec).total_likelihood(bad); nan_ok = False
+    except g.LikelihoodIsNan as e:
+        nan_ok = nan_ok and e.cell >= 0
+    for nm, fn in (("direct", b.total_likelihood), (name, obj.total_likelihood)):
+        for _ in range(20): fn(P)
+        t0 = time.perf_counter()
+        for _ in range(200): fn(P)
+        t[nm] = 1e3 * (time.perf_counter() - t0) / 200
 dist.destroy_process_group()
-print(json.dumps({"same": same, "nan_ok": nan_ok, "ms": t}))
+print(json.dumps({"same": same, "nan_ok": nan_ok, "ms": t, "engine_mode": mode}))
 '''
 
 
 def test_sharded_objective_collective_path_on_rccl():
-    """ShardedObjective's RCCL path (pinned staging, all_gather, rank-order sum) on a 1-rank
-    nccl group in a child process: bitwise the direct objective over a carried-state chain,
-    NaN raised; prints the per-call cost of the collective path"""
+    """ShardedObjective's two RCCL paths on a 1-rank nccl group in a child process -- the
+    engine's own (ggp_comm_attach: partial, all-gather and rank-order sum on the engine's stream)
+    and torch's (pinned staging, all_gather_into_tensor, combine_partials): bitwise the direct
+    objective over a carried-state chain, NaN raised with this rank's cell; prints the per-call
+    cost of each"""
     import socket
     import subprocess
     import sys
@@ -565,4 +571,5 @@ def test_sharded_objective_collective_path_on_rccl():
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     out = json.loads(r.stdout.strip().splitlines()[-1])
     print("collective path ms/call:", out["ms"])
+    assert out["engine_mode"] == {"engine": True, "torch": False}
     assert out["same"] and out["nan_ok"]
