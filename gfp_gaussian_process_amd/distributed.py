@@ -6,6 +6,10 @@ row count (ties: critical-path length, then tree order).  Each rank keeps its sh
 device-resident data and carried root state; one objective call = every rank evaluates
 its shard, then ONE collective exchanges one double per rank (all_gather), and the
 partials are summed in rank order so the result is bitwise reproducible run to run.
+With an nccl group the collective runs inside the engine (include/ggp.h ggp_comm_attach:
+partial, RCCL all-gather and rank-order sum enqueued on the engine's stream behind the
+evaluation); otherwise (gloo, or engine_comm=False) through torch's all_gather_into_tensor.
+Both give the same bits.
 The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
 Scan samples and optimiser steps stay sequential (carried state), only the forest is
 parallel.
@@ -122,14 +126,27 @@ class ShardedObjective:
         self._h_recv_np = self._h_recv.numpy()
 
     def _attach_engine(self, torch, dist, group):
-        from .forest import comm_unique_id
+        """join the engine's RCCL communicator; every rank first checks it can (the library and
+        its entry points) and the group agrees, so a rank that cannot never leaves the others
+        waiting in ncclCommInitRank: then all keep torch's all_gather path"""
+        import sys
+        from .forest import GGPError, comm_unique_id
         lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
         lib = lib if os.path.exists(lib) else None      # the RCCL torch loaded: one RCCL per process
         rank = dist.get_rank(group)
         src = 0 if group is None else dist.get_global_rank(group, 0)
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(comm_unique_id(lib)), dtype=torch.uint8))
+        try:
+            mine = comm_unique_id(lib)
+            ok = 1
+        except GGPError as e:
+            print(f"ShardedObjective: engine RCCL unavailable on rank {rank} ({e}); torch's all_gather instead",
+                  file=sys.stderr)
+            mine, ok = bytes(128), 0
+        flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if int(flag.item()) == 0:
+            return
+        uid = torch.frombuffer(bytearray(mine), dtype=torch.uint8).to("cuda")
         dist.broadcast(uid, src=src, group=group)
         self.f.comm_attach(self.world, rank, bytes(uid.cpu().numpy().tobytes()), lib)
         self.engine = True
