@@ -121,7 +121,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--trees", type=int, default=1000, help="trees per GPU")
     ap.add_argument("--rows", type=int, default=200, help="rows per tree")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group", "wave"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group", "wave", "pair"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--large-trees", type=int, default=12500,

@@ -15,7 +15,7 @@ LIB_DIR = os.path.join(_PKG, "lib")
 GGP_OK, GGP_EINVAL, GGP_ENAN, GGP_EDEV, GGP_ENOMEM = 0, 1, 2, 3, 4
 N_PARAMS = 11
 STATE = 20
-KERNELS = {"auto": 0, "lane": 1, "group": 2, "wave": 3}
+KERNELS = {"auto": 0, "lane": 1, "group": 2, "wave": 3, "pair": 4}
 
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

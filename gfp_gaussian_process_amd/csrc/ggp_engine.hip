@@ -205,6 +205,219 @@ __global__ __launch_bounds__(64) void k_loglik_level_batch(DevForest F, const do
                      cell_nan + pt * n_cells, s_tab, lane);
 }
 
+// ------------------------------------------------------------------------------------------
+// LANE-PAIR schedule (k_loglik_pair<CPW>): the lane schedule with every step of a cell split
+// over the two waves of a workgroup.  Lane l of both waves holds cell l (CPW cells per
+// workgroup); wave 0 forms exponentials [0, 37), Dawson values [0, 7), integrals [0, 23) and the
+// output group 1 (ggp::outputs<1>), wave 1 the rest; each half goes through LDS to the other
+// wave (three workgroup barriers per step), and both waves run the measurement update.  Every
+// value is the lane schedule's expression (the same task bodies, index sequences and outputs
+// text), so results are bitwise the lane schedule's; a step issues ~half the lane schedule's
+// instructions per wave, for levels too small to fill the SIMDs with 64-cell lane waves
+// (C3, C4 shards) where the lane schedule waits on its ~4.1k-instruction step.
+// ------------------------------------------------------------------------------------------
+namespace pair {
+constexpr int kXS = 37;   // exponentials [0, kXS) in wave 0
+constexpr int kDS = 7;    // Dawson values [0, kDS) in wave 0
+constexpr int kIS = 23;   // integrals [0, kIS) in wave 0
+constexpr int kO0 = 6;    // group-1 covariances through LDS (C[0], C[1], C[2], C[3], C[6], C[10])
+constexpr int kO1 = 4;    // group-2 covariances (C[5], C[7], C[11], C[15])
+
+template <int OFF, size_t... J>
+GGP_DEV void exps(const ggp::Step &S, double *X, std::index_sequence<J...>)
+{
+    ((X[OFF + J] = ggp::exp_body(S, ggp::XTask{ggp::kXT[OFF + J].kind, ggp::kXT[OFF + J].iB, ggp::kXT[OFF + J].ic,
+                                               ggp::kXT[OFF + J].it})), ...);
+}
+template <int OFF, size_t... J>
+GGP_DEV void dawsons(const ggp::Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
+{
+    ((Dw[OFF + J] = ggp_dawson_tab(ggp::zval(S, ggp::kDT[OFF + J].iB, ggp::kDT[OFF + J].it), tab)), ...);
+}
+template <int OFF, class XA, class DA, class PA, size_t... J>
+GGP_DEV void taus(const ggp::Step &S, const XA &X, const DA &Dw, const PA &PW, double *I, std::index_sequence<J...>)
+{
+    ((I[OFF + J] = ggp::lane_tau<(int)(OFF + J)>(S, X, Dw, PW)), ...);
+}
+
+// one propagation (propagate_lane's order) by wave W of the pair; Xl/Dl/Il/Ol: LDS [slot][CPW]
+template <int W, int CPW>
+GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, const double *tab, double *Xl,
+                       double *Dl, double *Il, double *Ol, const int lane)
+{
+    constexpr int X0 = W == 0 ? 0 : kXS, XN = W == 0 ? kXS : ggp::NXT - kXS;
+    constexpr int XO = W == 0 ? kXS : 0, XON = W == 0 ? ggp::NXT - kXS : kXS;   // the other wave's
+    constexpr int D0 = W == 0 ? 0 : kDS, DN = W == 0 ? kDS : ggp::ND - kDS;
+    constexpr int DO = W == 0 ? kDS : 0, DON = W == 0 ? ggp::ND - kDS : kDS;
+    constexpr int I0 = W == 0 ? 0 : kIS, IN = W == 0 ? kIS : ggp::NI - kIS;
+    constexpr int IO = W == 0 ? kIS : 0, ION = W == 0 ? ggp::NI - kIS : kIS;
+    ggp::Step S;
+    ggp::step_init(S, m, C, t, P);
+    double X[ggp::NX], Dw[ggp::ND];
+    exps<X0>(S, X, std::make_index_sequence<XN>{});
+    X[ggp::X_ONE] = 1.0;
+    dawsons<D0>(S, Dw, tab, std::make_index_sequence<DN>{});
+    const bool own = lane < CPW;   // lanes past CPW hold no cell and store nothing
+    if (own) {
+#pragma unroll
+        for (int j = 0; j < XN; ++j) Xl[(X0 + j) * CPW + lane] = X[X0 + j];
+#pragma unroll
+        for (int j = 0; j < DN; ++j) Dl[(D0 + j) * CPW + lane] = Dw[D0 + j];
+    }
+    __syncthreads();
+    const int ln = own ? lane : 0;
+#pragma unroll
+    for (int j = 0; j < XON; ++j) X[XO + j] = Xl[(XO + j) * CPW + ln];
+#pragma unroll
+    for (int j = 0; j < DON; ++j) Dw[DO + j] = Dl[(DO + j) * CPW + ln];
+    double PW[ggp::NPW];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        PW[q] = ggp::pow_task(S, q);
+        PW[3 + q] = ggp::frcp(PW[q]);   // rdiv seeds
+    }
+    double I[ggp::NI];
+    taus<I0>(S, X, Dw, PW, I, std::make_index_sequence<IN>{});
+    if (own) {
+#pragma unroll
+        for (int j = 0; j < IN; ++j) Il[(I0 + j) * CPW + lane] = I[I0 + j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ION; ++j) I[IO + j] = Il[(IO + j) * CPW + ln];
+    double Co[16];
+    ggp::outputs<W == 0 ? 1 : 2>(S, I, X, m, Co);   // the means in both waves, one group each
+    constexpr int k0[kO0] = {0, 1, 2, 3, 6, 10}, k1[kO1] = {5, 7, 11, 15};
+    if (W == 0 && own) {
+#pragma unroll
+        for (int k = 0; k < kO0; ++k) Ol[k * CPW + lane] = Co[k0[k]];
+    } else if (W == 1 && own) {
+#pragma unroll
+        for (int k = 0; k < kO1; ++k) Ol[(kO0 + k) * CPW + lane] = Co[k1[k]];
+    }
+    __syncthreads();
+    if (W == 0) {
+#pragma unroll
+        for (int k = 0; k < kO1; ++k) Co[k1[k]] = Ol[(kO0 + k) * CPW + ln];
+    } else {
+#pragma unroll
+        for (int k = 0; k < kO0; ++k) Co[k0[k]] = Ol[k * CPW + ln];
+    }
+    Co[4] = Co[1]; Co[8] = Co[2]; Co[12] = Co[3]; Co[9] = Co[6]; Co[13] = Co[7]; Co[14] = Co[11];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) C[k] = Co[k];
+}
+}  // namespace pair
+
+template <int CPW>
+__global__ __launch_bounds__(128) void k_loglik_pair(DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n,
+                                                     double *__restrict__ state, double *__restrict__ cell_ll,
+                                                     int32_t *__restrict__ cell_nan)
+{
+    __shared__ double s_tab[kDawsonTab];
+    __shared__ double s_x[ggp::NXT * CPW], s_d[ggp::ND * CPW], s_i[ggp::NI * CPW],
+        s_o[(pair::kO0 + pair::kO1) * CPW];
+    __shared__ int s_rows[64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w == 0) load_dawson_table(s_tab, lane);
+    const int i = blockIdx.x * CPW + lane;
+    const bool valid = lane < CPW && i < n;
+    const double *p = P.p;
+    const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    int c = 0, nrows = 0;
+    int64_t r0 = 0;
+    double m[4] = {0, 0, 0, 0}, C[16] = {0};
+    double dt = 0.0;
+    bool pending = false, divide = false;
+    if (valid) {
+        c = cells[i];
+        r0 = F.row_off[c];
+        nrows = (int)(F.row_off[c + 1] - r0);
+        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        divide = pending;
+    }
+    // lanes without a cell propagate lane 0's state (never stored): finite operands, so they
+    // take none of the Dawson's rare branches
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double v = __shfl(m[q], 0);
+        m[q] = valid ? m[q] : v;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const double v = __shfl(C[q], 0);
+        C[q] = valid ? C[q] : v;
+    }
+    {
+        const double v = __shfl(dt, 0);
+        dt = valid ? dt : v;
+    }
+    // the steps both waves take: the longest cell of the workgroup (a barrier count both share)
+    if (w == 0) s_rows[lane] = nrows;
+    __syncthreads();
+    int kmax = 0;
+    for (int l = 0; l < CPW; ++l) kmax = max(kmax, s_rows[l]);
+    double cl = 0.0;
+    int nan_row = kNanNone;
+    bool live = valid && nrows > 0;
+    for (int k = 0; k < kmax; ++k) {
+        const int64_t r = r0 + k;
+        double y_l = 0.0, y_f = 0.0, t_next = 0.0;
+        if (live) {
+            y_l = F.logl[r];
+            y_f = F.fp[r];
+            if (k + 1 < nrows) t_next = F.time[r + 1];
+        }
+        // both waves decide alike: the same cells, the same flags
+        if (__builtin_amdgcn_ballot_w64(live && pending)) {
+            double mn[4], Cn[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) mn[q] = m[q];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Cn[q] = C[q];
+            if (w == 0)
+                pair::propagate<0, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
+            else
+                pair::propagate<1, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
+            if (live && pending) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = mn[q];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) C[q] = Cn[q];
+                if (divide) {
+                    ggp::division_map(m, C, p[9], p[10], F.binomial, F.log2);
+                    divide = false;
+                }
+            }
+        }
+        if (live) {   // likelihood.h:53-69, as loglik_lane_cell
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
+            ggp_innov v;
+            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+            cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
+            if (cl != cl) {
+                nan_row = k;
+                live = false;
+            } else {
+                ggp_posterior(m, C, x0, x1, v);
+                pending = k + 1 < nrows;
+                if (pending) dt = t_next - F.time[r];
+                live = k + 1 < nrows;
+            }
+        }
+    }
+    if (valid && w == 0) {
+        double *st = state + (size_t)20 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st[q] = m[q];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) st[4 + q] = C[q];
+        cell_ll[F.dfs_rank[c]] = cl;
+        cell_nan[F.dfs_rank[c]] = nan_row;
+    }
+}
+
 // every batch point starts from the handle's carried state: dst[pt] = src, for pt < n_pts
 __global__ __launch_bounds__(256) void k_replicate(const double *__restrict__ src, int64_t n,
                                                    double *__restrict__ dst, int64_t n_pts)
@@ -1556,8 +1769,10 @@ struct Shard {
     int kernel_pref = GGP_KERNEL_AUTO;
     int auto_small = GGP_KERNEL_WAVE;   // auto's schedule for small levels
     int64_t wave_max_cells = 5120;    // auto: wave schedule for levels up to this size
-    int64_t group_max_cells = 8192;   // auto: group schedule above that, up to this size
+    int64_t group_max_cells = 8192;   // auto with GGP_AUTO_SMALL=group: group schedule above that
+    int64_t pair_max_cells = 32768;   // auto: lane-pair schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
+    int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -1689,10 +1904,10 @@ int lane_cpw(const Shard *f) { return f->tune_lane_cpw > 0 ? f->tune_lane_cpw : 
 // above that the lane schedule
 int level_kind(const Shard *f, int64_t n)
 {
-    return f->kernel_pref != GGP_KERNEL_AUTO ? f->kernel_pref
-           : n <= f->wave_max_cells          ? f->auto_small
-           : n <= f->group_max_cells         ? GGP_KERNEL_GROUP
-                                             : GGP_KERNEL_LANE;
+    if (f->kernel_pref != GGP_KERNEL_AUTO) return f->kernel_pref;
+    if (n <= f->wave_max_cells) return f->auto_small;
+    if (f->auto_small == GGP_KERNEL_GROUP && n <= f->group_max_cells) return GGP_KERNEL_GROUP;
+    return n <= f->pair_max_cells ? GGP_KERNEL_PAIR : GGP_KERNEL_LANE;
 }
 
 int launch_levels(Shard *f, const ggp_params &P)
@@ -1738,6 +1953,17 @@ int launch_levels(Shard *f, const ggp_params &P)
                                (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
+        } else if (kind == GGP_KERNEL_PAIR) {
+            const int cpw = f->tune_pair_cpw;
+            const int blocks = (n + cpw - 1) / cpw;
+            if (cpw == 32)
+                hipLaunchKernelGGL(k_loglik_pair<32>, dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                                   f->d_state, f->d_cell_ll, f->d_cell_nan);
+            else
+                hipLaunchKernelGGL(k_loglik_pair<64>, dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                                   f->d_state, f->d_cell_ll, f->d_cell_nan);
+            f->kernel_used = GGP_KERNEL_PAIR;
+            f->last_code = GGP_KERNEL_PAIR << 8 | cpw;
         } else if (kind == GGP_KERNEL_GROUP) {
             // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
@@ -1963,6 +2189,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     f->n_cu = dev->n_cu;
     f->wave_max_cells = (int64_t)f->n_cu * 4 * 5;   // r08 scan: wave ahead of group up to ~5 cells/SIMD
     f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
+    f->pair_max_cells = (int64_t)f->n_cu * 64 * 2;   // r13 scan: two rounds of 64-cell pair workgroups
     if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
     if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
@@ -1971,6 +2198,8 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         f->tune_group_cpw = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_PAIR_CPW")) f->tune_pair_cpw = atoi(e) == 32 ? 32 : 64;
+    if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);
@@ -2551,7 +2780,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
 {
     if (!d || !out) { g_last_err = "null argument"; return GGP_EINVAL; }
     *out = nullptr;
-    if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_WAVE) {
+    if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_PAIR) {
         g_last_err = "ggp_forest_create: unknown kernel policy";
         return GGP_EINVAL;
     }

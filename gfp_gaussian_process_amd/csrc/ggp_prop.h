@@ -523,7 +523,10 @@ GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const P
 }
 
 // ---- the outputs: new mean and covariance (mean_cov_model.h:73-208) -------------------
-template <class IA, class XA>
+// PARTS selects the output groups a caller forms (the lane-pair schedule splits them over two
+// waves): 1 = cov_xg, cov_xl, cov_xq, cov_gl, cov_xx, cov_ll; 2 = cov_gq, cov_gg, cov_lq, cov_qq;
+// the means always.  Outputs of a group not formed are left 0.
+template <int PARTS = 3, class IA, class XA>
 GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
 {
     const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
@@ -549,7 +552,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
     nm[3] = mq + (bq - mq) * egq;
 
     double nxg = 0, nxl = 0, nxq = 0, ngl = 0, nxx = 0, nll = 0, ngq = 0, ngg = 0, nlq = 0, nqq = 0;
-    {
+    if constexpr ((PARTS & 1) != 0) {
     // cov_xg (mean_cov_model.h:97-115)
     nxg =
         rdiv(bg * bx, ebt, r_ebt) + rdiv(Cxg, ebt, r_ebt) + rdiv(bg * bl, ebt_gl, r_ebt_gl)
@@ -595,7 +598,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
           + S.k_xx * (2 * gl * t - 3 + 4 * egl - (egl * egl));
     nll = Cll * (egl * egl) + S.k_ll * (1 - (egl * egl));
     }
-    {
+    if constexpr ((PARTS & 2) != 0) {
     // cov_gq (mean_cov_model.h:183-196)
     ngq =
         rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)

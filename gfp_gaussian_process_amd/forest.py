@@ -365,6 +365,8 @@ def kernel_name(code: int) -> str:
         return "k_loglik_level"
     if kind == N.KERNELS["wave"]:
         return "k_loglik_wave"
+    if kind == N.KERNELS["pair"]:
+        return f"k_loglik_pair<{lanes}>"
     return f"k_loglik_group<{lanes}>"
 
 

@@ -96,18 +96,23 @@ typedef struct {
  * a fixed pairwise tree on the host.  So every result (total, NaN location, -p rows, joints,
  * carried state) has the same bits for any device list -- 8 GPUs, or N logical shards on one. */
 
-#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 5 cells per SIMD, GROUP up to
-                                 8, LANE above (measured crossovers)       */
+#define GGP_KERNEL_AUTO 0     /* per level: WAVE up to 5 cells per SIMD, PAIR up to
+                                 2 x 64 cells per CU, LANE above (measured crossovers,
+                                 DESIGN.md); GGP_AUTO_SMALL=group: GROUP, GROUP, PAIR,
+                                 LANE -- every schedule bitwise equal to LANE         */
 #define GGP_KERNEL_LANE 1     /* one lane per cell (throughput)                      */
 #define GGP_KERNEL_GROUP 2    /* G lanes per cell (latency); bitwise equal to LANE   */
 #define GGP_KERNEL_WAVE 3     /* one wave per cell, table-driven outputs (latency);
                                  agrees with LANE/GROUP to ~1e-10, not bitwise        */
+#define GGP_KERNEL_PAIR 4     /* one lane per cell, each step split over two waves
+                                 (mid-size levels); bitwise equal to LANE             */
 /* Launch form (per shard, fixed at creation): when every level takes the wave schedule and the
  * shard has at most as many leaves as the device holds wave blocks, an evaluation is ONE launch
  * (a block per root-to-leaf path, the sum formed in-launch); otherwise one launch per level plus
  * a reduction.  Both give the same bits.  Environment (read at creation, tuning only):
  * GGP_WAVE_PATHS_MAX (paths allowed in one launch; 0 = always level launches),
- * GGP_WAVE_MAX_CELLS / GGP_GROUP_MAX_CELLS (auto's thresholds), GGP_AUTO_SMALL=group. */
+ * GGP_WAVE_MAX_CELLS / GGP_GROUP_MAX_CELLS / GGP_PAIR_MAX_CELLS (auto's thresholds),
+ * GGP_AUTO_SMALL=group, GGP_PAIR_CPW (32: 32 cells per lane-pair workgroup). */
 
 int ggp_forest_create(const ggp_forest_desc *desc, ggp_forest **out);
 void ggp_forest_destroy(ggp_forest *f);

@@ -34,8 +34,9 @@ def example_forests(example_paths):
 
 
 # every schedule against the oracle: lane (throughput), group (latency, bitwise = lane), wave
-# (latency; outputs summed in another order and four exp(c) formed as products, ~1e-10)
-KERNELS = ["lane", "group", "wave"]
+# (latency; outputs summed in another order and four exp(c) formed as products, ~1e-10), pair
+# (mid-size levels, a step over two waves, bitwise = lane)
+KERNELS = ["lane", "group", "wave", "pair"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -251,17 +252,44 @@ def test_baseline_size_properties():
 
 
 @pytest.mark.parametrize("which", ["example", "synthetic", "ragged"])
-def test_lane_and_group_schedules_bitwise_equal(example_forests, which):
-    """the two schedules run the same task expressions (csrc/ggp_prop.h): identical bits"""
+@pytest.mark.parametrize("other", ["group", "pair", "pair32"])
+def test_lane_group_pair_schedules_bitwise_equal(example_forests, which, other, monkeypatch):
+    """the schedules run the same task expressions (csrc/ggp_prop.h): identical bits (pair32:
+    the lane-pair schedule with 32 cells per workgroup, half its lanes empty)"""
     import gfp_gaussian_process_amd as g
     hf = {"example": lambda: example_forests[("scaled", "binomial")],
           "synthetic": lambda: g.HostForest.synthetic(300, 40),
           "ragged": _ragged_roots}[which]()
     P = CONFIGS[0][2]
-    lane, group = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel="group")
+    monkeypatch.setenv("GGP_PAIR_CPW", "32" if other == "pair32" else "64")
+    lane, o = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel=other.rstrip("32"))
     for _ in range(3):
-        assert lane.total_likelihood(P) == group.total_likelihood(P)
-    assert np.array_equal(lane.state(), group.state())
+        assert lane.total_likelihood(P) == o.total_likelihood(P)
+    assert np.array_equal(lane.state(), o.state())
+
+
+def test_pair_schedule_c4_shard_bitwise_and_auto():
+    """a C4-shard-sized forest (12.5k trees x 200 rows): auto takes the lane-pair schedule for
+    both levels (12.5k and 25k cells), bitwise the lane schedule over a chain, and a NaN is
+    located as the lane schedule locates it"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(12500, 200)
+    P = CONFIGS[0][2]
+    auto, lane = g.Forest(hf), g.Forest(hf, kernel="lane")
+    for _ in range(2):
+        assert auto.total_likelihood(P) == lane.total_likelihood(P)
+    assert np.array_equal(auto.state(), lane.state())
+    auto.enable_profile()
+    auto.total_likelihood(P)
+    assert all(k.startswith("k_loglik_pair") for k in auto.launch_profile()[2])
+    bad = list(P)
+    bad[2] = -1.0
+    errs = []
+    for f in (g.Forest(hf), g.Forest(hf, kernel="lane")):
+        with pytest.raises(g.LikelihoodIsNan) as e:
+            f.total_likelihood(bad)
+        errs.append((e.value.cell, e.value.row))
+    assert errs[0] == errs[1]
 
 
 # ------------------------------------------------------------------------------------------
