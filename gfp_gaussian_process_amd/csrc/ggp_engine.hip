@@ -206,20 +206,17 @@ __global__ __launch_bounds__(64) void k_loglik_level_batch(DevForest F, const do
 }
 
 // ------------------------------------------------------------------------------------------
-// LANE-PAIR schedule (k_loglik_pair<CPW>): the lane schedule with every step of a cell split
-// over the two waves of a workgroup.  Lane l of both waves holds cell l (CPW cells per
-// workgroup); wave 0 forms exponentials [0, 37), Dawson values [0, 7), integrals [0, 23) and the
-// output group 1 (ggp::outputs<1>), wave 1 the rest; each half goes through LDS to the other
-// wave (three workgroup barriers per step), and both waves run the measurement update.  Every
-// value is the lane schedule's expression (the same task bodies, index sequences and outputs
-// text), so results are bitwise the lane schedule's; a step issues ~half the lane schedule's
-// instructions per wave, for levels too small to fill the SIMDs with 64-cell lane waves
-// (C3, C4 shards) where the lane schedule waits on its ~4.1k-instruction step.
+// LANE-PAIR schedule (k_loglik_pair<Q, CPW>): the lane schedule with every step of a cell split
+// over the Q = 2 or 4 waves of a workgroup.  Lane l of every wave holds cell l (CPW cells per
+// workgroup); wave w forms the w-th Q-th of the exponentials, of the Dawson values and of the
+// integrals, and waves 0 and 1 one output group each (ggp::outputs<1>, <2>); each part goes
+// through LDS to the other waves (three workgroup barriers per step), and every wave runs the
+// measurement update.  Every value is the lane schedule's expression (the same task bodies,
+// index sequences and outputs text), so results are bitwise the lane schedule's; a step issues
+// ~1/Q of the lane schedule's task work per wave, for levels too small to fill the SIMDs with
+// 64-cell lane waves (C3, C4 shards), where the lane schedule waits on its ~4.1k-instruction step.
 // ------------------------------------------------------------------------------------------
 namespace pair {
-constexpr int kXS = 37;   // exponentials [0, kXS) in wave 0
-constexpr int kDS = 7;    // Dawson values [0, kDS) in wave 0
-constexpr int kIS = 23;   // integrals [0, kIS) in wave 0
 constexpr int kO0 = 6;    // group-1 covariances through LDS (C[0], C[1], C[2], C[3], C[6], C[10])
 constexpr int kO1 = 4;    // group-2 covariances (C[5], C[7], C[11], C[15])
 
@@ -240,17 +237,33 @@ GGP_DEV void taus(const ggp::Step &S, const XA &X, const DA &Dw, const PA &PW, d
     ((I[OFF + J] = ggp::lane_tau<(int)(OFF + J)>(S, X, Dw, PW)), ...);
 }
 
-// one propagation (propagate_lane's order) by wave W of the pair; Xl/Dl/Il/Ol: LDS [slot][CPW]
-template <int W, int CPW>
+// wave W's part [N W / Q, N (W + 1) / Q) of N tasks: own values to LDS (slot-major, [slot][CPW])
+// before the barrier, the other waves' into the register array after it
+template <int N, int W, int Q, int CPW>
+GGP_DEV void put_part(const double *v, double *L, const int lane)
+{
+    constexpr int lo = N * W / Q, hi = N * (W + 1) / Q;
+#pragma unroll
+    for (int j = lo; j < hi; ++j) L[j * CPW + lane] = v[j];
+}
+template <int N, int W, int Q, int CPW>
+GGP_DEV void get_rest(double *v, const double *L, const int lane)
+{
+    constexpr int lo = N * W / Q, hi = N * (W + 1) / Q;
+#pragma unroll
+    for (int j = 0; j < lo; ++j) v[j] = L[j * CPW + lane];
+#pragma unroll
+    for (int j = hi; j < N; ++j) v[j] = L[j * CPW + lane];
+}
+
+// one propagation (propagate_lane's order) by wave W of Q; Xl/Dl/Il/Ol: LDS [slot][CPW]
+template <int W, int Q, int CPW>
 GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, const double *tab, double *Xl,
                        double *Dl, double *Il, double *Ol, const int lane)
 {
-    constexpr int X0 = W == 0 ? 0 : kXS, XN = W == 0 ? kXS : ggp::NXT - kXS;
-    constexpr int XO = W == 0 ? kXS : 0, XON = W == 0 ? ggp::NXT - kXS : kXS;   // the other wave's
-    constexpr int D0 = W == 0 ? 0 : kDS, DN = W == 0 ? kDS : ggp::ND - kDS;
-    constexpr int DO = W == 0 ? kDS : 0, DON = W == 0 ? ggp::ND - kDS : kDS;
-    constexpr int I0 = W == 0 ? 0 : kIS, IN = W == 0 ? kIS : ggp::NI - kIS;
-    constexpr int IO = W == 0 ? kIS : 0, ION = W == 0 ? ggp::NI - kIS : kIS;
+    constexpr int X0 = ggp::NXT * W / Q, XN = ggp::NXT * (W + 1) / Q - X0;
+    constexpr int D0 = ggp::ND * W / Q, DN = ggp::ND * (W + 1) / Q - D0;
+    constexpr int I0 = ggp::NI * W / Q, IN = ggp::NI * (W + 1) / Q - I0;
     ggp::Step S;
     ggp::step_init(S, m, C, t, P);
     double X[ggp::NX], Dw[ggp::ND];
@@ -258,18 +271,14 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
     X[ggp::X_ONE] = 1.0;
     dawsons<D0>(S, Dw, tab, std::make_index_sequence<DN>{});
     const bool own = lane < CPW;   // lanes past CPW hold no cell and store nothing
+    const int ln = own ? lane : 0;
     if (own) {
-#pragma unroll
-        for (int j = 0; j < XN; ++j) Xl[(X0 + j) * CPW + lane] = X[X0 + j];
-#pragma unroll
-        for (int j = 0; j < DN; ++j) Dl[(D0 + j) * CPW + lane] = Dw[D0 + j];
+        put_part<ggp::NXT, W, Q, CPW>(X, Xl, lane);
+        put_part<ggp::ND, W, Q, CPW>(Dw, Dl, lane);
     }
     __syncthreads();
-    const int ln = own ? lane : 0;
-#pragma unroll
-    for (int j = 0; j < XON; ++j) X[XO + j] = Xl[(XO + j) * CPW + ln];
-#pragma unroll
-    for (int j = 0; j < DON; ++j) Dw[DO + j] = Dl[(DO + j) * CPW + ln];
+    get_rest<ggp::NXT, W, Q, CPW>(X, Xl, ln);
+    get_rest<ggp::ND, W, Q, CPW>(Dw, Dl, ln);
     double PW[ggp::NPW];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -278,15 +287,11 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
     }
     double I[ggp::NI];
     taus<I0>(S, X, Dw, PW, I, std::make_index_sequence<IN>{});
-    if (own) {
-#pragma unroll
-        for (int j = 0; j < IN; ++j) Il[(I0 + j) * CPW + lane] = I[I0 + j];
-    }
+    if (own) put_part<ggp::NI, W, Q, CPW>(I, Il, lane);
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < ION; ++j) I[IO + j] = Il[(IO + j) * CPW + ln];
+    get_rest<ggp::NI, W, Q, CPW>(I, Il, ln);
     double Co[16];
-    ggp::outputs<W == 0 ? 1 : 2>(S, I, X, m, Co);   // the means in both waves, one group each
+    ggp::outputs<W == 0 ? 1 : W == 1 ? 2 : 0>(S, I, X, m, Co);   // the means in every wave
     constexpr int k0[kO0] = {0, 1, 2, 3, 6, 10}, k1[kO1] = {5, 7, 11, 15};
     if (W == 0 && own) {
 #pragma unroll
@@ -296,10 +301,11 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
         for (int k = 0; k < kO1; ++k) Ol[(kO0 + k) * CPW + lane] = Co[k1[k]];
     }
     __syncthreads();
-    if (W == 0) {
+    if (W != 1) {
 #pragma unroll
         for (int k = 0; k < kO1; ++k) Co[k1[k]] = Ol[(kO0 + k) * CPW + ln];
-    } else {
+    }
+    if (W != 0) {
 #pragma unroll
         for (int k = 0; k < kO0; ++k) Co[k0[k]] = Ol[k * CPW + ln];
     }
@@ -309,11 +315,12 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
 }
 }  // namespace pair
 
-template <int CPW>
-__global__ __launch_bounds__(128) void k_loglik_pair(DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n,
-                                                     double *__restrict__ state, double *__restrict__ cell_ll,
-                                                     int32_t *__restrict__ cell_nan)
+template <int Q, int CPW>
+__global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n,
+                                                        double *__restrict__ state, double *__restrict__ cell_ll,
+                                                        int32_t *__restrict__ cell_nan)
 {
+    static_assert(Q == 2 || Q == 4, "two or four waves per workgroup");
     __shared__ double s_tab[kDawsonTab];
     __shared__ double s_x[ggp::NXT * CPW], s_d[ggp::ND * CPW], s_i[ggp::NI * CPW],
         s_o[(pair::kO0 + pair::kO1) * CPW];
@@ -352,7 +359,7 @@ __global__ __launch_bounds__(128) void k_loglik_pair(DevForest F, ggp_params P, 
         const double v = __shfl(dt, 0);
         dt = valid ? dt : v;
     }
-    // the steps both waves take: the longest cell of the workgroup (a barrier count both share)
+    // the steps every wave takes: the longest cell of the workgroup (a barrier count all share)
     if (w == 0) s_rows[lane] = nrows;
     __syncthreads();
     int kmax = 0;
@@ -368,17 +375,19 @@ __global__ __launch_bounds__(128) void k_loglik_pair(DevForest F, ggp_params P, 
             y_f = F.fp[r];
             if (k + 1 < nrows) t_next = F.time[r + 1];
         }
-        // both waves decide alike: the same cells, the same flags
+        // every wave decides alike: the same cells, the same flags
         if (__builtin_amdgcn_ballot_w64(live && pending)) {
             double mn[4], Cn[16];
 #pragma unroll
             for (int q = 0; q < 4; ++q) mn[q] = m[q];
 #pragma unroll
             for (int q = 0; q < 16; ++q) Cn[q] = C[q];
-            if (w == 0)
-                pair::propagate<0, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
-            else
-                pair::propagate<1, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
+            switch (w) {
+            case 0: pair::propagate<0, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
+            case 1: pair::propagate<1, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
+            case 2: pair::propagate<2 % Q, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
+            default: pair::propagate<3 % Q, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
+            }
             if (live && pending) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) m[q] = mn[q];
@@ -1773,6 +1782,7 @@ struct Shard {
     int64_t pair_max_cells = 32768;   // auto: lane-pair schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
+    int tune_pair_q = 0;                         // GGP_PAIR_Q: waves per cell (2, 4; 0 = by level size)
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -1954,16 +1964,24 @@ int launch_levels(Shard *f, const ggp_params &P)
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
         } else if (kind == GGP_KERNEL_PAIR) {
+            // four waves per cell while one 64-cell workgroup per CU holds the level, else two
+            const int q = f->tune_pair_q > 0 ? f->tune_pair_q : (n <= (int64_t)f->n_cu * 64 ? 4 : 2);
             const int cpw = f->tune_pair_cpw;
             const int blocks = (n + cpw - 1) / cpw;
-            if (cpw == 32)
-                hipLaunchKernelGGL(k_loglik_pair<32>, dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                                   f->d_state, f->d_cell_ll, f->d_cell_nan);
+            if (q == 4 && cpw == 64)
+                hipLaunchKernelGGL((k_loglik_pair<4, 64>), dim3(blocks), dim3(256), 0, f->stream, f->F, P, f->d_level_cells + a,
+                                   n, f->d_state, f->d_cell_ll, f->d_cell_nan);
+            else if (q == 4)
+                hipLaunchKernelGGL((k_loglik_pair<4, 32>), dim3(blocks), dim3(256), 0, f->stream, f->F, P, f->d_level_cells + a,
+                                   n, f->d_state, f->d_cell_ll, f->d_cell_nan);
+            else if (cpw == 32)
+                hipLaunchKernelGGL((k_loglik_pair<2, 32>), dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a,
+                                   n, f->d_state, f->d_cell_ll, f->d_cell_nan);
             else
-                hipLaunchKernelGGL(k_loglik_pair<64>, dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                                   f->d_state, f->d_cell_ll, f->d_cell_nan);
+                hipLaunchKernelGGL((k_loglik_pair<2, 64>), dim3(blocks), dim3(128), 0, f->stream, f->F, P, f->d_level_cells + a,
+                                   n, f->d_state, f->d_cell_ll, f->d_cell_nan);
             f->kernel_used = GGP_KERNEL_PAIR;
-            f->last_code = GGP_KERNEL_PAIR << 8 | cpw;
+            f->last_code = GGP_KERNEL_PAIR << 8 | q;
         } else if (kind == GGP_KERNEL_GROUP) {
             // one cell per wave while that fits one wave per SIMD, else two (G = 32); the
             // auto threshold keeps bigger levels on the lane schedule (tools/lane_scan.py)
@@ -2200,6 +2218,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
     if (const char *e = getenv("GGP_PAIR_CPW")) f->tune_pair_cpw = atoi(e) == 32 ? 32 : 64;
     if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);

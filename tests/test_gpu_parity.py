@@ -252,17 +252,18 @@ def test_baseline_size_properties():
 
 
 @pytest.mark.parametrize("which", ["example", "synthetic", "ragged"])
-@pytest.mark.parametrize("other", ["group", "pair", "pair32"])
+@pytest.mark.parametrize("other", ["group", "pair-q2", "pair-q4", "pair-q2-c32", "pair-q4-c32"])
 def test_lane_group_pair_schedules_bitwise_equal(example_forests, which, other, monkeypatch):
-    """the schedules run the same task expressions (csrc/ggp_prop.h): identical bits (pair32:
-    the lane-pair schedule with 32 cells per workgroup, half its lanes empty)"""
+    """the schedules run the same task expressions (csrc/ggp_prop.h): identical bits (pair-qQ:
+    the lane schedule split over Q waves; -c32: 32 cells per workgroup, half its lanes empty)"""
     import gfp_gaussian_process_amd as g
     hf = {"example": lambda: example_forests[("scaled", "binomial")],
           "synthetic": lambda: g.HostForest.synthetic(300, 40),
           "ragged": _ragged_roots}[which]()
     P = CONFIGS[0][2]
-    monkeypatch.setenv("GGP_PAIR_CPW", "32" if other == "pair32" else "64")
-    lane, o = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel=other.rstrip("32"))
+    monkeypatch.setenv("GGP_PAIR_CPW", "32" if other.endswith("c32") else "64")
+    monkeypatch.setenv("GGP_PAIR_Q", "4" if "q4" in other else "2")
+    lane, o = g.Forest(hf, kernel="lane"), g.Forest(hf, kernel=other.split("-")[0])
     for _ in range(3):
         assert lane.total_likelihood(P) == o.total_likelihood(P)
     assert np.array_equal(lane.state(), o.state())
@@ -270,8 +271,8 @@ def test_lane_group_pair_schedules_bitwise_equal(example_forests, which, other, 
 
 def test_pair_schedule_c4_shard_bitwise_and_auto():
     """a C4-shard-sized forest (12.5k trees x 200 rows): auto takes the lane-pair schedule for
-    both levels (12.5k and 25k cells), bitwise the lane schedule over a chain, and a NaN is
-    located as the lane schedule locates it"""
+    both levels (12.5k cells over four waves per cell, 25k over two), bitwise the lane schedule
+    over a chain, and a NaN is located as the lane schedule locates it"""
     import gfp_gaussian_process_amd as g
     hf = g.HostForest.synthetic(12500, 200)
     P = CONFIGS[0][2]
@@ -281,7 +282,7 @@ def test_pair_schedule_c4_shard_bitwise_and_auto():
     assert np.array_equal(auto.state(), lane.state())
     auto.enable_profile()
     auto.total_likelihood(P)
-    assert all(k.startswith("k_loglik_pair") for k in auto.launch_profile()[2])
+    assert auto.launch_profile()[2] == ["k_loglik_pair<4>", "k_loglik_pair<2>"]
     bad = list(P)
     bad[2] = -1.0
     errs = []
