@@ -39,6 +39,7 @@ def outputs_text():
 
 def to_python(body):
     body = re.sub(r"//[^\n]*", "", body)
+    body = re.sub(r"if constexpr \(\(PARTS & \d\) != 0\)", "", body)
     body = body.replace("{", " ").replace("}", " ")
     stmts = [x.strip() for x in body.split(";")]
     out = []
