@@ -217,8 +217,12 @@ __global__ __launch_bounds__(64) void k_loglik_level_batch(DevForest F, const do
 // 64-cell lane waves (C3, C4 shards), where the lane schedule waits on its ~4.1k-instruction step.
 // ------------------------------------------------------------------------------------------
 namespace pair {
-constexpr int kO0 = 6;    // group-1 covariances through LDS (C[0], C[1], C[2], C[3], C[6], C[10])
-constexpr int kO1 = 4;    // group-2 covariances (C[5], C[7], C[11], C[15])
+// the output groups of ggp::outputs<PARTS> (bits 1, 2, 4, 8) and the covariance slots each forms;
+// wave w of Q forms the groups of kParts[Q / 4][w], the others come through LDS slot kOSlot
+constexpr int kOGroups[4][6] = {{1, -1}, {0, 2, 3, 6, 10, -1}, {7, 11, 15, -1}, {5, -1}};
+constexpr int kOSlot[16] = {1, 0, 2, 3, -1, 9, 4, 6, -1, -1, 5, 7, -1, -1, -1, 8};
+constexpr int kOSlots = 10;
+constexpr int kParts[2][4] = {{1 | 2, 4 | 8, 0, 0}, {1, 2, 4, 8}};
 
 template <int OFF, size_t... J>
 GGP_DEV void exps(const ggp::Step &S, double *X, std::index_sequence<J...>)
@@ -291,24 +295,21 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
     __syncthreads();
     get_rest<ggp::NI, W, Q, CPW>(I, Il, ln);
     double Co[16];
-    ggp::outputs<W == 0 ? 1 : W == 1 ? 2 : 0>(S, I, X, m, Co);   // the means in every wave
-    constexpr int k0[kO0] = {0, 1, 2, 3, 6, 10}, k1[kO1] = {5, 7, 11, 15};
-    if (W == 0 && own) {
+    constexpr int PM = kParts[Q / 4][W];
+    ggp::outputs<PM>(S, I, X, m, Co);   // the means in every wave, this wave's output groups
+    if (own) {
 #pragma unroll
-        for (int k = 0; k < kO0; ++k) Ol[k * CPW + lane] = Co[k0[k]];
-    } else if (W == 1 && own) {
+        for (int gi = 0; gi < 4; ++gi)
+            if ((PM >> gi) & 1)
 #pragma unroll
-        for (int k = 0; k < kO1; ++k) Ol[(kO0 + k) * CPW + lane] = Co[k1[k]];
+                for (int k = 0; k < 6 && kOGroups[gi][k] >= 0; ++k) Ol[kOSlot[kOGroups[gi][k]] * CPW + lane] = Co[kOGroups[gi][k]];
     }
     __syncthreads();
-    if (W != 1) {
 #pragma unroll
-        for (int k = 0; k < kO1; ++k) Co[k1[k]] = Ol[(kO0 + k) * CPW + ln];
-    }
-    if (W != 0) {
+    for (int gi = 0; gi < 4; ++gi)
+        if (!((PM >> gi) & 1))
 #pragma unroll
-        for (int k = 0; k < kO0; ++k) Co[k0[k]] = Ol[k * CPW + ln];
-    }
+            for (int k = 0; k < 6 && kOGroups[gi][k] >= 0; ++k) Co[kOGroups[gi][k]] = Ol[kOSlot[kOGroups[gi][k]] * CPW + ln];
     Co[4] = Co[1]; Co[8] = Co[2]; Co[12] = Co[3]; Co[9] = Co[6]; Co[13] = Co[7]; Co[14] = Co[11];
 #pragma unroll
     for (int k = 0; k < 16; ++k) C[k] = Co[k];
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
     static_assert(Q == 2 || Q == 4, "two or four waves per workgroup");
     __shared__ double s_tab[kDawsonTab];
     __shared__ double s_x[ggp::NXT * CPW], s_d[ggp::ND * CPW], s_i[ggp::NI * CPW],
-        s_o[(pair::kO0 + pair::kO1) * CPW];
+        s_o[pair::kOSlots * CPW];
     __shared__ int s_rows[64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (w == 0) load_dawson_table(s_tab, lane);

@@ -523,10 +523,10 @@ GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const P
 }
 
 // ---- the outputs: new mean and covariance (mean_cov_model.h:73-208) -------------------
-// PARTS selects the output groups a caller forms (the lane-pair schedule splits them over two
-// waves): 1 = cov_xg, cov_xl, cov_xq, cov_gl, cov_xx, cov_ll; 2 = cov_gq, cov_gg, cov_lq, cov_qq;
-// the means always.  Outputs of a group not formed are left 0.
-template <int PARTS = 3, class IA, class XA>
+// PARTS selects the output groups a caller forms (the lane-pair schedule splits them over its
+// waves): 1 = cov_xg; 2 = cov_xl, cov_xq, cov_gl, cov_xx, cov_ll; 4 = cov_gq, cov_lq, cov_qq;
+// 8 = cov_gg; the means always.  Outputs of a group not formed are left 0.
+template <int PARTS = 15, class IA, class XA>
 GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
 {
     const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
@@ -574,7 +574,8 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
         + (-(DGL(bl * bq)) - DGL(Clq) - DGL(bq * Cxl) - DGL(bl * Cxq) - DGL(Cxl * Cxq) + DGL(bq * ml)
            + DGL(Cxq * ml) + DGL(bl * mq) + DGL(Cxl * mq) - DGL(ml * mq)) * I[Z_2B]
         - nm[1] * nm[0];
-
+    }
+    if constexpr ((PARTS & 2) != 0) {
     // cov_xl, cov_xq (mean_cov_model.h:117-123)
     nxl = S.k_xl * ((1 - egl) * (1 - egl))
                        + DGL(Cll * egl * (1 - egl)) + Cxl * egl;
@@ -598,7 +599,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
           + S.k_xx * (2 * gl * t - 3 + 4 * egl - (egl * egl));
     nll = Cll * (egl * egl) + S.k_ll * (1 - (egl * egl));
     }
-    if constexpr ((PARTS & 2) != 0) {
+    if constexpr ((PARTS & 4) != 0) {
     // cov_gq (mean_cov_model.h:183-196)
     ngq =
         rdiv(bg * bq, ebgqt, r_ebgqt) + rdiv(Cgq, ebgqt, r_ebgqt) + rdiv(bg * mq, ebt, r_ebt)
@@ -613,6 +614,11 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
         + rdiv(sq2 * I[Z_5I], gq2, r_gq2)
         - nm[1] * nm[3];
 
+    // cov_lq, cov_qq (mean_cov_model.h:202-208)
+    nlq = Clq * egl * egq;
+    nqq = S.k_qq * (1 - (egq * egq)) + Cqq * (egq * egq);
+    }
+    if constexpr ((PARTS & 8) != 0) {
     // cov_gg (mean_cov_model.h:125-170)
     const double k17 = DGQ(2 * bq * mq) + DGQ(4 * Cxq * mq) - DGQ(2 * (mq * mq));
     const double k19 = DGQ(-2 * bq * mq) - DGQ(4 * Cxq * mq) + DGQ(2 * (mq * mq));
@@ -651,10 +657,6 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
         + k17 * I[Z_4F2]
         - rdiv(sq2 * I[Z_6H2], gqq2, r_gqq2)
         - (nm[1] * nm[1]);
-
-    // cov_lq, cov_qq (mean_cov_model.h:202-208)
-    nlq = Clq * egl * egq;
-    nqq = S.k_qq * (1 - (egq * egq)) + Cqq * (egq * egq);
     }
 
 #undef DGL
