@@ -96,6 +96,7 @@ HOST_SYMBOLS = {
     "ggp_dataset_segments": (ctypes.c_int, [ctypes.c_void_p, c_int32_p, ctypes.c_int32, c_int32_p]),
     "ggp_dataset_is_binary": (ctypes.c_int, [ctypes.c_char_p]),
     "ggp_dataset_save": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "ggp_dataset_write_csv": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]),
     "ggp_dataset_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "ggp_dataset_create": (ctypes.c_int, [ctypes.c_int64, c_int64_p, c_double_p, c_double_p, c_double_p, c_int32_p,
                                           ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),

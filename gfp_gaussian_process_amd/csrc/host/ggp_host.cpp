@@ -376,6 +376,41 @@ extern "C" int ggp_dataset_is_binary(const char *path)
     return ok ? 1 : 0;
 }
 
+// ---- CSV writer: the reference's input layout, read back bit for bit ------
+extern "C" int ggp_dataset_write_csv(const ggp_dataset *d, const char *csv_path, const char *config_path)
+{
+    if (!d || !csv_path || !config_path) return fail(GGP_EINVAL, "null argument");
+    bool segmented = false;
+    for (const Cell &c : d->cells) {
+        if (c.id.empty() || remove_last_decimal(c.id) != c.id || remove_last_decimal(c.parent_id) != c.parent_id ||
+            c.id.find(',') != std::string::npos || c.parent_id.find(',') != std::string::npos)
+            return fail(GGP_EINVAL, "ggp_dataset_write_csv: id '" + c.id + "' / '" + c.parent_id +
+                                        "' would not read back as itself");
+        for (int32_t s : c.segment) segmented = segmented || s != 0;
+    }
+    std::FILE *f = std::fopen(csv_path, "w");
+    if (!f) return fail(GGP_EINVAL, std::string("cannot write ") + csv_path);
+    std::fprintf(f, ",cell_id,time_min,parent_id,log_length,gfp%s\n", segmented ? ",segment" : "");
+    int64_t row = 0;
+    bool ok = true;
+    for (const Cell &c : d->cells)
+        for (size_t k = 0; k < c.time.size() && ok; ++k, ++row) {
+            ok = std::fprintf(f, "%lld,%s,%.17g,%s,%.17g,%.17g", (long long)row, c.id.c_str(), c.time[k],
+                              c.parent_id.c_str(), c.log_length[k], c.fp[k]) > 0;
+            if (ok && segmented) ok = std::fprintf(f, ",%d", (int)c.segment[k]) > 0;
+            if (ok) ok = std::fputc('\n', f) != EOF;
+        }
+    ok = (std::fclose(f) == 0) && ok;
+    std::FILE *g = std::fopen(config_path, "w");
+    if (!g) return fail(GGP_EINVAL, std::string("cannot write ") + config_path);
+    std::fprintf(g, "# written by ggp_dataset_write_csv\ntime_col = time_min\nlength_col = log_length\n"
+                    "length_islog = true\nfp_col = gfp\ncell_tags = cell_id\nparent_tags = parent_id\n"
+                    "rescale_time = 1\nfp_auto = %.17g\n%s",
+                 d->fp_auto, segmented ? "segment_col = segment\n" : "");
+    ok = (std::fclose(g) == 0) && ok;
+    return ok ? GGP_OK : fail(GGP_EINVAL, "ggp_dataset_write_csv: write failed");
+}
+
 extern "C" int ggp_dataset_save(const ggp_dataset *d, const char *path)
 {
     if (!d || !path) return fail(GGP_EINVAL, "null argument");

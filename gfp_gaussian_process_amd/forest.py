@@ -148,6 +148,12 @@ class Dataset:
             raise GGPError(_host_err())
         return cls(h)
 
+    def write_csv(self, csv_path: str, config_path: str) -> None:
+        """the reference's input CSV (example column layout, %.17g) and the csv_config that reads
+        it back bit for bit (ggp_dataset_write_csv): a synthetic forest the reference can read"""
+        if N.host().ggp_dataset_write_csv(self._h, csv_path.encode(), config_path.encode()) != N.GGP_OK:
+            raise GGPError(_host_err())
+
     def save(self, path: str) -> None:
         """binary dataset ("GGPD0001", ggp_dataset_save): the CLI's -i reads it directly"""
         if N.host().ggp_dataset_save(self._h, path.encode()) != N.GGP_OK:

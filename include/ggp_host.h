@@ -70,6 +70,13 @@ int ggp_dataset_load(const char *path, ggp_dataset **out);
 int ggp_dataset_create(int64_t n_cells, const int64_t *row_offset, const double *time, const double *log_length,
                        const double *fp, const int32_t *segment, const char *const *ids,
                        const char *const *parent_ids, double fp_auto, ggp_dataset **out);
+/* A dataset as the reference's input CSV (the example's column layout: an index column,
+ * cell_id, time_min, parent_id, log_length, gfp[, segment]) plus the csv_config that reads it
+ * back (length_islog = true, rescale_time = 1): values in %.17g, so ggp_dataset_read of the
+ * pair gives the dataset bit for bit -- a synthetic forest the reference binary can read
+ * (SURVEY §8(d)).  Ids are written verbatim; an id read_data would renormalise (all digits and
+ * dots, last part zeros: moma_input.h:320-338) is refused (GGP_EINVAL). */
+int ggp_dataset_write_csv(const ggp_dataset *d, const char *csv_path, const char *config_path);
 
 /* segment indices in order of first occurrence; *n receives the count (<= cap copied) */
 int ggp_dataset_segments(const ggp_dataset *d, int32_t *out, int32_t cap, int32_t *n);

@@ -263,6 +263,38 @@ def test_binary_dataset_roundtrip(tmp_path, example_paths):
         g.Dataset.load(example_paths["params"])
 
 
+def test_dataset_csv_writer_roundtrip(tmp_path, example_paths):
+    """ggp_dataset_write_csv (synthetic forests as the reference's input CSV): a
+    synthetic forest and the example (with its segments) written as CSV + csv_config and read
+    back by the reference-semantics reader build the bit-identical forest; ids read_data would
+    renormalise are refused"""
+    import gfp_gaussian_process_amd as g
+    syn = g.HostForest.synthetic(40, 40, with_ids=True)
+    csv, cfg = str(tmp_path / "syn.csv"), str(tmp_path / "syn_config.txt")
+    g.Dataset.from_forest(syn).write_csv(csv, cfg)
+    head = open(csv).readline().strip()
+    assert head == ",cell_id,time_min,parent_id,log_length,gfp"
+    back = g.HostForest.from_csv(csv, cfg)
+    assert back.ids == syn.ids and back.parent_ids == syn.parent_ids
+    for k in ("time", "log_length", "fp", "row_offset", "parent", "daughter1", "daughter2", "root_mean_xg",
+              "root_var_xg", "leaf_mean_xg", "leaf_var_xg"):
+        assert np.array_equal(np.asarray(back.a[k]), np.asarray(syn.a[k])), k
+    ds = g.Dataset.read(example_paths["csv"], g.CSVConfig.load(example_paths["config"]))
+    csv2, cfg2 = str(tmp_path / "ex.csv"), str(tmp_path / "ex_config.txt")
+    ds.write_csv(csv2, cfg2)
+    ds2 = g.Dataset.read(csv2, g.CSVConfig.load(cfg2))
+    assert ds2.segment_indices() == ds.segment_indices()
+    for seg in [-1] + ds.segment_indices()[:2]:
+        a, b = g.HostForest.build(ds, seg), g.HostForest.build(ds2, seg)
+        assert a.ids == b.ids
+        for k, v in a.a.items():
+            assert np.array_equal(np.asarray(b.a[k]), np.asarray(v)), (seg, k)
+    bad = g.HostForest.synthetic(2, 40, with_ids=True)
+    bad.ids = ["1.0"] + bad.ids[1:]
+    with pytest.raises(g.GGPError, match="read back"):
+        g.Dataset.from_forest(bad).write_csv(str(tmp_path / "bad.csv"), str(tmp_path / "bad_cfg.txt"))
+
+
 def test_sparse_joints_converter_handcrafted(tmp_path):
     """joints_format.sparse_to_dense on a hand-made case: three rows, a duplicated (cell_id, time)
     column pair (a joint lands in both, Joint_vector::add), rows without joints, the last add
