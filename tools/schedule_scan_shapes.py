@@ -38,7 +38,7 @@ def replicate(hf, k):
 
 def scan(name, hf):
     res = []
-    for k in ("wave", "group", "lane", "auto"):
+    for k in ("wave", "group", "pair", "lane", "auto"):
         f = g.Forest(hf, kernel=k)
         for _ in range(2):
             f.total_likelihood(P)
@@ -53,8 +53,8 @@ def scan(name, hf):
         lv = " ".join(f"{m:.3f}" for m in ms[:6]) + (" ..." if len(ms) > 6 else "")
         res.append((k, 1e3 * dt, lv, names))
         f.close()
-    best = min(res[:3], key=lambda r: r[1])
-    auto = res[3]
+    best = min(res[:4], key=lambda r: r[1])
+    auto = res[4]
     print(f"{name} cells={hf.n_cells} rows={hf.n_rows}: " + " | ".join(f"{k} {t:.3f} ms [{lv}]" for k, t, lv, _ in res)
           + f" || best fixed: {best[0]} {best[1]:.3f}; auto/best = {auto[1] / best[1]:.3f}", flush=True)
 
@@ -65,7 +65,7 @@ with gzip.open(os.path.join(ROOT, "tests", "golden", "example_input.csv.gz"), "r
 ex = g.HostForest.from_csv(d + "/in.csv", os.path.join(ROOT, "tests", "golden", "example_csv_config.txt"))
 for k in (1, 32, 128, 512):
     scan(f"example x{k}", replicate(ex, k) if k > 1 else ex)
-for t in (1000, 2500, 4000, 6000):
+for t in (1000, 2500, 4000, 6000, 12500):
     scan(f"C5-shape {t} trees x 500", g.HostForest.synthetic(t, 500))
-for t in (1000, 4000, 6000, 12500):
+for t in (1000, 4000, 6000, 12500, 20000, 40000):
     scan(f"C2-shape {t} trees x 200", g.HostForest.synthetic(t, 200))
