@@ -2688,10 +2688,9 @@ static int rccl_load(const char *path, RcclApi &a)
 
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id)
 {
-    if (!id) return GGP_EINVAL;
     RcclApi a;
     int rc = rccl_load(rccl_lib, a);
-    if (rc != GGP_OK) return rc;
+    if (rc != GGP_OK || !id) return rc;   // id NULL: only check that the library can be used
     ggp_rccl_id u;
     const int e = a.get_unique_id(&u);
     if (e != 0) {

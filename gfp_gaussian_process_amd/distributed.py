@@ -135,8 +135,8 @@ class ShardedObjective:
         lib = lib if os.path.exists(lib) else None      # the RCCL torch loaded: one RCCL per process
         rank = dist.get_rank(group)
         src = 0 if group is None else dist.get_global_rank(group, 0)
-        try:
-            mine = comm_unique_id(lib)
+        try:   # rank 0 makes the id, the others only check the library (one bootstrap root)
+            mine = comm_unique_id(lib) if rank == 0 else (comm_unique_id(lib, probe=True) or bytes(128))
             ok = 1
         except GGPError as e:
             print(f"ShardedObjective: engine RCCL unavailable on rank {rank} ({e}); torch's all_gather instead",

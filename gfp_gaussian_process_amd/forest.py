@@ -376,14 +376,15 @@ def kernel_name(code: int) -> str:
     return f"k_loglik_group<{lanes}>"
 
 
-def comm_unique_id(rccl_lib: str | None = None) -> bytes:
-    """the 128-byte RCCL unique id (ncclGetUniqueId) rank 0 makes for Forest.comm_attach"""
-    buf = ctypes.create_string_buffer(128)
+def comm_unique_id(rccl_lib: str | None = None, probe: bool = False) -> bytes | None:
+    """the 128-byte RCCL unique id (ncclGetUniqueId) rank 0 makes for Forest.comm_attach;
+    probe=True only checks that the RCCL library and its entry points load (None)"""
+    buf = None if probe else ctypes.create_string_buffer(128)
     lib = N.engine()
     rc = lib.ggp_comm_unique_id(rccl_lib.encode() if rccl_lib else None, buf)
     if rc != N.GGP_OK:
         raise GGPError(lib.ggp_strerror(rc).decode())
-    return buf.raw
+    return None if probe else buf.raw
 
 
 class Forest:

@@ -203,6 +203,8 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
  *   rccl_lib: the RCCL library to use (the one torch already loaded, so the process holds one
  *             RCCL; NULL = "librccl.so.1")
  *   id: 128 bytes (ncclUniqueId) made by ggp_comm_unique_id on rank 0 and given to every rank
+ *       (ggp_comm_unique_id with id NULL only checks that the library and its entry points load:
+ *       the other ranks' check before they join)
  * The shard's device must be the process's current device for RCCL (one device per handle). */
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
