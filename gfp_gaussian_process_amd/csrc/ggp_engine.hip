@@ -54,6 +54,13 @@ struct DevForest {
 
 constexpr int kNanNone = 0x7fffffff;
 
+// lane-schedule kernels' register budget (tools/lane_wpe_ab.py builds a GGP_LANE_WPE=2 variant)
+#ifdef GGP_LANE_WPE
+#define GGP_LANE_ATTR __attribute__((amdgpu_waves_per_eu(GGP_LANE_WPE)))
+#else
+#define GGP_LANE_ATTR
+#endif
+
 // Dawson coefficient table copied to LDS once per workgroup (LDS gather ~100 cycles vs an
 // L2 round trip per coefficient from constant memory).  Every lane issues all its global loads
 // before the first LDS store (one memory latency per launch, not one per 64 coefficients:
@@ -173,7 +180,7 @@ GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t
     cell_nan[F.dfs_rank[c]] = nan_row;
 }
 
-__global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
+__global__ __launch_bounds__(64) GGP_LANE_ATTR void k_loglik_level(DevForest F, ggp_params P,
                                                       const int32_t *__restrict__ cells, int n,
                                                       int cpw, double *__restrict__ state,
                                                       double *__restrict__ cell_ll,
@@ -190,7 +197,7 @@ __global__ __launch_bounds__(64) void k_loglik_level(DevForest F, ggp_params P,
 // its own parameter row, state slice [n_cells x 20] and per-cell ll / NaN slices; the cell
 // body is the lane schedule's, so a point's result is bitwise that of a single lane-schedule
 // evaluation from the same starting state.
-__global__ __launch_bounds__(64) void k_loglik_level_batch(DevForest F, const double *__restrict__ ptab,
+__global__ __launch_bounds__(64) GGP_LANE_ATTR void k_loglik_level_batch(DevForest F, const double *__restrict__ ptab,
                                                             const int32_t *__restrict__ cells, int n, int cpw,
                                                             int64_t n_cells, double *__restrict__ state,
                                                             double *__restrict__ cell_ll,
@@ -1138,7 +1145,7 @@ GGP_DEV void store20(double *dst, const double *m, const double *C)
 }
 
 // prediction_forward / sc_prediction_forward (predictions.h:93-173)
-__global__ __launch_bounds__(64) void k_fwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
+__global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
                                                   const int32_t *__restrict__ cells, int n, int cpw,
                                                   double *__restrict__ pstate, double *__restrict__ out)
 {
@@ -1181,7 +1188,7 @@ __global__ __launch_bounds__(64) void k_fwd_level(DevForest F, const double *__r
 }
 
 // prediction_backward / sc_prediction_backward (predictions.h:368-444), levels bottom-up
-__global__ __launch_bounds__(64) void k_bwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
+__global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
                                                   const int32_t *__restrict__ cells, int n, int cpw,
                                                   double *__restrict__ pstate, double *__restrict__ out)
 {
