@@ -1263,6 +1263,234 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
     store20(pstate + (size_t)20 * c, m, C);
 }
 
+// ------------------------------------------------------------------------------------------
+// The smoother's levels on the lane-pair split (k_fwd_pair / k_bwd_pair<Q, CPW>): k_fwd_level /
+// k_bwd_level with each propagation split over the Q waves of a workgroup (pair::propagate, the
+// lane schedule's expressions: bitwise the lane smoother).  The row loop is workgroup-uniform
+// (the longest cell of the workgroup; a cell past its rows computes on its frozen state and
+// stores nothing); wave 0 stores the rows.  For levels up to pair_max_cells (the example's deep
+// trees, per-GPU shards of C3/C4-sized forests), where the lane smoother waits on its step.
+// ------------------------------------------------------------------------------------------
+namespace pair {
+// the workgroup's step count (its longest cell) and lane 0's operands for lanes without a cell
+template <int CPW>
+GGP_DEV int wg_rows(int *s_rows, const int w, const int lane, const int nrows)
+{
+    if (w == 0) s_rows[lane] = nrows;
+    __syncthreads();
+    int kmax = 0;
+    for (int l = 0; l < CPW; ++l) kmax = max(kmax, s_rows[l]);
+    return kmax;
+}
+GGP_DEV void adopt_lane0(const bool valid, double *m, double *C, double &dt)
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double v = __shfl(m[q], 0);
+        m[q] = valid ? m[q] : v;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const double v = __shfl(C[q], 0);
+        C[q] = valid ? C[q] : v;
+    }
+    const double v = __shfl(dt, 0);
+    dt = valid ? dt : v;
+}
+template <int Q, int CPW>
+GGP_DEV void propagate_w(const int w, double *m, double *C, const double t, const ggp::OU &P, const double *tab,
+                         double *Xl, double *Dl, double *Il, double *Ol, const int lane)
+{
+    switch (w) {
+    case 0: propagate<0, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
+    case 1: propagate<1, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
+    case 2: propagate<2 % Q, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
+    default: propagate<3 % Q, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
+    }
+}
+}  // namespace pair
+
+#define GGP_PAIR_LDS(CPW)                                                                         \
+    __shared__ double s_tab[kDawsonTab];                                                          \
+    __shared__ double s_x[ggp::NXT * (CPW)], s_d[ggp::ND * (CPW)], s_i[ggp::NI * (CPW)],          \
+        s_o[pair::kOSlots * (CPW)];                                                               \
+    __shared__ int s_rows[64]
+
+// prediction_forward (predictions.h:93-173) on the split: k_fwd_level's row loop
+template <int Q, int CPW>
+__global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                     const int32_t *__restrict__ cells, int n, double *__restrict__ pstate,
+                                                     double *__restrict__ out)
+{
+    GGP_PAIR_LDS(CPW);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w == 0) load_dawson_table(s_tab, lane);
+    const int i = blockIdx.x * CPW + lane;
+    const bool valid = lane < CPW && i < n;
+    int c = 0, nrows = 0;
+    int64_t r0 = 0;
+    const double *pi = ptab, *pprop = ptab;
+    double m[4] = {0, 0, 0, 0}, C[16] = {0}, dt = 0.0;
+    bool pending = false, divide = false;
+    if (valid) {
+        c = cells[i];
+        r0 = F.row_off[c];
+        nrows = (int)(F.row_off[c + 1] - r0);
+        const int par = F.parent[c];
+        pi = seg_params(F, ptab, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);   // :103-108
+        pending = cell_prologue(F, pi, pstate, c, r0, m, C, dt);
+        divide = pending;
+        pprop = pi;
+    }
+    pair::adopt_lane0(valid, m, C, dt);
+    const int kmax = pair::wg_rows<CPW>(s_rows, w, lane, nrows);
+    bool live = valid && nrows > 0;
+    for (int k = 0; k < kmax; ++k) {
+        const int64_t r = r0 + k;
+        if (__builtin_amdgcn_ballot_w64(live && pending)) {
+            double mn[4], Cn[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) mn[q] = m[q];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Cn[q] = C[q];
+            pair::propagate_w<Q, CPW>(w, mn, Cn, dt, ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]),
+                                      s_tab, s_x, s_d, s_i, s_o, lane);
+            if (live && pending) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = mn[q];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) C[q] = Cn[q];
+                if (divide) {
+                    ggp::division_map(m, C, pi[9], pi[10], F.binomial, F.log2);
+                    divide = false;
+                }
+            }
+        }
+        if (live) {
+            const double *p = seg_params(F, ptab, n_seg, r);
+            const double x0 = F.logl[r] - m[0];
+            const double x1 = F.fp[r] - m[1];
+            ggp_innov v;
+            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+            ggp_posterior(m, C, x0, x1, v);
+            if (w == 0) store20(out + (size_t)20 * r, m, C);
+            pending = k + 1 < nrows;
+            if (pending) dt = F.time[r + 1] - F.time[r];
+            pprop = p;   // the step t -> t+1 uses row t's parameters (:143-146)
+            live = k + 1 < nrows;
+        }
+    }
+    if (valid && w == 0) store20(pstate + (size_t)20 * c, m, C);
+}
+
+// prediction_backward (predictions.h:368-444) on the split: k_bwd_level's row loop, bottom-up
+template <int Q, int CPW>
+__global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *__restrict__ ptab, int n_seg,
+                                                     const int32_t *__restrict__ cells, int n, double *__restrict__ pstate,
+                                                     double *__restrict__ out)
+{
+    GGP_PAIR_LDS(CPW);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w == 0) load_dawson_table(s_tab, lane);
+    const int i = blockIdx.x * CPW + lane;
+    const bool valid = lane < CPW && i < n;
+    int c = 0, nrows = 0, d1 = -1;
+    int64_t r0 = 0, r1 = 0;
+    const double *pi = ptab;
+    double m[4] = {0, 0, 0, 0}, C[16] = {0}, dt = 0.0;
+    bool internal = false;
+    if (valid) {
+        c = cells[i];
+        r0 = F.row_off[c];
+        r1 = F.row_off[c + 1];
+        nrows = (int)(r1 - r0);
+        pi = seg_params(F, ptab, n_seg, r1 - 1);   // :376-378
+        d1 = F.d1[c];
+        const int d2 = F.d2[c];
+        if (d1 < 0 && d2 < 0) {   // init_sc_distribution_r leaf branch (:317-332)
+            const double *st = pstate + (size_t)20 * c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = st[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) C[k] = st[4 + k];
+            m[0] = F.leaf_mean0;
+            m[1] = F.leaf_mean1;
+            C[0] = F.leaf_var0;
+            C[5] = F.leaf_var1;
+            m[2] = -pi[0];
+            m[3] = -pi[3];
+            C[10] = pi[2] / (2. * pi[1]);
+            C[15] = pi[5] / (2. * pi[4]);
+        } else {   // mean_cov_after_division_r (:201-275), then the propagation below
+            const double *s1 = pstate + (size_t)20 * d1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = s1[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) C[k] = s1[4 + k];
+            ggp::division_map_r(m, C, pi[9], pi[10], F.binomial, F.log2);
+            if (d2 >= 0) {
+                double m2[4], C2[16];
+                const double *s2 = pstate + (size_t)20 * d2;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) m2[k] = s2[k];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) C2[k] = s2[4 + k];
+                ggp::division_map_r(m2, C2, pi[9], pi[10], F.binomial, F.log2);
+                ggp::mult_gauss(m, C, m2, C2);
+            }
+            dt = F.time[F.row_off[d1]] - F.time[r1 - 1];
+            internal = true;
+        }
+    }
+    pair::adopt_lane0(valid, m, C, dt);
+    const int kmax = pair::wg_rows<CPW>(s_rows, w, lane, nrows);
+    const double *pq = pi;   // the next propagation's parameters (the reversed model)
+    auto prop = [&](const bool act, const double t) {
+        double mn[4], Cn[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mn[q] = m[q];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Cn[q] = C[q];
+        pair::propagate_w<Q, CPW>(w, mn, Cn, t, ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]), s_tab, s_x,
+                                  s_d, s_i, s_o, lane);
+        if (act) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m[q] = mn[q];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) C[q] = Cn[q];
+        }
+    };
+    if (__builtin_amdgcn_ballot_w64(internal)) prop(internal, dt);
+    bool live = valid && nrows > 0;
+    for (int k = 0; k < kmax; ++k) {
+        const int64_t r = r1 - 1 - k;
+        bool more = false;
+        if (live) {
+            double rm[4], rC[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rm[q] = m[q];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) rC[q] = C[q];
+            ggp::reverse_state(rm, rC);
+            if (w == 0) store20(out + (size_t)20 * r, rm, rC);   // the prior, before the update
+            const double *p = seg_params(F, ptab, n_seg, r);
+            const double x0 = F.logl[r] - m[0];
+            const double x1 = F.fp[r] - m[1];
+            ggp_innov v;
+            ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+            ggp_posterior(m, C, x0, x1, v);
+            more = r > r0;
+            if (more) {
+                pq = seg_params(F, ptab, n_seg, r - 1);
+                dt = F.time[r] - F.time[r - 1];
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(more)) prop(more, dt);
+        live = more;
+    }
+    if (valid && w == 0) store20(pstate + (size_t)20 * c, m, C);
+}
+
 // combine_predictions (predictions.h:466-499): one lane per row
 __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab, int n_seg,
                                                  const int32_t *__restrict__ prior_seg, int64_t n_rows,
@@ -1791,6 +2019,7 @@ struct Shard {
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
     int tune_pair_q = 0;                         // GGP_PAIR_Q: waves per cell (2, 4; 0 = by level size)
+    bool smoother_lane = false;                  // GGP_SMOOTHER_LANE=1: the lane smoother on every level
     int kernel_used = GGP_KERNEL_LANE;
     int32_t last_code = 0;
     DevForest F{};
@@ -2067,23 +2296,48 @@ int shard_wait(Shard *s)
 hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd, double *d_bwd)
 {
     const int n_levels = (int)f->level_start.size() - 1;
+    // a level up to pair_max_cells takes the lane-pair split (four waves per cell while one
+    // 64-cell workgroup per CU holds it, else two; bitwise the lane smoother), larger ones the
+    // lane smoother (GGP_SMOOTHER_LANE=1: every level)
+    auto launch = [&](const bool fwd, const int64_t a, const int n) {
+        if (!f->smoother_lane && n <= f->pair_max_cells) {
+            const int q = n <= (int64_t)f->n_cu * 64 ? 4 : 2;
+            const dim3 grid((n + 63) / 64);
+            if (fwd && q == 4)
+                hipLaunchKernelGGL((k_fwd_pair<4, 64>), grid, dim3(256), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                                   d_pstate, d_fwd);
+            else if (fwd)
+                hipLaunchKernelGGL((k_fwd_pair<2, 64>), grid, dim3(128), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                                   d_pstate, d_fwd);
+            else if (q == 4)
+                hipLaunchKernelGGL((k_bwd_pair<4, 64>), grid, dim3(256), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                                   d_pstate, d_bwd);
+            else
+                hipLaunchKernelGGL((k_bwd_pair<2, 64>), grid, dim3(128), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                                   d_pstate, d_bwd);
+            return;
+        }
+        const int cpw = lane_cpw(f);
+        if (fwd)
+            hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        else
+            hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
+    };
     hipError_t e = hipMemsetAsync(d_pstate, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream);
     for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
         const int64_t a = f->level_start[L];
         const int n = (int)(f->level_start[L + 1] - a);
         if (n <= 0) continue;
-        const int cpw = lane_cpw(f);
-        hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                           f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        launch(true, a, n);
         e = hipGetLastError();
     }
     for (int L = n_levels - 1; L >= 0 && e == hipSuccess; --L) {   // backward: leaves first
         const int64_t a = f->level_start[L];
         const int n = (int)(f->level_start[L + 1] - a);
         if (n <= 0) continue;
-        const int cpw = lane_cpw(f);
-        hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                           f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
+        launch(false, a, n);
         e = hipGetLastError();
     }
     return e;
@@ -2227,6 +2481,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_PAIR_CPW")) f->tune_pair_cpw = atoi(e) == 32 ? 32 : 64;
     if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
+    if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);

@@ -344,6 +344,34 @@ def test_predict_segments_vs_oracle():
     _check_predict(hf, np.stack([P0, P1]))
 
 
+@pytest.mark.parametrize("which", ["example", "segments", "ragged", "wide"])
+def test_predict_split_smoother_bitwise_lane(example_forests, which, monkeypatch):
+    """the smoother's levels on the lane-pair split (k_fwd_pair / k_bwd_pair, four or two waves
+    per cell) give the lane smoother's bits: forward, backward and combined rows (the example's
+    deep small levels, two parameter segments, ragged cells, and a forest whose 6000-cell and
+    12000-cell levels take Q = 4 and Q = 2)"""
+    import gfp_gaussian_process_amd as g
+    P0 = np.array(CONFIGS[0][2])
+    if which == "example":
+        hf, params = example_forests[("scaled", "binomial")], P0
+    elif which == "segments":
+        hf = g.HostForest.synthetic(40, 40)
+        hf.a["segment"] = (hf.a["time"] >= np.median(hf.a["time"])).astype(np.int32)
+        P1 = P0.copy()
+        P1[0] *= 1.1
+        P1[7] *= 1.2
+        params = np.stack([P0, P1])
+    elif which == "ragged":
+        hf, params = _ragged_roots(), P0
+    else:
+        hf, params = g.HostForest.synthetic(6000, 40), P0
+    got = g.Forest(hf).predict(params)
+    monkeypatch.setenv("GGP_SMOOTHER_LANE", "1")
+    ref = g.Forest(hf).predict(params)
+    for name, x, y in zip(("forward", "backward", "combined"), got, ref):
+        assert np.array_equal(x, y), name
+
+
 def test_predict_ragged_and_single_rows():
     _check_predict(_ragged_roots(), CONFIGS[0][2])
 
