@@ -136,6 +136,8 @@ class ShardedObjective:
         rank = dist.get_rank(group)
         src = 0 if group is None else dist.get_global_rank(group, 0)
         try:   # rank 0 makes the id, the others only check the library (one bootstrap root)
+            if len(self.f.shards()) != 1:   # ggp_comm_attach needs one shard (one device) per rank
+                raise GGPError(f"{len(self.f.shards())} shards on this rank")
             mine = comm_unique_id(lib) if rank == 0 else (comm_unique_id(lib, probe=True) or bytes(128))
             ok = 1
         except GGPError as e:

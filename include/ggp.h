@@ -205,7 +205,9 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
  *   id: 128 bytes (ncclUniqueId) made by ggp_comm_unique_id on rank 0 and given to every rank
  *       (ggp_comm_unique_id with id NULL only checks that the library and its entry points load:
  *       the other ranks' check before they join)
- * The shard's device must be the process's current device for RCCL (one device per handle). */
+ * The shard's device must be the process's current device for RCCL (one device per handle).
+ * Only the objective is collective: ggp_total_loglik_batch, ggp_predict and ggp_joints stay
+ * per-rank (each rank's own trees), as distributed.py's ShardedPredictor expects. */
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
 int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last call, -1 none */
