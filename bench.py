@@ -31,6 +31,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (AMD spec)
 COMBINE_BYTES_PER_ROW = 484   # k_combine: fwd + bwd rows (2 x 160 B) + prior segment (4 B) read, 160 B written
+VALU_ISSUE_CYCLES = 4          # cycles a SIMD takes per 64-lane FP64 VALU wave-instruction (16 lanes/cycle)
+CLOCK_HZ = 2.4e9               # MI355X peak engine clock (MI355X_MICROARCH.md)
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
              3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
 SEED = 20261015
@@ -218,6 +220,20 @@ def main() -> int:
                 "frac_useful": useful / FP64_PEAK_TFLOPS,
                 "issued_lane_flops_per_update": cnt.get("issued_flops_per_update"), "issued_lane_rate": issued,
                 "source": "profiles/fp64_counts.json (rocprofv3 PMC of this build) x the live launch time"}
+        # the bound the kernel actually meets: VALU issue.  A SIMD issues at most one 64-lane FP64
+        # wave-instruction per 4 cycles (16 lanes/cycle); the PMC pass counts the wave's VALU
+        # instructions per update (SQ_INSTS_VALU), so their issue time over every SIMD of the chip
+        # for one launch, against the launch time at the 2.4 GHz peak clock
+        vpu = (cnt.get("wave") or {}).get("valu_wave_insts_per_update")
+        if vpu:
+            n_simd = 4 * torch.cuda.get_device_properties(local).multi_processor_count
+            need = vpu * (d_rows / d_n) * VALU_ISSUE_CYCLES / n_simd
+            have = avg_ms * 1e-3 * CLOCK_HZ
+            fp64["valu_issue"] = {"valu_wave_insts_per_update": vpu, "simds": n_simd,
+                                  "cycles_per_valu_inst": VALU_ISSUE_CYCLES, "clock_ghz": CLOCK_HZ / 1e9,
+                                  "frac": need / have,
+                                  "note": "VALU issue cycles the launch needs per SIMD / the launch's cycles: the "
+                                          "root level runs one wave per SIMD (latency), the daughters two (issue)"}
 
     # ---- the same path on a C4-shard-sized forest (BASELINE configs[3]: 100k trees over 8
     # GPUs = 12.5k trees per GPU), reported beside the C2 headline ----
