@@ -321,6 +321,24 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
 #pragma unroll
     for (int k = 0; k < 16; ++k) C[k] = Co[k];
 }
+// wave w's body (w is wave-uniform): one instantiation per wave of the workgroup
+template <int W, int Q, int CPW>
+GGP_DEV void propagate_from(const int w, double *m, double *C, const double t, const ggp::OU &P, const double *tab,
+                            double *Xl, double *Dl, double *Il, double *Ol, const int lane)
+{
+    if constexpr (W + 1 == Q) {
+        propagate<W, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane);
+    } else {
+        if (w == W) propagate<W, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane);
+        else propagate_from<W + 1, Q, CPW>(w, m, C, t, P, tab, Xl, Dl, Il, Ol, lane);
+    }
+}
+template <int Q, int CPW>
+GGP_DEV void propagate_w(const int w, double *m, double *C, const double t, const ggp::OU &P, const double *tab,
+                         double *Xl, double *Dl, double *Il, double *Ol, const int lane)
+{
+    propagate_from<0, Q, CPW>(w, m, C, t, P, tab, Xl, Dl, Il, Ol, lane);
+}
 }  // namespace pair
 
 template <int Q, int CPW>
@@ -390,12 +408,7 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
             for (int q = 0; q < 4; ++q) mn[q] = m[q];
 #pragma unroll
             for (int q = 0; q < 16; ++q) Cn[q] = C[q];
-            switch (w) {
-            case 0: pair::propagate<0, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
-            case 1: pair::propagate<1, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
-            case 2: pair::propagate<2 % Q, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
-            default: pair::propagate<3 % Q, Q, CPW>(mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane); break;
-            }
+            pair::propagate_w<Q, CPW>(w, mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
             if (live && pending) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) m[q] = mn[q];
@@ -1296,17 +1309,6 @@ GGP_DEV void adopt_lane0(const bool valid, double *m, double *C, double &dt)
     }
     const double v = __shfl(dt, 0);
     dt = valid ? dt : v;
-}
-template <int Q, int CPW>
-GGP_DEV void propagate_w(const int w, double *m, double *C, const double t, const ggp::OU &P, const double *tab,
-                         double *Xl, double *Dl, double *Il, double *Ol, const int lane)
-{
-    switch (w) {
-    case 0: propagate<0, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
-    case 1: propagate<1, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
-    case 2: propagate<2 % Q, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
-    default: propagate<3 % Q, Q, CPW>(m, C, t, P, tab, Xl, Dl, Il, Ol, lane); break;
-    }
 }
 }  // namespace pair
 
