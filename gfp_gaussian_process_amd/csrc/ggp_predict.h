@@ -17,10 +17,13 @@
 namespace ggp {
 
 // dense 4x4 inverse by partial-pivot LU (first max |a| pivot, unit-lower L), solved column by
-// column against the identity -- the algorithm of oracle/ggp_oracle.c inv4
+// column against the identity -- the algorithm of oracle/ggp_oracle.c inv4.  RCP: divide by each
+// pivot through its reciprocal (4 divisions instead of 22, one more rounding per quotient; the
+// combine only, DESIGN.md "The -p combine")
+template <bool RCP = false>
 GGP_DEV void inv4(const double *A, double *R)
 {
-    double lu[16];
+    double lu[16], rd[4];
     int perm[4] = {0, 1, 2, 3};
 #pragma unroll
     for (int i = 0; i < 16; ++i) lu[i] = A[i];
@@ -51,9 +54,13 @@ GGP_DEV void inv4(const double *A, double *R)
 #pragma unroll
             for (int i = k + 1; i < 4; ++i) perm[i] = (i == piv) ? pk : perm[i];
         }
+        if constexpr (RCP) rd[k] = 1.0 / lu[4 * k + k];
         if (big != 0.0) {
 #pragma unroll
-            for (int i = k + 1; i < 4; ++i) lu[4 * i + k] /= lu[4 * k + k];
+            for (int i = k + 1; i < 4; ++i) {
+                if constexpr (RCP) lu[4 * i + k] *= rd[k];
+                else lu[4 * i + k] /= lu[4 * k + k];
+            }
 #pragma unroll
             for (int i = k + 1; i < 4; ++i)
 #pragma unroll
@@ -73,7 +80,8 @@ GGP_DEV void inv4(const double *A, double *R)
         for (int i = 3; i >= 0; --i) {
 #pragma unroll
             for (int j = i + 1; j < 4; ++j) y[i] -= lu[4 * i + j] * y[j];
-            y[i] /= lu[4 * i + i];
+            if constexpr (RCP) y[i] *= rd[i];
+            else y[i] /= lu[4 * i + i];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) R[4 * i + col] = y[i];
@@ -105,14 +113,15 @@ GGP_DEV void mv4(const double *A, const double *v, double *r)
 }
 
 // multiply_gaussian (predictions.h:183-188): in place on (m1, c1)
+template <bool RCP = false>
 GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
 {
     double i1[16], i2[16], sum[16], nc[16], t1[16], t2[16], v1[4], v2[4];
-    inv4(c1, i1);
-    inv4(c2, i2);
+    inv4<RCP>(c1, i1);
+    inv4<RCP>(c2, i2);
 #pragma unroll
     for (int k = 0; k < 16; ++k) sum[k] = i1[k] + i2[k];
-    inv4(sum, nc);
+    inv4<RCP>(sum, nc);
     mm4(nc, i1, t1);
     mm4(nc, i2, t2);
     mv4(t1, m1, v1);
@@ -124,6 +133,7 @@ GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *
 }
 
 // divide_by_prior (predictions.h:446-463)
+template <bool RCP = false>
 GGP_DEV void divide_prior(double *m, double *c, const double *p)
 {
     const double mp[4] = {0, 0, p[0], p[3]};
@@ -133,10 +143,10 @@ GGP_DEV void divide_prior(double *m, double *c, const double *p)
     ip[10] = (2. * p[1]) / p[2];
     ip[15] = (2. * p[4]) / p[5];
     double ic[16], d[16], nc[16], a[4], bv[4], r[4];
-    inv4(c, ic);
+    inv4<RCP>(c, ic);
 #pragma unroll
     for (int k = 0; k < 16; ++k) d[k] = ic[k] - ip[k];
-    inv4(d, nc);
+    inv4<RCP>(d, nc);
     mv4(ic, m, a);
     mv4(ip, mp, bv);
 #pragma unroll

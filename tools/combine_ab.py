@@ -1,39 +1,48 @@
-"""A/B of a -p build against another (diagnostic): python tools/combine_ab.py OLD_LIB_DIR
-runs the C5-shard smoother with the package's libggp.so and with OLD_LIB_DIR's in two
-processes, and compares device times and the combined rows bitwise on a small forest."""
+"""k_combine A/B (diagnostic): the -p combine with IEEE pivot quotients (GGP_COMBINE_RCP=0)
+and through reciprocal pivots (=1), alternating, on a C5-shaped forest (500 rows per tree); the
+combined rows of the two compared on a sample (means relative to |m| + sd, covariances to
+sqrt(Cii Cjj), as tests/test_gpu_parity.py's smoother check).
+  python tools/combine_ab.py [TREES]"""
 import json
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CHILD = r'''
-import os, sys, json, hashlib
 sys.path.insert(0, ROOT)
-from gfp_gaussian_process_amd import _native
-if LIB: _native.LIB_DIR = LIB
-import numpy as np
-import gfp_gaussian_process_amd as g
+import numpy as np  # noqa: E402
+
+import gfp_gaussian_process_amd as g  # noqa: E402
+
 P = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]
-small = g.Forest(g.HostForest.synthetic(300, 60))
-f, b, c = small.predict(P)
-h = hashlib.sha256(f.tobytes() + b.tobytes() + c.tobytes()).hexdigest()
-big = g.Forest(g.HostForest.synthetic(125000, 500))
-big.predict(P, outputs=(False, False, False))
-sm, cb = [], []
-for _ in range(5):
-    big.predict(P, outputs=(False, False, False))
-    a_, b_ = big.predict_profile()
-    sm.append(a_); cb.append(b_)
-print(json.dumps({"sha": h, "smooth_ms": sorted(sm)[2], "combine_ms": sorted(cb)[2]}))
-'''
-out = {}
-for tag, lib in (("new", ""), ("old", os.path.abspath(sys.argv[1])), ("new2", ""), ("old2", os.path.abspath(sys.argv[1]))):
-    code = f"ROOT={ROOT!r}\nLIB={lib!r}\n" + CHILD
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
-    if r.returncode != 0:
-        print(tag, "failed", r.stderr[-2000:])
-        sys.exit(1)
-    out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
-    print(tag, out[tag], flush=True)
-print("bitwise equal:", out["new"]["sha"] == out["old"]["sha"])
+
+
+def run(hf, rcp, reps=3):
+    os.environ["GGP_COMBINE_RCP"] = str(rcp)
+    f = g.Forest(hf)
+    f.predict(P, outputs=(False, False, False))
+    cb = []
+    for _ in range(reps):
+        f.predict(P, outputs=(False, False, False))
+        cb.append(f.predict_profile()[1])
+    sample = np.concatenate([f.predict_rows(0, 50000), f.predict_rows(hf.n_rows - 50000, hf.n_rows)])
+    f.close()
+    return min(cb), sample
+
+
+if __name__ == "__main__":
+    trees = int(sys.argv[1]) if len(sys.argv) > 1 else 40000
+    hf = g.HostForest.synthetic(trees, 500)
+    ref = None
+    out = {"trees": trees, "rows": hf.n_rows, "combine_ms": {}}
+    for rnd in range(2):
+        for rcp in (0, 1):
+            ms, smp = run(hf, rcp)
+            out["combine_ms"].setdefault(str(rcp), []).append(round(ms, 4))
+            if ref is None:
+                ref = smp
+            sd = np.sqrt(np.abs(np.einsum("nii->ni", ref[:, 4:].reshape(-1, 4, 4))))
+            em = np.max(np.abs(smp[:, :4] - ref[:, :4]) / (np.abs(ref[:, :4]) + sd).clip(1e-300))
+            ec = np.max(np.abs(smp[:, 4:].reshape(-1, 4, 4) - ref[:, 4:].reshape(-1, 4, 4))
+                        / (sd[:, :, None] * sd[:, None, :]).clip(1e-300))
+            out.setdefault("err_vs_ieee", {})[str(rcp)] = [float(em), float(ec)]
+    print(json.dumps(out), flush=True)
