@@ -1493,9 +1493,9 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
     if (valid && w == 0) store20(pstate + (size_t)20 * c, m, C);
 }
 
-// combine_predictions (predictions.h:466-499): one lane per row.  RCP: the inverses divide through
-// each pivot's reciprocal (GGP_COMBINE_RCP=0: IEEE quotients, the oracle's operations)
-template <bool RCP>
+// combine_predictions (predictions.h:466-499): one lane per row.  FAST (the default): the
+// inverses through reciprocal pivots (ggp_predict.h); GGP_COMBINE_EXACT=1: the oracle's operations
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab, int n_seg,
                                                  const int32_t *__restrict__ prior_seg, int64_t n_rows,
                                                  const double *__restrict__ fwd, const double *__restrict__ bwd,
@@ -1509,10 +1509,10 @@ __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab
     for (int k = 0; k < 4; ++k) { m[k] = f[k]; mb[k] = b[k]; }
 #pragma unroll
     for (int k = 0; k < 16; ++k) { C[k] = f[4 + k]; Cb[k] = b[4 + k]; }
-    ggp::mult_gauss<RCP>(m, C, mb, Cb);
+    ggp::mult_gauss<FAST>(m, C, mb, Cb);
     int s = prior_seg[r];
     if (s < 0 || s >= n_seg) s = 0;
-    ggp::divide_prior<RCP>(m, C, ptab + 11 * s);
+    ggp::divide_prior<FAST>(m, C, ptab + 11 * s);
     store20(out + (size_t)20 * r, m, C);
 }
 
@@ -2022,7 +2022,7 @@ struct Shard {
     int64_t pair_max_cells = 32768;   // auto: lane-pair schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
-    bool combine_rcp = true;                     // GGP_COMBINE_RCP: k_combine's inverses by reciprocal pivots
+    bool combine_exact = false;                  // GGP_COMBINE_EXACT=1: k_combine with the oracle's operations
     int tune_pair_q = 0;                         // GGP_PAIR_Q: waves per cell (2, 4; 0 = by level size)
     bool smoother_lane = false;                  // GGP_SMOOTHER_LANE=1: the lane smoother on every level
     int kernel_used = GGP_KERNEL_LANE;
@@ -2485,7 +2485,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_GROUP_MAX_CELLS")) f->group_max_cells = atoll(e);
     if (const char *e = getenv("GGP_PAIR_CPW")) f->tune_pair_cpw = atoi(e) == 32 ? 32 : 64;
     if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_COMBINE_RCP")) f->combine_rcp = atoi(e) != 0;
+    if (const char *e = getenv("GGP_COMBINE_EXACT")) f->combine_exact = atoi(e) != 0;
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
@@ -3594,7 +3594,7 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
         if (e == hipSuccess) e = hipEventRecord(s->ev_pred[1], s->stream);
         if (e == hipSuccess) {
             const int64_t blocks = (s->n_rows + 255) / 256;
-            auto *kc = s->combine_rcp ? k_combine<true> : k_combine<false>;
+            auto *kc = s->combine_exact ? k_combine<false> : k_combine<true>;
             hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), 0, s->stream, s->d_sm_ptab, n_seg,
                                s->d_prior_seg, s->n_rows, dv->sm_fwd, dv->sm_bwd, s->d_sm_comb);
             e = hipGetLastError();

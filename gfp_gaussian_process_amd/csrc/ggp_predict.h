@@ -17,10 +17,12 @@
 namespace ggp {
 
 // dense 4x4 inverse by partial-pivot LU (first max |a| pivot, unit-lower L), solved column by
-// column against the identity -- the algorithm of oracle/ggp_oracle.c inv4.  RCP: divide by each
-// pivot through its reciprocal (4 divisions instead of 22, one more rounding per quotient; the
-// combine only, DESIGN.md "The -p combine")
-template <bool RCP = false>
+// column against the identity -- the algorithm of oracle/ggp_oracle.c inv4.  FAST (the combine
+// only, DESIGN.md "Smoother"): divide by each pivot through its reciprocal (4 divisions instead
+// of 22, one more rounding per quotient).  (Solving only the lower triangle of each column and
+// mirroring it, A being symmetric, saved 5% more but moved the combined means 10x further from
+// the exact combine: 1.1e-10 against 1.2e-11.)
+template <bool FAST = false>
 GGP_DEV void inv4(const double *A, double *R)
 {
     double lu[16], rd[4];
@@ -54,11 +56,11 @@ GGP_DEV void inv4(const double *A, double *R)
 #pragma unroll
             for (int i = k + 1; i < 4; ++i) perm[i] = (i == piv) ? pk : perm[i];
         }
-        if constexpr (RCP) rd[k] = 1.0 / lu[4 * k + k];
+        if constexpr (FAST) rd[k] = 1.0 / lu[4 * k + k];
         if (big != 0.0) {
 #pragma unroll
             for (int i = k + 1; i < 4; ++i) {
-                if constexpr (RCP) lu[4 * i + k] *= rd[k];
+                if constexpr (FAST) lu[4 * i + k] *= rd[k];
                 else lu[4 * i + k] /= lu[4 * k + k];
             }
 #pragma unroll
@@ -80,7 +82,7 @@ GGP_DEV void inv4(const double *A, double *R)
         for (int i = 3; i >= 0; --i) {
 #pragma unroll
             for (int j = i + 1; j < 4; ++j) y[i] -= lu[4 * i + j] * y[j];
-            if constexpr (RCP) y[i] *= rd[i];
+            if constexpr (FAST) y[i] *= rd[i];
             else y[i] /= lu[4 * i + i];
         }
 #pragma unroll
@@ -112,16 +114,18 @@ GGP_DEV void mv4(const double *A, const double *v, double *r)
     }
 }
 
-// multiply_gaussian (predictions.h:183-188): in place on (m1, c1)
-template <bool RCP = false>
+// multiply_gaussian (predictions.h:183-188): in place on (m1, c1).  (The mean is kept as
+// (nc i1) m1 + (nc i2) m2: nc (i1 m1 + i2 m2) saves two 4x4 products but sums two large
+// precision-weighted means that cancel -- 1e-10 instead of 1e-11 from the exact combine.)
+template <bool FAST = false>
 GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
 {
     double i1[16], i2[16], sum[16], nc[16], t1[16], t2[16], v1[4], v2[4];
-    inv4<RCP>(c1, i1);
-    inv4<RCP>(c2, i2);
+    inv4<FAST>(c1, i1);
+    inv4<FAST>(c2, i2);
 #pragma unroll
     for (int k = 0; k < 16; ++k) sum[k] = i1[k] + i2[k];
-    inv4<RCP>(sum, nc);
+    inv4<FAST>(sum, nc);
     mm4(nc, i1, t1);
     mm4(nc, i2, t2);
     mv4(t1, m1, v1);
@@ -132,8 +136,9 @@ GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *
     for (int k = 0; k < 16; ++k) c1[k] = nc[k];
 }
 
-// divide_by_prior (predictions.h:446-463)
-template <bool RCP = false>
+// divide_by_prior (predictions.h:446-463).  FAST: the prior precision's product with its mean
+// formed from its two nonzero entries (the same values up to the sign of a zero)
+template <bool FAST = false>
 GGP_DEV void divide_prior(double *m, double *c, const double *p)
 {
     const double mp[4] = {0, 0, p[0], p[3]};
@@ -143,12 +148,18 @@ GGP_DEV void divide_prior(double *m, double *c, const double *p)
     ip[10] = (2. * p[1]) / p[2];
     ip[15] = (2. * p[4]) / p[5];
     double ic[16], d[16], nc[16], a[4], bv[4], r[4];
-    inv4<RCP>(c, ic);
+    inv4<FAST>(c, ic);
 #pragma unroll
     for (int k = 0; k < 16; ++k) d[k] = ic[k] - ip[k];
-    inv4<RCP>(d, nc);
+    inv4<FAST>(d, nc);
     mv4(ic, m, a);
-    mv4(ip, mp, bv);
+    if constexpr (FAST) {
+        bv[0] = bv[1] = 0.0;
+        bv[2] = ip[10] * mp[2];
+        bv[3] = ip[15] * mp[3];
+    } else {
+        mv4(ip, mp, bv);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = a[k] - bv[k];
     mv4(nc, r, m);

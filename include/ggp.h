@@ -114,8 +114,8 @@ typedef struct {
  * GGP_WAVE_MAX_CELLS / GGP_GROUP_MAX_CELLS / GGP_PAIR_MAX_CELLS (auto's thresholds),
  * GGP_AUTO_SMALL=group, GGP_PAIR_CPW (32: 32 cells per lane-pair workgroup), GGP_PAIR_Q (2 or 4
  * waves per lane-pair cell), GGP_SMOOTHER_LANE=1 (-p levels on the lane schedule only),
- * GGP_COMBINE_RCP=0 (ggp_predict's combine with IEEE pivot quotients, the oracle's operations;
- * default: through reciprocal pivots, within ~1e-11 of them, DESIGN.md "Smoother"). */
+ * GGP_COMBINE_EXACT=1 (ggp_predict's combine with the oracle's operations; default: through
+ * reciprocal pivots, within ~1e-11 of them, DESIGN.md "Smoother"). */
 
 int ggp_forest_create(const ggp_forest_desc *desc, ggp_forest **out);
 void ggp_forest_destroy(ggp_forest *f);

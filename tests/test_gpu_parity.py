@@ -373,9 +373,9 @@ def test_predict_split_smoother_bitwise_lane(example_forests, which, monkeypatch
 
 
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
-def test_combine_reciprocal_pivots_vs_ieee_quotients(example_forests, noise, div, monkeypatch):
-    """k_combine's inverses through reciprocal pivots (the default) against the same kernel with
-    IEEE quotients (GGP_COMBINE_RCP=0, the oracle's operations): forward and backward rows
+def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
+    """k_combine's fast form (the default: reciprocal pivots) against the
+    same kernel with the oracle's operations (GGP_COMBINE_EXACT=1): forward and backward rows
     bitwise (only the combine differs), combined rows within 1e-9 in the smoother check's
     normalisation, and both within PRED_TOL of the oracle"""
     import gfp_gaussian_process_amd as g
@@ -383,13 +383,13 @@ def test_combine_reciprocal_pivots_vs_ieee_quotients(example_forests, noise, div
     hf = example_forests[(noise, div)]
     params = next(p for n, d, p in CONFIGS if (n, d) == (noise, div))
     got = g.Forest(hf).predict(params)
-    monkeypatch.setenv("GGP_COMBINE_RCP", "0")
-    ieee = g.Forest(hf).predict(params)
-    assert np.array_equal(got[0], ieee[0]) and np.array_equal(got[1], ieee[1])
-    em, ec = _smoother_err(got[2], ieee[2])
+    monkeypatch.setenv("GGP_COMBINE_EXACT", "1")
+    exact = g.Forest(hf).predict(params)
+    assert np.array_equal(got[0], exact[0]) and np.array_equal(got[1], exact[1])
+    em, ec = _smoother_err(got[2], exact[2])
     assert em < 1e-9 and ec < 1e-9, (em, ec)
     ref = O.OracleForest(hf.a).predict(params)[2]
-    for x in (got[2], ieee[2]):
+    for x in (got[2], exact[2]):
         em, ec = _smoother_err(x, ref)
         assert em < PRED_TOL and ec < PRED_TOL, (em, ec)
 
