@@ -114,9 +114,8 @@ GGP_DEV void mv4(const double *A, const double *v, double *r)
     }
 }
 
-// multiply_gaussian (predictions.h:183-188): in place on (m1, c1).  (The mean is kept as
-// (nc i1) m1 + (nc i2) m2: nc (i1 m1 + i2 m2) saves two 4x4 products but sums two large
-// precision-weighted means that cancel -- 1e-10 instead of 1e-11 from the exact combine.)
+// multiply_gaussian (predictions.h:183-188): in place on (m1, c1).  Both forms keep the mean as
+// (nc i1) m1 + (nc i2) m2, the reference's order; FAST changes the inverses only
 template <bool FAST = false>
 GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
 {
