@@ -1494,7 +1494,8 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
 }
 
 // combine_predictions (predictions.h:466-499): one lane per row.  FAST (the default): the
-// inverses through reciprocal pivots (ggp_predict.h); GGP_COMBINE_EXACT=1: the oracle's operations
+// inverses through reciprocal pivots, the product's mean reassociated (ggp_predict.h);
+// GGP_COMBINE_EXACT=1: the oracle's operations
 template <bool FAST>
 __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab, int n_seg,
                                                  const int32_t *__restrict__ prior_seg, int64_t n_rows,

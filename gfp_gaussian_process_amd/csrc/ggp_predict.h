@@ -20,7 +20,7 @@ namespace ggp {
 // column against the identity -- the algorithm of oracle/ggp_oracle.c inv4.  FAST (the combine
 // only, DESIGN.md "Smoother"): divide by each pivot through its reciprocal (4 divisions instead
 // of 22, one more rounding per quotient).  (Solving only the lower triangle of each column and
-// mirroring it, A being symmetric, saved 5% more but moved the combined means 10x further from
+// mirroring it, A being symmetric, saved 5% more but moved the combined rows 10x further from
 // the exact combine: 1.1e-10 against 1.2e-11.)
 template <bool FAST = false>
 GGP_DEV void inv4(const double *A, double *R)
@@ -114,8 +114,9 @@ GGP_DEV void mv4(const double *A, const double *v, double *r)
     }
 }
 
-// multiply_gaussian (predictions.h:183-188): in place on (m1, c1).  Both forms keep the mean as
-// (nc i1) m1 + (nc i2) m2, the reference's order; FAST changes the inverses only
+// multiply_gaussian (predictions.h:183-188): in place on (m1, c1).  FAST: the mean as
+// nc (i1 m1 + i2 m2), three matrix-vector products instead of two 4x4 products and two
+// matrix-vector ones
 template <bool FAST = false>
 GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *c2)
 {
@@ -125,6 +126,16 @@ GGP_DEV void mult_gauss(double *m1, double *c1, const double *m2, const double *
 #pragma unroll
     for (int k = 0; k < 16; ++k) sum[k] = i1[k] + i2[k];
     inv4<FAST>(sum, nc);
+    if constexpr (FAST) {
+        mv4(i1, m1, v1);
+        mv4(i2, m2, v2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v1[k] = v1[k] + v2[k];
+        mv4(nc, v1, m1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c1[k] = nc[k];
+        return;
+    }
     mm4(nc, i1, t1);
     mm4(nc, i2, t2);
     mv4(t1, m1, v1);

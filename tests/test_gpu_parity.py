@@ -374,7 +374,7 @@ def test_predict_split_smoother_bitwise_lane(example_forests, which, monkeypatch
 
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
 def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
-    """k_combine's fast form (the default: reciprocal pivots) against the
+    """k_combine's fast form (the default: reciprocal pivots, reassociated mean) against the
     same kernel with the oracle's operations (GGP_COMBINE_EXACT=1): forward and backward rows
     bitwise (only the combine differs), combined rows within 1e-9 in the smoother check's
     normalisation, and both within PRED_TOL of the oracle"""

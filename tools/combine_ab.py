@@ -1,5 +1,5 @@
 """k_combine A/B (diagnostic): the -p combine with the oracle's operations (GGP_COMBINE_EXACT=1)
-and in its fast form (=0: reciprocal pivots), alternating, on a C5-shaped forest (500 rows per tree); the
+and in its fast form (=0: reciprocal pivots, reassociated mean), alternating, on a C5-shaped forest (500 rows per tree); the
 combined rows of the two compared on a sample (means relative to |m| + sd, covariances to
 sqrt(Cii Cjj), as tests/test_gpu_parity.py's smoother check).
   python tools/combine_ab.py [TREES]"""
