@@ -1178,9 +1178,16 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
     bool pending = cell_prologue(F, pi, pstate, c, r0, m, C, dt);
     bool divide = pending;
     const double *pprop = pi;
+    // the OU constants (six divisions and a pow) are formed again only when the segment changes
+    const double *ou_src = nullptr;
+    ggp::OU ou{};
     for (int64_t r = r0; r < r1; ++r) {
         if (pending) {
-            ggp::propagate_lane(m, C, dt, ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]), s_tab);
+            if (pprop != ou_src) {
+                ou = ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]);
+                ou_src = pprop;
+            }
+            ggp::propagate_lane(m, C, dt, ou, s_tab);
             if (divide) {
                 ggp::division_map(m, C, pi[9], pi[10], F.binomial, F.log2);
                 divide = false;
@@ -1254,6 +1261,8 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
         const double dt = F.time[F.row_off[d1]] - F.time[r1 - 1];
         ggp::propagate_lane(m, C, dt, ggp::make_ou(-pi[0], pi[1], pi[2], -pi[3], pi[4], pi[5], -pi[6]), s_tab);
     }
+    const double *ou_src = nullptr;   // as k_fwd_level: the OU constants per segment change only
+    ggp::OU ou{};
     for (int64_t r = r1 - 1; r >= r0; --r) {
         double rm[4], rC[16];
 #pragma unroll
@@ -1270,7 +1279,11 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
         ggp_posterior(m, C, x0, x1, v);
         if (r > r0) {
             const double *q = seg_params(F, ptab, n_seg, r - 1);
-            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], ggp::make_ou(-q[0], q[1], q[2], -q[3], q[4], q[5], -q[6]), s_tab);
+            if (q != ou_src) {
+                ou = ggp::make_ou(-q[0], q[1], q[2], -q[3], q[4], q[5], -q[6]);
+                ou_src = q;
+            }
+            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], ou, s_tab);
         }
     }
     store20(pstate + (size_t)20 * c, m, C);
