@@ -1360,6 +1360,8 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
     pair::adopt_lane0(valid, m, C, dt);
     const int kmax = pair::wg_rows<CPW>(s_rows, w, lane, nrows);
     bool live = valid && nrows > 0;
+    const double *ou_src = nullptr;   // the OU constants per segment change only (k_fwd_level)
+    ggp::OU ou{};
     for (int k = 0; k < kmax; ++k) {
         const int64_t r = r0 + k;
         if (__builtin_amdgcn_ballot_w64(live && pending)) {
@@ -1368,8 +1370,11 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
             for (int q = 0; q < 4; ++q) mn[q] = m[q];
 #pragma unroll
             for (int q = 0; q < 16; ++q) Cn[q] = C[q];
-            pair::propagate_w<Q, CPW>(w, mn, Cn, dt, ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]),
-                                      s_tab, s_x, s_d, s_i, s_o, lane);
+            if (pprop != ou_src) {
+                ou = ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]);
+                ou_src = pprop;
+            }
+            pair::propagate_w<Q, CPW>(w, mn, Cn, dt, ou, s_tab, s_x, s_d, s_i, s_o, lane);
             if (live && pending) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) m[q] = mn[q];
@@ -1460,14 +1465,19 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
     pair::adopt_lane0(valid, m, C, dt);
     const int kmax = pair::wg_rows<CPW>(s_rows, w, lane, nrows);
     const double *pq = pi;   // the next propagation's parameters (the reversed model)
+    const double *ou_src = nullptr;   // the OU constants per segment change only (k_fwd_level)
+    ggp::OU ou{};
     auto prop = [&](const bool act, const double t) {
         double mn[4], Cn[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) mn[q] = m[q];
 #pragma unroll
         for (int q = 0; q < 16; ++q) Cn[q] = C[q];
-        pair::propagate_w<Q, CPW>(w, mn, Cn, t, ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]), s_tab, s_x,
-                                  s_d, s_i, s_o, lane);
+        if (pq != ou_src) {
+            ou = ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]);
+            ou_src = pq;
+        }
+        pair::propagate_w<Q, CPW>(w, mn, Cn, t, ou, s_tab, s_x, s_d, s_i, s_o, lane);
         if (act) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) m[q] = mn[q];
