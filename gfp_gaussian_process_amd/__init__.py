@@ -6,11 +6,11 @@ behind the C-ABI of include/ggp.h.  This package is the thin host-side mirror of
 reference's objective entry points (see forest.py for the mapping).
 """
 from .forest import (  # noqa: F401
-    CSVConfig, Dataset, Forest, GGPError, HostForest, LikelihoodIsNan, ParameterSet,
+    CSVConfig, Dataset, EvaluationStalled, Forest, GGPError, HostForest, LikelihoodIsNan, ParameterSet,
     PARAM_NAMES, total_likelihood, total_likelihood_log_params, total_likelihood_nlopt,
 )
 
 __all__ = [
-    "CSVConfig", "Dataset", "Forest", "GGPError", "HostForest", "LikelihoodIsNan", "ParameterSet",
+    "CSVConfig", "Dataset", "EvaluationStalled", "Forest", "GGPError", "HostForest", "LikelihoodIsNan", "ParameterSet",
     "PARAM_NAMES", "total_likelihood", "total_likelihood_log_params", "total_likelihood_nlopt",
 ]

@@ -12,7 +12,7 @@ import os
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_PKG, "lib")
 
-GGP_OK, GGP_EINVAL, GGP_ENAN, GGP_EDEV, GGP_ENOMEM = 0, 1, 2, 3, 4
+GGP_OK, GGP_EINVAL, GGP_ENAN, GGP_EDEV, GGP_ENOMEM, GGP_ETIMEOUT = 0, 1, 2, 3, 4, 5
 N_PARAMS = 11
 STATE = 20
 KERNELS = {"auto": 0, "lane": 1, "group": 2, "wave": 3, "pair": 4}

@@ -34,6 +34,7 @@
 #include "ggp_prop.h"
 #include "ggp_outtab.h"
 #include "ggp_wave.h"
+#include "ggp_wave2.h"
 #include "ggp_predict.h"
 #include "ggp_joints.h"
 
@@ -1138,6 +1139,330 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     if (red) chain_reduce(*red, call_seq, blockIdx.x, lane, cell_ll, cell_nan);
 }
 
+// ------------------------------------------------------------------------------------------
+// WAVE schedule with the distributed state (ggp_wave2.h): one 64-lane wave per cell, the
+// 20-double state spread over lanes 0-19 (lane e owns entry e), stage B's exponentials and
+// Dawson values in one Horner stream, products for the 22 exponentials exp(c + ...) that differ
+// from a computed one by a cached exp(k t).  Same launch forms as k_loglik_wave (path launch:
+// seq != nullptr; level launch: one cell per block), same chain hand-offs and in-launch reduction.
+// A second daughter whose parent does not finish within spin_max polls ends as a stall (NaN
+// total, row kRowStall: GGP_ETIMEOUT on the host), never as a model NaN.
+// ------------------------------------------------------------------------------------------
+constexpr int kRowStall = 0xffffff;   // a cell never has 2^24 - 1 rows (ggp_forest_create checks)
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave2(
+    DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
+    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
+    const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed *__restrict__ red, const int64_t call_seq,
+    const unsigned spin_max)
+{
+    namespace W = ggp::wave;
+    namespace W2 = ggp::w2;
+    [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // GGP_STAMPS builds only
+    __shared__ __attribute__((aligned(16))) double lds[W2::kLds];
+    const int lane = threadIdx.x;
+    GGP_PSTAMP_DECL;
+    GGP_PSTAMP(0);
+    lds_fill<W2::kTabRows * W2::kTabRow>(lds + W2::L_TAB, lane, [](const int k) { return W2::tab_entry(k); });
+    GGP_PSTAMP(1);
+    const double *p = P.p;
+    const W2::LaneC LC = W2::kLaneTab.l[lane];   // this lane's row of the compile-time table
+    W2::Lane L;
+    {
+        const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        lds[W2::L_MONO + lane] = W2::lane_kappa(lane, ou);   // the 33 kappas, one per lane (MONO is free here)
+        __syncthreads();
+        L = W2::lane_from(lane, LC, ou, lds + W2::L_MONO);
+        __syncthreads();
+    }
+    const double var_x = p[7], var_g = p[8], var_dx = p[9], var_dg = p[10], b = p[6];
+    if (lane == 0) {
+        lds[W2::L_X + ggp::X_ONE] = 1.0;
+        lds[W2::L_BV + ggp::BV_ONE] = 1.0;
+        lds[W2::L_V + ggp::V_ONE] = 1.0;
+        lds[W2::L_ONE1] = 1.0;
+        lds[W2::L_ZERO] = 0.0;
+    }
+    GGP_PSTAMP(2);
+    // exp(s t) and the exp-derived basis depend on the parameters and dt only; dt compared by its
+    // bits (a NaN pattern no time difference produces: nothing cached yet)
+    unsigned long long dt_cached = 0x7ff4dead0000beefULL;
+    GGP_STAMP_DECL;
+    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
+    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
+    int64_t prev_last = -1;
+    // the cell's first state into POST (lanes' entries) and V (stage D's variables), from registers
+    // holding the same values in every lane (once per cell)
+    auto scatter = [&](const double *m, const double *C) {
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v = lane == k ? m[k] : v;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v = lane == 4 + k ? C[k] : v;
+        lds[L.u_post] = v;
+        lds[L.u_v] = v - L.u_vshift;
+    };
+    // one propagation of the state in POST / V over dt: the raw outputs in OUT (after a barrier)
+    auto propagate = [&](const double dt) {
+        GGP_STAMP(0);
+        const long long db = __double_as_longlong(dt);
+        const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
+                                         (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
+        if (dbits != dt_cached) {   // lane constants and kernel arguments only: no OU values live in the loop
+            if (lane < 7) lds[lane < 6 ? W2::L_X + ggp::XS_bt + lane : W2::L_XPGQ] = exp(L.c_sv * dt);
+            __syncthreads();
+            if (lane < ggp::kNDerived)
+                lds[W2::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W2::L_X, p[1], dt);
+            if (lane == 0) lds[W2::L_V + ggp::V_T] = dt;
+            __syncthreads();
+            dt_cached = dbits;
+        }
+        const double *po = lds + W2::L_POST;
+        const W::WStep S = W2::wstep2(po[0], po[2], po[4], po[6], po[14], dt, b);
+        if (lane == 0) W::store_pw(S, lds + W2::L_PW);
+        lds[L.mo_dst] = W2::mono(L, lds);   // stage D's monomials of this state
+        GGP_STAMP(1);
+        {   // stage B: one exponential or Dawson value per lane
+            const W2::BOut o = W2::stageB(S, L, lds);
+            double v = o.v;
+            if (__builtin_amdgcn_ballot_w64(o.rare)) v = o.rare ? W2::stageB_rare(L.b_isD, o.arg, o.z, o.v) : v;
+            lds[L.b_dst] = v;
+        }
+        GGP_STAMP(2);
+        __syncthreads();
+        GGP_STAMP(3);
+        lds[L.i_dst] = W2::stageC(S, L, lds);   // stage C: one integral per lane
+        GGP_STAMP(4);
+        __syncthreads();
+        GGP_STAMP(5);
+        double acc = W2::stageD(L, lds);   // stage D: the lane's output terms
+        GGP_STAMP(6);
+        {   // block sums: DPP butterfly (ggp::out_partner)
+            const int bs = L.d_bs;
+            double w;
+            w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
+            w = dpp_f64<0x4E>(acc);  acc = bs > 2 ? acc + w : acc;
+            w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
+            w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
+        }
+        lds[L.d_out] = acc;
+        GGP_STAMP(7);
+        __syncthreads();
+    };
+    for (int i = i_lo; i < i_hi; ++i) {
+        const int c = cells[i];
+        const int2 ch = chain[c];
+        bool chain_broken = false;
+        if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            // the parent runs in this launch and is not done: sleep through ~0.5 us per parent row
+            // without polling, then poll (relaxed agent-scope loads); spin_max polls at most
+            if (spin_max > 0) {
+                const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+                const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
+                while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
+            }
+            unsigned spins = 0;
+            while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                if (++spins > spin_max) {
+                    chain_broken = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+        double dt = 0.0;
+        bool pending;
+        if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in POST / V
+            pending = true;
+            dt = F.time[r0] - F.time[prev_last];
+        } else if (ch.x >= 0) {   // a second daughter of a cell in another path: lane e takes entry e
+            if (lane < 20) {
+                const double v = ld_agent(state + (size_t)20 * ch.x + lane);
+                lds[L.u_post] = v;
+                lds[L.u_v] = v - L.u_vshift;
+            }
+            pending = true;
+            dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
+        } else {
+            double m[4], C[16];
+            pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+            scatter(m, C);
+        }
+        const bool divide = pending;
+        double t_cur = F.time[r0];
+        prev_last = r1 - 1;
+        GGP_PSTAMP(3);
+        // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane)
+        auto load_chunk = [&](const int64_t base) {
+            const int64_t rr = base + lane;
+            double a = 0.0, bb = 0.0, t = 0.0;
+            if (rr < r1) {
+                a = F.logl[rr];
+                bb = F.fp[rr];
+                t = F.time[rr];
+            }
+            lds[W2::L_ROWL + lane] = a;
+            lds[W2::L_ROWF + lane] = bb;
+            lds[W2::L_ROWT + lane] = t;
+            if (lane == 0) lds[W2::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
+        };
+        load_chunk(r0);
+        __syncthreads();
+        double cl = 0.0;
+        int nan_row = kNanNone;
+        int slot = 0;                    // row - chunk base
+        const int nrows = (int)(r1 - r0);
+        int left = nrows;                // rows from the current one on
+        bool live = !chain_broken;
+        if (chain_broken) {
+            cl = __longlong_as_double(0x7ff8000000000000LL);
+            nan_row = kRowStall;
+        }
+        // after a step: the ll ring is flushed every 64 rows (and at the cell's end), then the
+        // next chunk loaded.  false = stop (a NaN term; nan_row set)
+        auto end_step = [&]() -> bool {
+            ++slot;
+            --left;
+            live = left > 0;
+            if (slot == 64 || !live) {
+                const int done = nrows - left;
+                const int64_t base = done - slot;
+                __syncthreads();
+                if (lane < slot) {
+                    const double s00 = lds[W2::L_RS0 + lane], s01 = lds[W2::L_RS1 + lane], s11 = lds[W2::L_RS2 + lane];
+                    lds[W2::L_RT + lane] = W::ll_quad(lds[W2::L_RX0 + lane], lds[W2::L_RX1 + lane], s00, s01, s11) -
+                                           0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - F.two_log_2pi;
+                }
+                __syncthreads();
+                bool ok = true;
+                if (lane == 0) {
+                    // the terms in row order (the reference's running sum), unrolled for a full chunk;
+                    // the scan for the first NaN row only when the chunk's sum is NaN
+                    double acc = cl;
+                    if (slot == 64) {
+#pragma unroll
+                        for (int k = 0; k < 64; ++k) acc += lds[W2::L_RT + k];
+                    } else {
+                        for (int k = 0; k < slot; ++k) acc += lds[W2::L_RT + k];
+                    }
+                    if (acc != acc) {
+                        acc = cl;
+                        for (int k = 0; k < slot; ++k) {
+                            acc += lds[W2::L_RT + k];
+                            if (acc != acc) {
+                                nan_row = (int)(base + k);
+                                ok = false;
+                                break;
+                            }
+                        }
+                    }
+                    cl = acc;
+                }
+                if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) return false;
+                slot = 0;
+                if (live) load_chunk(r0 + done);
+            }
+            GGP_STAMP(10);
+            __syncthreads();   // the LDS slots are rewritten by the next step
+            return true;
+        };
+        GGP_PSTAMP(4);
+        if (live) {   // the cell's first step: uniform registers (no propagation / division map)
+            const double y_l = lds[W2::L_ROWL], y_f = lds[W2::L_ROWF];
+            const double t_next = left > 1 ? lds[W2::L_ROWT + 1] : 0.0;
+            double m[4], C[16];
+            if (pending) {
+                propagate(dt);
+                double o[ggp::kOutN];
+#pragma unroll
+                for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W2::L_OUT + k];
+#pragma unroll
+                for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j
+                    if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
+                ggp::out_store(o, m, C);
+                if (divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) m[k] = lds[W2::L_POST + k];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) C[k] = lds[W2::L_POST + 4 + k];
+            }
+            const double x0 = y_l - m[0], x1 = y_f - m[1];
+            const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
+            if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
+                lds[W2::L_RX0 + slot] = x0;
+                lds[W2::L_RX1 + slot] = x1;
+                lds[W2::L_RS0 + slot] = v.S00;
+                lds[W2::L_RS1 + slot] = v.S01;
+                lds[W2::L_RS2 + slot] = v.S11;
+            }
+            W::posterior(m, C, x0, x1, v, true);
+            scatter(m, C);
+            pending = left > 1;
+            if (pending) dt = t_next - t_cur;
+            t_cur = t_next;
+            if (!end_step()) live = false;
+        }
+        GGP_PSTAMP(5);
+        while (live) {   // steady steps: the state distributed over lanes 0-19
+            GGP_STAMP_STEP();
+            const double t_next = left > 1 ? lds[W2::L_ROWT + slot + 1] : 0.0;
+            propagate(dt);
+            {
+                lds[L.f_dst] = W2::finish(L, lds, slot);   // the prior's entries, -x0, -x1
+                // meanwhile every lane forms the innovation from the raw outputs: the same values
+                // lanes 1, 4, 5, 9, 20, 24 finish (fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11)
+                const double *o = lds + W2::L_OUT;
+                const double o0 = o[0], o1 = o[1];
+                const double nx0 = o0 - lds[W2::L_ROWL + slot], nx1 = o1 - lds[W2::L_ROWF + slot];
+                const W2::UInnov v = W2::uinnov(o1, o[4], __builtin_fma(-o0, o1, o[5]), __builtin_fma(-o1, o1, o[8]), var_x, var_g,
+                                                F.scaled, F.fp_auto);
+                if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
+                    lds[W2::L_RX0 + slot] = nx0;
+                    lds[W2::L_RX1 + slot] = nx1;
+                    lds[W2::L_RS0 + slot] = v.S00;
+                    lds[W2::L_RS1 + slot] = v.S01;
+                    lds[W2::L_RS2 + slot] = v.S11;
+                }
+                GGP_STAMP(8);
+                __syncthreads();
+                const double up = W2::upost(L, lds, v);
+                lds[L.u_post] = up;
+                lds[L.u_v] = up - L.u_vshift;
+            }
+            GGP_STAMP(9);
+            dt = t_next - t_cur;
+            t_cur = t_next;
+            if (!end_step()) break;
+        }
+        GGP_PSTAMP(6);
+        __syncthreads();
+        // the cell's results; its state from lanes 0-19 (one coalesced store), agent-coherent with
+        // the flag after it when a second daughter waits for it
+        if (lane == 0) {
+            st_agent(cell_ll + F.dfs_rank[c], cl);   // coherent: a path launch sums them in-launch
+            st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
+        }
+        if (lane < 20) {
+            const double v = lds[W2::L_POST + lane];
+            if (ch.y)
+                st_agent(state + (size_t)20 * c + lane, v);
+            else
+                state[(size_t)20 * c + lane] = v;
+        }
+        if (ch.y) {
+            __builtin_amdgcn_s_waitcnt(0);   // every lane's stores at the coherence point, then the flag
+            if (lane == 0) __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        GGP_PSTAMP(7);
+        __syncthreads();   // the LDS rows and ring are the next cell's
+    }
+    GGP_STAMP_FLUSH();
+    GGP_PSTAMP_FLUSH();
+    if (red) chain_reduce(*red, call_seq, blockIdx.x, lane, cell_ll, cell_nan);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // -p smoother kernels (lane schedule).  Parameters per row come from the segment table.
@@ -2067,6 +2392,8 @@ struct Shard {
     unsigned *d_cell_done = nullptr;
     unsigned epoch = 0;
     int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
+    int wave_v1 = 0;                   // GGP_WAVE_V1=1: the r20 wave kernel (k_loglik_wave), A/B only
+    unsigned spin_max = 1u << 24;      // GGP_CHAIN_SPIN_MAX: polls of a waiting second daughter (~20 s)
     int32_t *d_path_cells = nullptr, *d_path_seq = nullptr;   // path launch: cells, [n_paths + 1] starts
     int64_t n_paths = 0;               // 0: level launches
     // path launch's in-launch reduction (ChainRed): path -> block, paths per block, the blocks'
@@ -2207,9 +2534,14 @@ int launch_levels(Shard *f, const ggp_params &P)
     };
     if (f->n_paths > 0) {   // every level on the wave schedule: one launch, one block per path
         HIPCHK(prof_begin());
-        hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
-                           f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
-                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq);
+        if (f->wave_v1)
+            hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
+                               f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
+                               f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq);
+        else
+            hipLaunchKernelGGL(k_loglik_wave2, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
+                               f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
+                               f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max);
         HIPCHK(hipGetLastError());
         f->kernel_used = GGP_KERNEL_WAVE;
         f->last_code = GGP_KERNEL_WAVE << 8 | 64;
@@ -2224,9 +2556,14 @@ int launch_levels(Shard *f, const ggp_params &P)
         const int64_t n_simd = (int64_t)f->n_cu * 4;
         const int kind = f->level_kind[L];
         if (kind == GGP_KERNEL_WAVE) {
-            hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                               f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
-                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
+            if (f->wave_v1)
+                hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                                   f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
+                                   (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
+            else
+                hipLaunchKernelGGL(k_loglik_wave2, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                                   f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
+                                   (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
         } else if (kind == GGP_KERNEL_PAIR) {
@@ -2500,6 +2837,8 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
     f->pair_max_cells = (int64_t)f->n_cu * 64 * 2;   // r13 scan: two rounds of 64-cell pair workgroups
     if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
+    if (const char *e = getenv("GGP_WAVE_V1")) f->wave_v1 = atoi(e) != 0;
+    if (const char *e = getenv("GGP_CHAIN_SPIN_MAX")) f->spin_max = (unsigned)strtoul(e, nullptr, 10);
     if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
     if (const char *e = getenv("GGP_GROUP_CPW")) {
@@ -2644,7 +2983,9 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             all_wave = all_wave && f->level_kind[L] == GGP_KERNEL_WAVE;
         }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0) == hipSuccess && per_cu > 0)
+        const hipError_t oe = f->wave_v1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0)
+                                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave2, 64, 0);
+        if (oe == hipSuccess && per_cu > 0)
             f->wave_resident = per_cu * f->n_cu;
         if (const char *e = getenv("GGP_WAVE_PATHS_MAX")) f->wave_resident = atoi(e);
         std::vector<int2> ch(nc, int2{-1, 0});
@@ -2952,6 +3293,7 @@ const char *ggp_strerror(int code)
     case GGP_ENAN: return "Likelihood is Nan";
     case GGP_EDEV: return g_last_err.empty() ? "HIP device error" : g_last_err.c_str();
     case GGP_ENOMEM: return "device allocation failed";
+    case GGP_ETIMEOUT: return g_last_err.empty() ? "evaluation stalled (timeout)" : g_last_err.c_str();
     default: return "unknown error";
     }
 }
@@ -3359,8 +3701,12 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
     if (code != kNoNan) {
         const int64_t rank = code >> 24, row = code & 0xffffff;
         if (nan_cell) *nan_cell = f->dfs_order[rank];
-        if (nan_row) *nan_row = row;
+        if (nan_row) *nan_row = row == kRowStall ? -1 : row;
         if (ll) *ll = std::nan("");
+        if (row == kRowStall) {   // the first bad cell in reference order waited for its parent too long
+            g_last_err = "evaluation stalled: a daughter cell's wait for its parent timed out (a scheduling stall, not a NaN)";
+            return GGP_ETIMEOUT;
+        }
         return GGP_ENAN;
     }
     if (std::isnan(v)) return GGP_ENAN;   // NaN from +inf + -inf across cells (see include/ggp.h)

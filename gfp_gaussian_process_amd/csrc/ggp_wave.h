@@ -252,6 +252,7 @@ GGP_DEV double dawson_arg(const WStep &S, const LaneTasks &T)
 // Horner with fused multiply-adds (<= 1 ulp from the separate-rounding form; the device
 // Dawson stays within the reference's bound, tests/test_gpu_device_math.py)
 constexpr int kDawsonRow = 10;
+#ifndef GGP_HOST_SIM
 GGP_DEV double dawson_bf(const double x, const double *tab)
 {
     const double ax = fabs(x);
@@ -295,6 +296,8 @@ GGP_DEV double dawson_bf(const double x, const double *tab)
     }
     return GGP_SPI2 * (x < 0.0 ? -w : w);
 }
+
+#endif  // GGP_HOST_SIM
 
 // The tauint denominators of k = 0..3 (2 sqrt a, then pow_task's 4 a^1.5, 8 a^2.5, 16 a^3.5)
 // and their rdiv seeds (r_two_sa, then 1/(4 a^1.5) = 2 r4a r2sa and each next power one factor

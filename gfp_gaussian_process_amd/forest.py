@@ -43,6 +43,12 @@ class LikelihoodIsNan(GGPError):
         super().__init__(f"Likelihood is Nan (cell {cell_id or cell}, row {row})")
 
 
+class EvaluationStalled(GGPError):
+    """GGP_ETIMEOUT: a wait inside one evaluation timed out (a daughter cell's wait for its parent,
+    or a peer rank's collective) -- a scheduling failure, never reported as LikelihoodIsNan.  The
+    carried state is unspecified afterwards, as after a NaN."""
+
+
 def _host_err() -> str:
     return (N.host().ggp_host_last_error() or b"").decode()
 
@@ -443,8 +449,14 @@ class Forest:
         rc = self._lib.ggp_total_loglik(self._h, self._p_ptr, *self._out_refs)
         if rc == N.GGP_ENAN:
             raise self._nan(self._nc.value, self._nr.value)
+        self._stalled(rc)
         self._check(rc)
         return self._ll.value
+
+    def _stalled(self, rc):
+        if rc == N.GGP_ETIMEOUT:
+            self._poisoned = True
+            raise EvaluationStalled(self._lib.ggp_strerror(rc).decode())
 
     # -- one process per GPU: the engine's own RCCL collective (include/ggp.h ggp_comm_attach) --
     def comm_attach(self, nranks: int, rank: int, uid: bytes, rccl_lib: str | None = None) -> None:
@@ -469,6 +481,7 @@ class Forest:
         rc = self._lib.ggp_loglik_result(self._h, ctypes.byref(ll), ctypes.byref(nc), ctypes.byref(nr))
         if rc == N.GGP_ENAN:
             raise self._nan(nc.value, nr.value)
+        self._stalled(rc)
         self._check(rc)
         return ll.value
 

@@ -52,6 +52,10 @@ extern "C" {
 #define GGP_ENAN 2     /* log-likelihood is NaN (likelihood.h:71-93)             */
 #define GGP_EDEV 3     /* HIP runtime / device error                             */
 #define GGP_ENOMEM 4   /* device allocation failed                               */
+#define GGP_ETIMEOUT 5 /* a wait inside one evaluation timed out: a daughter cell's
+                          wait for its parent (a scheduling stall, never a model NaN),
+                          or a peer rank that never reached the collective; the carried
+                          state is unspecified afterwards, as after GGP_ENAN          */
 
 #define GGP_N_PARAMS 11      /* Parameters.h:175 order                           */
 #define GGP_STATE_DOUBLES 20 /* per cell/row: mean[4] then cov[16] row-major     */

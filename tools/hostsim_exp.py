@@ -22,7 +22,8 @@ L = O.lib(sens=True)
 FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p)
 L.ora_set_mcm_hook.argtypes = [ctypes.c_void_p]
 HOOKS = {"oracle": None, "lane": ctypes.cast(HS.hs_mcm_lane, ctypes.c_void_p).value,
-         "tab": ctypes.cast(HS.hs_mcm_tab, ctypes.c_void_p).value}
+         "tab": ctypes.cast(HS.hs_mcm_tab, ctypes.c_void_p).value,
+         "w2": ctypes.cast(HS.hs_mcm_w2, ctypes.c_void_p).value}
 
 G = os.path.join(ROOT, "tests", "golden")
 tmp = tempfile.mkdtemp()
@@ -66,4 +67,5 @@ for name, a, p in cases:
     L.ora_set_mcm_hook(None)
     base = res["oracle"]
     print(f"{name:28s} ll {base[0]:.10g}  lane rel {np.max(np.abs(res['lane'] - base) / np.abs(base)):.2e}"
-          f"  tab rel {np.max(np.abs(res['tab'] - base) / np.abs(base)):.2e}")
+          f"  tab rel {np.max(np.abs(res['tab'] - base) / np.abs(base)):.2e}"
+          f"  w2 rel {np.max(np.abs(res['w2'] - base) / np.abs(base)):.2e}")
