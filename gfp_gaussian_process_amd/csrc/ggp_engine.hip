@@ -1219,7 +1219,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         const double *po = lds + W2::L_POST;
         const W::WStep S = W2::wstep2(po[0], po[2], po[4], po[6], po[14], dt, b);
-        if (lane == 0) W::store_pw(S, lds + W2::L_PW);
         lds[L.mo_dst] = W2::mono(L, lds);   // stage D's monomials of this state
         GGP_STAMP(1);
         {   // stage B: one exponential or Dawson value per lane
@@ -1410,13 +1409,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             const double t_next = left > 1 ? lds[W2::L_ROWT + slot + 1] : 0.0;
             propagate(dt);
             {
-                lds[L.f_dst] = W2::finish(L, lds, slot);   // the prior's entries, -x0, -x1
-                // meanwhile every lane forms the innovation from the raw outputs: the same values
-                // lanes 1, 4, 5, 9, 20, 24 finish (fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11)
+                // every lane forms the innovation from the raw outputs (the values lanes 1, 4, 5, 9,
+                // 20, 24 finish: fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11), its loads issued
+                // with the finish's before any store
                 const double *o = lds + W2::L_OUT;
-                const double o0 = o[0], o1 = o[1];
-                const double nx0 = o0 - lds[W2::L_ROWL + slot], nx1 = o1 - lds[W2::L_ROWF + slot];
-                const W2::UInnov v = W2::uinnov(o1, o[4], __builtin_fma(-o0, o1, o[5]), __builtin_fma(-o1, o1, o[8]), var_x, var_g,
+                const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
+                const double yl = lds[W2::L_ROWL + slot], yf = lds[W2::L_ROWF + slot];
+                const double fv = W2::finish(L, lds, slot);   // the prior's entries, -x0, -x1
+                lds[L.f_dst] = fv;
+                const double nx0 = o0 - yl, nx1 = o1 - yf;
+                const W2::UInnov v = W2::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, var_g,
                                                 F.scaled, F.fp_auto);
                 if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
                     lds[W2::L_RX0 + slot] = nx0;

@@ -469,32 +469,44 @@ struct BOut {
     bool rare;
 };
 
+GGP_DEV void sched_fence()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
 {
+    // the Dawson argument and interval first, so the table row's six 128-bit LDS reads are in
+    // flight while the exponential's argument and reduction are formed (exp lanes read the exp row)
     const double ti = S.t * L.b_tau;
     const double B = wave::pin(__builtin_fma(S.Cxl, L.b_km, S.bbl) + L.b_gqks);
+    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
+    const double ax = fabs(z);
+    const double y100 = 100.0 * rcp1(1.0 + ax);
+    const int k = min(cvt_i32(y100), GGP_DAWSON_NINT - 1);
+    const int row = L.b_isD ? k * kTabRow : kExpRow * kTabRow;
+    const double *A = lds + L_TAB + row;
+    double a[kTabRow];
+#pragma unroll
+    for (int i = 0; i < kTabRow; ++i) a[i] = A[i];
+    sched_fence();
     const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
     const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
-    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
     const double argA = wave::pin(ti * (B + S.a * ti));
     const double argE = wave::pin(n + c + z * z);
     const double argZ = wave::pin(S.a * (ti * ti) + B * ti + c);
     const double arg = L.b_isE ? argE : L.b_isA ? argA : argZ;
-    // exp reduction (exp_ocml)
+    // exp reduction (exp_ocml); Dawson: the Chebyshev variable of interval k
     const double dn = __builtin_rint(arg * 0x1.71547652b82fep+0);
     double r = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, arg);
     r = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, r);
-    // Dawson reduction (ggp_wave.h dawson_bf): interval k of y100 = 100 / (1 + |z|)
-    const double ax = fabs(z);
-    const double y100 = 100.0 * rcp1(1.0 + ax);
-    const int k = min(cvt_i32(y100), GGP_DAWSON_NINT - 1);
     const double td = __builtin_fma(2.0, y100, -(double)(2 * k + 1));
     const double tv = L.b_isD ? td : r;
-    const int row = L.b_isD ? k * kTabRow : kExpRow * kTabRow;
-    const double *A = lds + L_TAB + row;
-    double h = __builtin_fma(A[0], tv, A[1]);
+    double h = __builtin_fma(a[0], tv, a[1]);
 #pragma unroll
-    for (int i = 2; i < kTabRow; ++i) h = __builtin_fma(h, tv, A[i]);
+    for (int i = 2; i < kTabRow; ++i) h = __builtin_fma(h, tv, a[i]);
     // no branches below: the exponent masked to 0 on Dawson lanes, the rare flags by bitwise ops
     double v = __builtin_ldexp(h * L.b_mult, cvt_i32(dn) & L.b_exmask);
     v = ((L.b_isD != 0) & (z < 0.0)) ? -v : v;
@@ -516,7 +528,6 @@ GGP_DEV double stageC(const wave::WStep &S, const Lane &L, const double *lds)
     const double E1 = lds[L.i_e1r] * lds[L.i_e1f];
     const double ec = lds[L.i_ecr] * lds[L.i_ecf];
     const double ea0 = lds[L.i_a0], ea1 = lds[L.i_a1];
-    const double den = lds[L.i_pw], rden = lds[L.i_pw + 4];
     const double B = wave::pin(__builtin_fma(S.Cxl, L.i_km, S.bbl) + L.i_gqks);
     const double t0 = S.t * L.i_tau0, t1 = S.t * L.i_tau1;
     const double BB = wave::pin(B * B);
@@ -530,7 +541,12 @@ GGP_DEV double stageC(const wave::WStep &S, const Lane &L, const double *lds)
     const double S1 = S.two_sa * L.i_S1;
     const double dterm = wave::pin(Q * (E0 * D0 - E1 * D1));
     const double x = S1 * ec * (ea0 * P0 - ea1 * P1) + dterm;
-    return rdiv(x, den, rden);
+    // the denominator 2^(k+1) a^k sqrt(a) as two_sa (2a)^k: the products of store_pw's
+    // denominators (scaling by powers of two is exact), and an rdiv seed from v_rcp_f64
+    const double p1 = S.two_a, p2 = p1 * p1, p3 = p2 * p1;
+    const double qk = __builtin_fma(L.i_s3, p3, __builtin_fma(L.i_s2, p2, __builtin_fma(L.i_s1, p1, -0.5 * L.i_s0)));
+    const double den = S.two_sa * qk;
+    return rdiv(x, den, rcp1(den));
 }
 
 // ---- stage D: the lane's output terms over the step's monomials ------------------------------
