@@ -32,6 +32,7 @@ BYTES_PER_UPDATE = 24          # time + log_length + fp doubles
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (AMD spec)
 COMBINE_BYTES_PER_ROW = 484   # k_combine: fwd + bwd rows (2 x 160 B) + prior segment (4 B) read, 160 B written
 VALU_ISSUE_CYCLES = 4          # cycles a SIMD takes per 64-lane FP64 VALU wave-instruction (16 lanes/cycle)
+VALU32_ISSUE_CYCLES = 2        # ... per 32-bit VALU wave-instruction (32-wide SIMD, MI355X_MICROARCH.md)
 CLOCK_HZ = 2.4e9               # MI355X peak engine clock (MI355X_MICROARCH.md)
 P_EXAMPLE = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04,
              3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]   # example_data_set/parameter_file.txt
@@ -116,6 +117,59 @@ def cpu_baseline_parallel(hf, budget_s: float, threads: int):
     return n_eval * hf.n_rows / el, n_eval, el
 
 
+def example_mp(tmp: str, cpu_budget: float):
+    """The reference's published workload (example_data_set/README.txt:1-3: `-m -p` on the example,
+    "around 5min"): the drop-in CLI lib/ggp with the reference's own arguments on the committed
+    example files, one GPU.  Evaluations = the Nelder-Mead objective calls (one _iterations.csv row
+    each, likelihood.h:142-148) + the chained Hessian error bars (3 epsilons x 4 k^2 points,
+    likelihood.h:211-258, k = free parameters).  cpu_estimate_s = evaluations x the 1-core oracle's
+    ms per evaluation of the same example forest, measured here."""
+    import gzip
+    import shutil
+    import subprocess
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    gold = os.path.join(ROOT, "tests", "golden")
+    os.makedirs(tmp, exist_ok=True)
+    csv = os.path.join(tmp, "input.csv")
+    with gzip.open(os.path.join(gold, "example_input.csv.gz"), "rb") as fi, open(csv, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    par = os.path.join(gold, "example_parameter_file.txt")
+    cfg = os.path.join(gold, "example_csv_config.txt")
+    out = os.path.join(tmp, "out")
+    cli = os.path.join(ROOT, "gfp_gaussian_process_amd", "lib", "ggp")
+    t0 = time.perf_counter()
+    r = subprocess.run([cli, "-i", csv, "-b", par, "-c", cfg, "-m", "-p", "-g", "1", "-o", out],
+                       capture_output=True, text=True, timeout=1200)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-400:]}
+    its = [f for f in os.listdir(out) if f.endswith("_iterations.csv")]
+    n_nm = sum(1 for _ in open(os.path.join(out, its[0]))) - 1 if its else 0
+    ps = g.ParameterSet.load(par)
+    k = len(ps.non_fixed())
+    n_hess = 3 * 4 * k * k
+    n_eval = n_nm + n_hess
+    # the 1-core oracle on the same forest (init values), evaluations until the budget is spent
+    hf = g.HostForest.from_csv(csv, cfg, -1, "scaled", "binomial")
+    of = O.OracleForest(hf.a)
+    pinit = ps.get_init()
+    n, t1 = 0, time.perf_counter()
+    while True:
+        of.total_likelihood(pinit)
+        n += 1
+        if time.perf_counter() - t1 >= cpu_budget:
+            break
+    cpu_ms = 1e3 * (time.perf_counter() - t1) / n
+    return {"wall_s": wall, "n_evals": n_eval, "n_nelder_mead": n_nm, "n_hessian": n_hess, "free_params": k,
+            "ms_per_eval": 1e3 * wall / n_eval, "rows": hf.n_rows,
+            "cpu_ms_per_eval_1core": cpu_ms, "cpu_estimate_s": n_eval * cpu_ms / 1e3,
+            "reference_published": "around 5min (example_data_set/README.txt:1-3, hardware not stated)",
+            "note": "lib/ggp -i input.csv -b parameter_file.txt -c csv_config.txt -m -p -g 1 (the reference's "
+                    "command), wall time of the whole CLI run incl. ingest, -p and output files; ms_per_eval = "
+                    "wall / evaluations (an upper bound per evaluation)"}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,6 +186,11 @@ def main() -> int:
                     help="also time the -p smoother on a C5-shard forest: trees per GPU (0 = skip)")
     ap.add_argument("--hessian", type=int, default=1, help="also time the batched 11-parameter Hessian (0 = skip)")
     ap.add_argument("--predict-rows", type=int, default=500, help="rows per tree of the -p forest")
+    ap.add_argument("--example-mp", type=int, default=1,
+                    help="also time the reference's published workload: the CLI's -m -p on the example (N=1; 0 = skip)")
+    ap.add_argument("--inprocess", type=int, default=1,
+                    help="N > 1: also time the CLI's in-process device-list path (one process, every rank's trees "
+                         "sharded over devices 0..N-1, include/ggp.h) on rank 0 while the others wait (0 = skip)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo: rehearsal of the "
                          "multi-rank path on one GPU, the per-call 16 B through host memory)")
@@ -211,7 +270,7 @@ def main() -> int:
     # lanes and unused task candidates included -- an issue rate, not work done
     fp64 = None
     cnt = _profile_json("fp64_counts.json", args)
-    if cnt and dom == "k_loglik_wave" and avg_ms > 0 and cnt.get("useful_flops_per_update"):
+    if cnt and dom.startswith("k_loglik_wave") and avg_ms > 0 and cnt.get("useful_flops_per_update"):
         upd_s = (d_rows / d_n) / (avg_ms * 1e-3)
         useful = cnt["useful_flops_per_update"] * upd_s / 1e12
         issued = (cnt.get("issued_flops_per_update") or 0.0) * upd_s / 1e12
@@ -224,16 +283,23 @@ def main() -> int:
         # wave-instruction per 4 cycles (16 lanes/cycle); the PMC pass counts the wave's VALU
         # instructions per update (SQ_INSTS_VALU), so their issue time over every SIMD of the chip
         # for one launch, against the launch time at the 2.4 GHz peak clock
-        vpu = (cnt.get("wave") or {}).get("valu_wave_insts_per_update")
+        wv = cnt.get("wave") or {}
+        vpu = wv.get("valu_wave_insts_per_update")
+        f64pu = wv.get("f64_wave_insts_per_update")
         if vpu:
             n_simd = 4 * torch.cuda.get_device_properties(local).multi_processor_count
-            need = vpu * (d_rows / d_n) * VALU_ISSUE_CYCLES / n_simd
+            # issue cycles by class: 4 per FP64 wave-instruction (16 FP64 lanes/cycle), 2 per 32-bit one
+            # (32-wide SIMD); without the split (an older summary) every instruction at 4
+            cyc = (VALU_ISSUE_CYCLES * f64pu + VALU32_ISSUE_CYCLES * (vpu - f64pu)) if f64pu is not None \
+                else VALU_ISSUE_CYCLES * vpu
+            need = cyc * (d_rows / d_n) / n_simd
             have = avg_ms * 1e-3 * CLOCK_HZ
-            fp64["valu_issue"] = {"valu_wave_insts_per_update": vpu, "simds": n_simd,
-                                  "cycles_per_valu_inst": VALU_ISSUE_CYCLES, "clock_ghz": CLOCK_HZ / 1e9,
-                                  "frac": need / have,
-                                  "note": "VALU issue cycles the launch needs per SIMD / the launch's cycles: the "
-                                          "root level runs one wave per SIMD (latency), the daughters two (issue)"}
+            fp64["valu_issue"] = {"valu_wave_insts_per_update": vpu, "f64_wave_insts_per_update": f64pu,
+                                  "issue_cycles_per_update": cyc, "simds": n_simd,
+                                  "cycles_per_f64_inst": VALU_ISSUE_CYCLES, "cycles_per_32bit_inst": VALU32_ISSUE_CYCLES,
+                                  "clock_ghz": CLOCK_HZ / 1e9, "frac": need / have,
+                                  "note": "VALU issue cycles the launch needs per SIMD (class-weighted) / the launch's "
+                                          "cycles: the root level runs one wave per SIMD (latency), the daughters two"}
 
     # ---- the same path on a C4-shard-sized forest (BASELINE configs[3]: 100k trees over 8
     # GPUs = 12.5k trees per GPU), reported beside the C2 headline ----
@@ -308,6 +374,36 @@ def main() -> int:
                         "resident in HBM; rows_per_s is whole-job; not the headline value"}
         fp_.close()
 
+    # ---- N > 1: the drop-in CLI's own multi-GPU path (-g all): ONE process, the whole job's trees
+    # sharded over devices 0..N-1 inside the C-ABI (include/ggp.h), timed on rank 0 while the other
+    # ranks wait on the store (no GPU work of theirs meanwhile) ----
+    inproc = None
+    if world > 1 and args.inprocess:
+        store = dist.distributed_c10d._get_default_store()
+        barrier()
+        if rank == 0:
+            ha = g.HostForest.synthetic(args.trees * world, args.rows, seed=SEED)
+            fa = g.Forest(ha, devices=list(range(world)), kernel=args.kernel)
+            for _ in range(args.warmup):
+                fa.total_likelihood(P_EXAMPLE)
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                fa.total_likelihood(P_EXAMPLE)
+            iel = time.perf_counter() - t1
+            inproc = {"devices": world, "trees": args.trees * world, "rows": ha.n_rows, "steps": args.steps,
+                      "ms_per_step": 1e3 * iel / args.steps, "value": ha.n_rows * args.steps / iel,
+                      "shards": len(fa.shards()),
+                      "note": "one process drives every device (Forest(hf, devices=range(N)), the CLI's -g all): "
+                              "the whole job's forest, bitwise the single-device total; the same metric as value"}
+            fa.close()
+            store.set("ggp_inprocess_done", "1")
+        else:
+            store.wait(["ggp_inprocess_done"])
+        barrier()
+    exmp = None
+    if world == 1 and args.example_mp:
+        exmp = example_mp(os.path.join("/tmp", f"ggp_example_mp_{os.getpid()}"), 3.0 if not args.no_cpu else 0.5)
+
     result = None
     if rank == 0:
         result = {
@@ -354,6 +450,10 @@ def main() -> int:
             result["predict"] = pred
         if hess is not None:
             result["hessian_batch"] = hess
+        if exmp is not None:
+            result["example_mp"] = exmp
+        if inproc is not None:
+            result["inprocess"] = inproc
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

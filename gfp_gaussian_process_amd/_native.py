@@ -13,6 +13,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_PKG, "lib")
 
 GGP_OK, GGP_EINVAL, GGP_ENAN, GGP_EDEV, GGP_ENOMEM, GGP_ETIMEOUT = 0, 1, 2, 3, 4, 5
+GGP_ALL_DEVICES = -1   # ggp_forest_desc.n_devices: every visible device
 N_PARAMS = 11
 STATE = 20
 KERNELS = {"auto": 0, "lane": 1, "group": 2, "wave": 3, "pair": 4}
@@ -78,6 +79,7 @@ ENGINE_SYMBOLS = {
     "ggp_comm_attach": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_char_p]),
     "ggp_comm_nan_rank": (ctypes.c_int32, [ctypes.c_void_p]),
+    "ggp_comm_local_nan": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),
     "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "ggp_version": (ctypes.c_char_p, []),

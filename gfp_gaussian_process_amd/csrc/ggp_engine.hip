@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1224,7 +1225,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         {   // stage B: one exponential or Dawson value per lane
             const W2::BOut o = W2::stageB(S, L, lds);
             double v = o.v;
-            if (__builtin_amdgcn_ballot_w64(o.rare)) v = o.rare ? W2::stageB_rare(L.b_isD, o.arg, o.z, o.v) : v;
+            if (o.rare) v = W2::stageB_rare(L.b_isD, o.arg, o.z, o.v);   // skipped (execz) when no lane needs it
             lds[L.b_dst] = v;
         }
         GGP_STAMP(2);
@@ -2206,7 +2207,8 @@ __global__ __launch_bounds__(256) void k_rank_partial(const double *__restrict__
         for (int k = 0; k < 256; ++k) mc = min(mc, cm[k]);
         const double s = v[0];
         part[0] = s;
-        part[1] = (mc != kNoNan || s != s) ? 1.0 : 0.0;
+        // 2: this rank's first bad cell stalled (GGP_ETIMEOUT on every rank), 1: a NaN
+        part[1] = (mc != kNoNan && (mc & 0xffffff) == kRowStall) ? 2.0 : (mc != kNoNan || s != s) ? 1.0 : 0.0;
     }
 }
 
@@ -2220,7 +2222,8 @@ __global__ void k_rank_sum(const double *__restrict__ g, int nranks, double *out
     double s = 0.0;
     long long nr = -1;
     for (int r = 0; r < nranks; ++r) {
-        if (nr < 0 && g[2 * r + 1] != 0.0) nr = r;
+        // the first bad rank, + 2^32 when its first bad cell stalled
+        if (nr < 0 && g[2 * r + 1] != 0.0) nr = r + (g[2 * r + 1] == 2.0 ? (1LL << 32) : 0);
         s = s + g[2 * r];
     }
     __hip_atomic_store(reinterpret_cast<unsigned long long *>(out_sum),
@@ -2302,6 +2305,24 @@ __global__ __launch_bounds__(64) void k_debug_tauint(const double *__restrict__ 
 // host side
 // ------------------------------------------------------------------------------------------
 thread_local std::string g_last_err;
+
+// Every exported entry point that touches a device restores the caller's current HIP device on
+// return: the engine switches devices per shard (hipSetDevice), and a caller (torch, another
+// library) must find its own current device unchanged after any ggp_* call.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard()
+    {
+        int now = -1;   // hipSetDevice only when a shard switched it (the common one-device case: never)
+        if (dev >= 0 && (hipGetDevice(&now) != hipSuccess || now != dev)) (void)hipSetDevice(dev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
 
 #define HIPCHK(expr)                                                                        \
     do {                                                                                    \
@@ -2466,6 +2487,7 @@ struct RcclApi {
     int (*comm_init_rank)(void **, int, ggp_rccl_id, int) = nullptr;
     int (*all_gather)(const void *, void *, size_t, int, void *, hipStream_t) = nullptr;
     int (*comm_destroy)(void *) = nullptr;
+    int (*comm_abort)(void *) = nullptr;   // ncclCommAbort (optional)
     const char *(*error_string)(int) = nullptr;
 };
 constexpr int kRcclUint8 = 1;   // ncclUint8 (rccl.h ncclDataType_t)
@@ -2484,7 +2506,22 @@ struct Comm {
     int64_t *m_rank = nullptr, *m_seq = nullptr;
     int64_t seq = 0;
     int32_t last_nan_rank = -1;
+    int32_t local_nan = 0;             // this rank's own evaluation had a NaN (or stalled) last call
+    bool failed = false;               // a failed collective evaluation: the communicator was aborted
 };
+
+// A failed evaluation after the collective may have been entered on other ranks (an enqueue error,
+// a timeout) is fatal for the group: the communicator is aborted (ncclCommAbort, so no peer waits
+// forever on it) and every later call on the handle returns GGP_EDEV.
+static void comm_fail(Comm *c)
+{
+    if (c->failed) return;
+    c->failed = true;
+    if (c->nc) {
+        if (c->api.comm_abort) c->api.comm_abort(c->nc);
+        c->nc = nullptr;
+    }
+}
 
 struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0, n_trees = 0, blk_trees = 1, n_blocks = 0;
@@ -3315,6 +3352,7 @@ static int rccl_load(const char *path, RcclApi &a)
     a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(a.lib, "ncclAllGather"));
     a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(a.lib, "ncclCommDestroy"));
     a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(a.lib, "ncclGetErrorString"));
+    a.comm_abort = reinterpret_cast<decltype(a.comm_abort)>(dlsym(a.lib, "ncclCommAbort"));
     if (!a.get_unique_id || !a.comm_init_rank || !a.all_gather || !a.comm_destroy) {
         g_last_err = std::string(lib) + " lacks the RCCL entry points";
         return GGP_EDEV;
@@ -3324,6 +3362,7 @@ static int rccl_load(const char *path, RcclApi &a)
 
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     RcclApi a;
     int rc = rccl_load(rccl_lib, a);
     if (rc != GGP_OK || !id) return rc;   // id NULL: only check that the library can be used
@@ -3339,6 +3378,7 @@ int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id)
 
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !id || nranks < 1 || rank < 0 || rank >= nranks) return GGP_EINVAL;
     if (f->comm) {
         g_last_err = "ggp_comm_attach: the handle is already attached";
@@ -3397,6 +3437,11 @@ int32_t ggp_comm_nan_rank(const ggp_forest *f)
     return f && f->comm ? f->comm->last_nan_rank : -1;
 }
 
+int32_t ggp_comm_local_nan(const ggp_forest *f)
+{
+    return f && f->comm ? f->comm->local_nan : 0;
+}
+
 int ggp_device_count(int32_t *n)
 {
     int c = 0;
@@ -3407,6 +3452,7 @@ int ggp_device_count(int32_t *n)
 
 void ggp_forest_destroy(ggp_forest *f)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f) return;
     if (Comm *c = f->comm) {
         if (!f->shards.empty()) {
@@ -3433,6 +3479,7 @@ void ggp_forest_destroy(ggp_forest *f)
 
 int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!d || !out) { g_last_err = "null argument"; return GGP_EINVAL; }
     *out = nullptr;
     if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_PAIR) {
@@ -3449,9 +3496,11 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
         g_last_err = "no HIP device";
         return GGP_EDEV;
     }
-    if (d->n_devices < 0) { g_last_err = "n_devices < 0"; return GGP_EINVAL; }
+    // n_devices: > 0 the list (or 0..n-1), 0 device 0 (a zero-filled descriptor), GGP_ALL_DEVICES
+    // every visible device
+    if (d->n_devices < 0 && d->n_devices != GGP_ALL_DEVICES) { g_last_err = "n_devices < 0 and not GGP_ALL_DEVICES"; return GGP_EINVAL; }
     std::vector<int32_t> devlist;
-    const int nd = d->n_devices > 0 ? d->n_devices : n_vis;
+    const int nd = d->n_devices > 0 ? d->n_devices : d->n_devices == 0 ? 1 : n_vis;
     for (int k = 0; k < nd; ++k) {
         const int32_t id = (d->n_devices > 0 && d->devices) ? d->devices[k] : k;
         if (id < 0 || id >= n_vis) { g_last_err = "device ordinal out of range"; return GGP_EINVAL; }
@@ -3555,6 +3604,7 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
 
 int ggp_forest_shards(ggp_forest *f, int32_t *n, int32_t *device, int64_t *rows, int64_t *cells, int32_t cap)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !n) return GGP_EINVAL;
     *n = (int32_t)f->shards.size();
     for (int32_t k = 0; k < *n && k < cap; ++k) {
@@ -3567,6 +3617,7 @@ int ggp_forest_shards(ggp_forest *f, int32_t *n, int32_t *device, int64_t *rows,
 
 int ggp_reset_state(ggp_forest *f)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -3579,6 +3630,7 @@ int ggp_reset_state(ggp_forest *f)
 
 int ggp_get_state(ggp_forest *f, double *out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !out) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -3598,6 +3650,7 @@ int ggp_get_state(ggp_forest *f, double *out)
 
 int ggp_set_state(ggp_forest *f, const double *in)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !in) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -3617,12 +3670,20 @@ int ggp_set_state(ggp_forest *f, const double *in)
 
 int ggp_total_loglik_async(ggp_forest *f, const double *params)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !params) return GGP_EINVAL;
+    if (f->comm && f->comm->failed) {
+        g_last_err = "the handle's communicator was aborted after a failed collective evaluation; re-create the group";
+        return GGP_EDEV;
+    }
     ggp_params P;
     std::memcpy(P.p, params, sizeof P.p);
     for (Shard *s : f->shards) {   // every device enqueued before any is waited for
         const int rc = shard_launch(s, P);
-        if (rc != GGP_OK) return rc;
+        if (rc != GGP_OK) {
+            if (f->comm) comm_fail(f->comm);   // the peers would wait for this rank's all-gather
+            return rc;
+        }
     }
     if (Comm *c = f->comm) {   // behind the evaluation: partial, all-gather, rank-order sum
         Shard *s = f->shards[0];
@@ -3630,60 +3691,105 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
         while (np2 < s->n_lblocks) np2 *= 2;
         hipLaunchKernelGGL(k_rank_partial, dim3(1), dim3(256), 0, s->stream, s->m_sum, s->m_nan, (int)s->n_lblocks, np2,
                            c->d_part);
-        HIPCHK(hipGetLastError());
+        if (hipGetLastError() != hipSuccess) {
+            g_last_err = "k_rank_partial launch failed";
+            comm_fail(c);
+            return GGP_EDEV;
+        }
         const int e = c->api.all_gather(c->d_part, c->d_gath, 2 * sizeof(double), kRcclUint8, c->nc, s->stream);
         if (e != 0) {
             g_last_err = std::string("RCCL all-gather: ") + (c->api.error_string ? c->api.error_string(e) : "error");
+            comm_fail(c);
             return GGP_EDEV;
         }
         ++c->seq;
         hipLaunchKernelGGL(k_rank_sum, dim3(1), dim3(64), 0, s->stream, c->d_gath, c->nranks, c->m_sum, c->m_rank, c->m_seq,
                            c->seq);
-        HIPCHK(hipGetLastError());
+        if (hipGetLastError() != hipSuccess) {
+            g_last_err = "k_rank_sum launch failed";
+            comm_fail(c);
+            return GGP_EDEV;
+        }
     }
     return GGP_OK;
 }
 
 // multi-process result: spin on the sequence number k_rank_sum releases (hipStreamQuery as the
-// way out), then the shard's own block results for this rank's NaN location
+// way out when the stream fails; a wall-clock bound, GGP_COMM_TIMEOUT_S (default 600 s), when a
+// peer never reaches the collective: GGP_ETIMEOUT and the communicator is aborted).  This rank's
+// own first NaN (or stall) is always read from its block results: nan_cell / nan_row hold it
+// (-1 if this rank was clean) and ggp_comm_local_nan reports it, whatever the lowest bad rank is.
 static int comm_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
     Comm *c = f->comm;
     Shard *s = f->shards[0];
-    bool seen = false;
+    if (c->failed) {
+        g_last_err = "the handle's communicator was aborted after a failed collective evaluation; re-create the group";
+        return GGP_EDEV;
+    }
+    static const double limit_s = [] {
+        const char *e = getenv("GGP_COMM_TIMEOUT_S");
+        return e ? atof(e) : 600.0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false, timed_out = false;
     for (uint32_t it = 1;; ++it) {
         if (*c->h_seq == c->seq) { seen = true; break; }
-        if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
+        if ((it & 1023) == 0) {
+            if (hipStreamQuery(s->stream) != hipErrorNotReady) break;
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+                timed_out = true;
+                break;
+            }
+        }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     s->seq_pending = false;
+    if (timed_out) {
+        g_last_err = "multi-process evaluation did not complete within GGP_COMM_TIMEOUT_S (a peer rank never reached the collective); communicator aborted";
+        comm_fail(c);
+        return GGP_ETIMEOUT;
+    }
     if (!seen || s->profile) {
         HIPCHK(hipSetDevice(s->device));
-        HIPCHK(hipStreamSynchronize(s->stream));
-        if (*c->h_seq != c->seq) {
+        const hipError_t e = hipStreamSynchronize(s->stream);
+        if (e != hipSuccess || *c->h_seq != c->seq) {
             g_last_err = "multi-process evaluation did not complete";
+            comm_fail(c);
             return GGP_EDEV;
         }
     }
     const double v = *c->h_sum;
-    c->last_nan_rank = (int32_t)*c->h_rank;
+    const int64_t code_rank = *c->h_rank;
+    const bool stall = code_rank >= 0 && (code_rank >> 32) != 0;
+    c->last_nan_rank = code_rank < 0 ? -1 : (int32_t)(code_rank & 0xffffffff);
     if (ll) *ll = v;
     if (nan_cell) *nan_cell = -1;
     if (nan_row) *nan_row = -1;
+    // this rank's own first bad cell, as ggp_loglik_result finds it
+    long long code = kNoNan;
+    bool own_nan_sum = false;
+    for (int64_t j = 0; j < s->n_lblocks; ++j) {
+        code = std::min<long long>(code, s->h_nan[j]);
+        own_nan_sum = own_nan_sum || std::isnan(s->h_sum[j]);
+    }
+    c->local_nan = (code != kNoNan || own_nan_sum) ? 1 : 0;
+    if (code != kNoNan) {
+        if (nan_cell) *nan_cell = f->dfs_order[code >> 24];
+        if (nan_row) *nan_row = (code & 0xffffff) == kRowStall ? -1 : (code & 0xffffff);
+    }
     if (c->last_nan_rank < 0) return GGP_OK;
-    if (c->last_nan_rank == c->rank) {   // this rank's first NaN, as ggp_loglik_result finds it
-        long long code = kNoNan;
-        for (int64_t j = 0; j < s->n_lblocks; ++j) code = std::min<long long>(code, s->h_nan[j]);
-        if (code != kNoNan) {
-            if (nan_cell) *nan_cell = f->dfs_order[code >> 24];
-            if (nan_row) *nan_row = code & 0xffffff;
-        }
+    if (stall) {
+        g_last_err = "evaluation stalled on rank " + std::to_string(c->last_nan_rank) +
+                     ": a daughter cell's wait for its parent timed out (a scheduling stall, not a NaN)";
+        return GGP_ETIMEOUT;
     }
     return GGP_ENAN;
 }
 
 int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f) return GGP_EINVAL;
     if (f->comm) return comm_result(f, ll, nan_cell, nan_row);
     std::vector<double> blocks((size_t)f->n_blocks, 0.0);
@@ -3717,6 +3823,7 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
 
 int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     int rc = ggp_total_loglik_async(f, params);
     if (rc != GGP_OK) return rc;
     return ggp_loglik_result(f, ll, nan_cell, nan_row);
@@ -3730,6 +3837,7 @@ static constexpr int64_t kBatchBytes = int64_t(4) << 30;
 
 int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *status)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || n_pts < 0 || (n_pts > 0 && (!params || !ll || !status))) {
         g_last_err = "ggp_total_loglik_batch: bad arguments";
         return GGP_EINVAL;
@@ -3824,6 +3932,7 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
 
 int ggp_last_launch_profile(ggp_forest *ff, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!ff || !n || ff->shards.empty()) return GGP_EINVAL;
     Shard *f = ff->shards[0];   // the first shard's launches
     if (!f->profile) {
@@ -3854,6 +3963,7 @@ int ggp_last_launch_profile(ggp_forest *ff, float *ms, int64_t *rows, int32_t *k
 
 int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, int32_t *kernel_used)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f) return GGP_EINVAL;
     int64_t mx = 0, nl = 0;
     for (const Shard *s : f->shards) {
@@ -3869,6 +3979,7 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, 
 
 int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f) return GGP_EINVAL;
     // per device: its shards run one after another; report the slowest device
     float best_a = 0, best_b = 0;
@@ -3899,6 +4010,7 @@ int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine)
 int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_fwd, double *out_bwd,
                 double *out_comb)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !params || n_seg < 1) { g_last_err = "ggp_predict: null params or n_seg < 1"; return GGP_EINVAL; }
     if (f->n_cells == 0) return GGP_OK;
     // ---- workspaces ----
@@ -4005,6 +4117,7 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
 // combined rows [r_lo, r_hi) of the last ggp_predict (input order) -> out[(r - r_lo) * 20]
 int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !out || r_lo < 0 || r_hi > f->n_rows || r_hi < r_lo) {
         g_last_err = "ggp_predict_rows: bad arguments";
         return GGP_EINVAL;
@@ -4032,6 +4145,7 @@ int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out)
 int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
                int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
     if (r_lo < 0) r_lo = 0;
     if (r_hi > f->n_rows) r_hi = f->n_rows;
@@ -4087,6 +4201,7 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
 // ---- test-only device math (tests/test_gpu_device_math.py) --------------------------------
 int ggp_debug_dawson(int32_t device, int32_t variant, const double *x, int64_t n, double *out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!x || !out || n < 0 || variant < 0 || variant > 1) { g_last_err = "ggp_debug_dawson: bad arguments"; return GGP_EINVAL; }
     if (n == 0) return GGP_OK;
     HIPCHK(hipSetDevice(device));
@@ -4107,6 +4222,7 @@ int ggp_debug_dawson(int32_t device, int32_t variant, const double *x, int64_t n
 
 int ggp_debug_tauint(int32_t device, const double *in, int64_t n, double *out)
 {
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!in || !out || n < 0) { g_last_err = "ggp_debug_tauint: bad arguments"; return GGP_EINVAL; }
     for (int64_t i = 0; i < n; ++i)
         if (in[6 * i] < 0 || in[6 * i] > 3 || in[6 * i] != (double)(int)in[6 * i]) {

@@ -428,6 +428,15 @@ GGP_DEV double rcp1(const double d)
 #endif
 }
 
+GGP_DEV int mul24(const int a, const int b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);   // v_mul_i32_i24: full rate (v_mul_lo_u32 is quarter rate)
+#else
+    return a * b;
+#endif
+}
+
 GGP_DEV int cvt_i32(const double x)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -486,7 +495,7 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     const double ax = fabs(z);
     const double y100 = 100.0 * rcp1(1.0 + ax);
     const int k = min(cvt_i32(y100), GGP_DAWSON_NINT - 1);
-    const int row = L.b_isD ? k * kTabRow : kExpRow * kTabRow;
+    const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
     const double *A = lds + L_TAB + row;
     double a[kTabRow];
 #pragma unroll

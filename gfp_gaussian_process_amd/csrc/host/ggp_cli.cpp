@@ -288,7 +288,7 @@ void build_forest(Forest &F, const ggp_dataset *d, int segment, const std::strin
     if (ggp_forest_build(d, segment, noise == "scaled", div == "binomial", &F.host) != GGP_OK)
         throw std::invalid_argument(ggp_host_last_error());
     ggp_host_forest_desc(F.host, &F.desc);
-    F.desc.n_devices = (int32_t)g_devices.size();   // 0: every visible device
+    F.desc.n_devices = g_devices.empty() ? GGP_ALL_DEVICES : (int32_t)g_devices.size();
     F.desc.devices = g_devices.empty() ? nullptr : g_devices.data();
     F.desc.max_shard_rows = g_max_shard_rows;
     F.desc.kernel = GGP_KERNEL_AUTO;

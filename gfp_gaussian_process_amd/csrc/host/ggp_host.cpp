@@ -458,6 +458,16 @@ extern "C" int ggp_dataset_load(const char *path, ggp_dataset **out)
     if (!read_all(f, &nc, 8) || !read_all(f, &nr, 8) || !read_all(f, &fp_auto, 8) || nc < 0 || nr < 0 ||
         nc > ((int64_t)1 << 31) || nr > ((int64_t)1 << 40))
         return bad("bad header");
+    // the counts against the file's size before anything is allocated from them: a truncated or
+    // corrupt header must not ask for tens of GB (offsets 8 (nc+1) + columns 28 nr + ids >= 8)
+    {
+        const long here = std::ftell(f);
+        if (here < 0 || std::fseek(f, 0, SEEK_END) != 0) return bad("cannot size the file");
+        const long end = std::ftell(f);
+        if (end < 0 || std::fseek(f, here, SEEK_SET) != 0) return bad("cannot size the file");
+        const int64_t need = 8 * (nc + 1) + 28 * nr + 8;
+        if ((int64_t)(end - here) < need) return bad("truncated (the header's counts exceed the file)");
+    }
     std::vector<int64_t> ro(nc + 1);
     if (!read_all(f, ro.data(), ro.size() * 8) || ro[0] != 0 || ro[nc] != nr) return bad("bad row offsets");
     for (int64_t c = 0; c < nc; ++c)

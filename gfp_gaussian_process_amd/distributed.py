@@ -6,10 +6,10 @@ row count (ties: critical-path length, then tree order).  Each rank keeps its sh
 device-resident data and carried root state; one objective call = every rank evaluates
 its shard, then ONE collective exchanges one double per rank (all_gather), and the
 partials are summed in rank order so the result is bitwise reproducible run to run.
-With an nccl group the collective runs inside the engine (include/ggp.h ggp_comm_attach:
+By default the collective is torch's all_gather_into_tensor (RCCL for an nccl group); opt-in
+(engine_comm=True / GGP_ENGINE_COMM=1) it runs inside the engine (include/ggp.h ggp_comm_attach:
 partial, RCCL all-gather and rank-order sum enqueued on the engine's stream behind the
-evaluation); otherwise (gloo, or engine_comm=False) through torch's all_gather_into_tensor.
-Both give the same bits.
+evaluation).  Both give the same bits.
 The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
 Scan samples and optimiser steps stay sequential (carried state), only the forest is
 parallel.
@@ -103,10 +103,12 @@ class ShardedObjective:
         self.always_gather = always_gather          # tests: the collective path at world size 1
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         # RCCL inside the engine (include/ggp.h ggp_comm_attach): the all-gather is enqueued on the
-        # engine's stream behind the evaluation, no host round trip in between.  Default on for
-        # nccl groups whose per-rank objective is a HIP Forest (GGP_ENGINE_COMM=0: torch's path)
+        # engine's stream behind the evaluation, no host round trip in between.  Opt-in
+        # (engine_comm=True or GGP_ENGINE_COMM=1) for nccl groups whose per-rank objective is a HIP
+        # Forest: it has run on a 1-rank group only (no multi-GPU box to the builder yet), so the
+        # default is torch's all_gather path until a multi-rank run has passed
         if engine_comm is None:
-            engine_comm = os.environ.get("GGP_ENGINE_COMM", "1") != "0"
+            engine_comm = os.environ.get("GGP_ENGINE_COMM", "0") == "1"
         self.engine = False
         if (engine_comm and backend == "nccl" and (self.world > 1 or always_gather)
                 and isinstance(device_forest, Forest)):

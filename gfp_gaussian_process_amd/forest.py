@@ -357,7 +357,7 @@ class HostForest:
         d.division_binomial = a["division_binomial"]
         d.fp_auto = a["fp_auto"]
         if devices is None:
-            d.n_devices, d.devices = 0, None
+            d.n_devices, d.devices = N.GGP_ALL_DEVICES, None
         else:
             dv = np.ascontiguousarray(devices, np.int32)
             if dv.ndim != 1 or dv.size == 0:
@@ -425,11 +425,15 @@ class Forest:
             raise GGPError(self._lib.ggp_strerror(rc).decode())
 
     def _nan(self, nc: int, nr: int):
-        r = self._lib.ggp_comm_nan_rank(self._h) if getattr(self, "_comm_rank", None) is not None else -1
-        if r >= 0 and r != self._comm_rank:   # another rank's NaN: this rank's state is intact
-            return LikelihoodIsNan(-1, -1, f"rank {r}")
         # after a NaN the carried state is unspecified (include/ggp.h "Errors"): the next
-        # evaluation needs reset_state() or set_state() first
+        # evaluation needs reset_state() or set_state() first.  With the engine's collective, a
+        # rank whose own evaluation was bad is marked even when a lower rank had the first NaN.
+        if getattr(self, "_comm_rank", None) is not None:
+            r = self._lib.ggp_comm_nan_rank(self._h)
+            if self._lib.ggp_comm_local_nan(self._h):
+                self._poisoned = True
+            if r >= 0 and r != self._comm_rank:
+                return LikelihoodIsNan(-1, -1, f"rank {r}")
         self._poisoned = True
         cid = self.host.ids[nc] if (self.host.ids and nc >= 0) else None
         return LikelihoodIsNan(nc, nr, cid)
@@ -455,7 +459,8 @@ class Forest:
 
     def _stalled(self, rc):
         if rc == N.GGP_ETIMEOUT:
-            self._poisoned = True
+            if getattr(self, "_comm_rank", None) is None or self._lib.ggp_comm_local_nan(self._h):
+                self._poisoned = True
             raise EvaluationStalled(self._lib.ggp_strerror(rc).decode())
 
     # -- one process per GPU: the engine's own RCCL collective (include/ggp.h ggp_comm_attach) --

@@ -62,6 +62,8 @@ extern "C" {
 
 typedef struct ggp_forest ggp_forest;
 
+#define GGP_ALL_DEVICES (-1) /* ggp_forest_desc.n_devices: every visible device     */
+
 typedef struct {
     int64_t n_cells;             /* cells in input order (read_data order)           */
     int64_t n_rows;              /* data points (count_data_points)                  */
@@ -80,8 +82,9 @@ typedef struct {
     int32_t noise_scaled;        /* 1 = "scaled" (default), 0 = "const"              */
     int32_t division_binomial;   /* 1 = "binomial" (default), 0 = "gauss"            */
     double fp_auto;              /* CSVconfig::fp_auto                               */
-    int32_t n_devices;           /* shard the forest over these devices; 0 = every
-                                    visible device                                   */
+    int32_t n_devices;           /* shard the forest over these devices; 0 = device 0
+                                    only (a zero-filled descriptor), GGP_ALL_DEVICES
+                                    (-1) = every visible device                      */
     int32_t kernel;              /* GGP_KERNEL_*: scheduling policy (see below)         */
     const int32_t *devices;      /* [n_devices] HIP ordinals or NULL (= 0..n_devices-1);
                                     an ordinal may repeat: logical shards on one device */
@@ -205,8 +208,13 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
  * blocks, and its first-NaN flag), one RCCL all-gather moves 16 B per rank over xGMI, and a
  * one-thread kernel sums the partials in rank order into mapped host memory (the host spins on
  * it): the same bits as distributed.ShardedObjective's all_gather + combine_partials.  A NaN
- * partial on any rank makes the call return GGP_ENAN on every rank; *nan_cell / *nan_row are
- * this rank's first NaN, or -1 when the first NaN rank is another (ggp_comm_nan_rank).
+ * partial on any rank makes the call return GGP_ENAN on every rank (GGP_ETIMEOUT when the first
+ * bad rank's first bad cell stalled); *nan_cell / *nan_row are this rank's own first NaN (-1 when
+ * this rank was clean), ggp_comm_nan_rank the lowest bad rank, ggp_comm_local_nan whether this
+ * rank's own evaluation was bad (its carried state is then unspecified, as after GGP_ENAN).
+ * A wait for the collective is bounded (GGP_COMM_TIMEOUT_S, default 600 s: GGP_ETIMEOUT); after
+ * any failure once the shard was enqueued the communicator is aborted (ncclCommAbort) and every
+ * later call returns GGP_EDEV: a failed collective evaluation is fatal for the group.
  *   rccl_lib: the RCCL library to use (the one torch already loaded, so the process holds one
  *             RCCL; NULL = "librccl.so.1")
  *   id: 128 bytes (ncclUniqueId) made by ggp_comm_unique_id on rank 0 and given to every rank
@@ -218,6 +226,7 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
 int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last call, -1 none */
+int32_t ggp_comm_local_nan(const ggp_forest *f);  /* 1: this rank's own last evaluation was bad */
 
 int ggp_device_count(int32_t *n);
 const char *ggp_strerror(int code);

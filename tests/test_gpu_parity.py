@@ -652,3 +652,75 @@ def test_sharded_objective_collective_path_on_rccl():
     print("collective path ms/call:", out["ms"])
     assert out["engine_mode"] == {"engine": True, "torch": False}
     assert out["same"] and out["nan_ok"]
+
+
+def test_chain_stall_is_a_timeout_not_a_nan(monkeypatch):
+    """A second daughter whose parent does not finish within the chain-wait limit (forced here:
+    GGP_CHAIN_SPIN_MAX=0, the parent root still running) ends the evaluation with GGP_ETIMEOUT
+    (EvaluationStalled), never as LikelihoodIsNan (likelihood.h:71-93 semantics are for real NaN
+    only); the carried state is then unspecified, so the handle refuses the next evaluation until
+    reset_state().  A handle made without the limit evaluates the same forest normally."""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import _native as N
+    from oracle import oracle as O
+    P = CONFIGS[0][2]
+    hf = g.HostForest.synthetic(64, 200)          # path launch: roots of 100 rows, two daughters each
+    monkeypatch.setenv("GGP_CHAIN_SPIN_MAX", "0")
+    f = g.Forest(hf, kernel="wave")
+    monkeypatch.delenv("GGP_CHAIN_SPIN_MAX")
+    with pytest.raises(g.EvaluationStalled) as ei:
+        f.total_likelihood(P)
+    assert not isinstance(ei.value, g.LikelihoodIsNan)
+    assert "stall" in str(ei.value)
+    # the raw C-ABI: GGP_ETIMEOUT, no NaN location
+    import ctypes
+    lib = N.engine()
+    ll, nc, nr = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+    p = np.ascontiguousarray(P, np.float64)
+    rc = lib.ggp_total_loglik(f._h, p.ctypes.data_as(N.c_double_p), ctypes.byref(ll), ctypes.byref(nc), ctypes.byref(nr))
+    assert rc == N.GGP_ETIMEOUT and nr.value == -1
+    with pytest.raises(g.GGPError, match="unspecified"):
+        f.total_likelihood(P)
+    ok = g.Forest(hf, kernel="wave")
+    ref = O.OracleForest(hf.a).total_likelihood(P)[0]
+    assert _rel(ok.total_likelihood(P), ref) < REL
+
+
+_DEVICE_CHILD = r"""
+import json, sys
+sys.path.insert(0, ROOT)
+import torch                                   # torch's HIP runtime first (as in bench.py)
+n = torch.cuda.device_count()
+torch.cuda.set_device(n - 1)
+import gfp_gaussian_process_amd as g
+hf = g.HostForest.synthetic(32, 40)
+seen = []
+for devs in ([0], [0, 0], list(range(n))):
+    f = g.Forest(hf, devices=devs)
+    seen.append(torch.cuda.current_device())
+    f.total_likelihood(PARAMS)
+    seen.append(torch.cuda.current_device())
+    f.predict([PARAMS])
+    f.state()
+    f.reset_state()
+    seen.append(torch.cuda.current_device())
+    f.close()
+    seen.append(torch.cuda.current_device())
+print(json.dumps({"n": n, "seen": seen}))
+"""
+
+
+def test_caller_device_restored_across_calls():
+    """Every C-ABI entry point restores the caller's current HIP device (include/ggp.h): Forests on
+    device 0, on two logical shards of it and on every device, driven from a process whose current
+    device is the last visible one, leave it there after create / evaluate / predict / state /
+    destroy (on a one-GPU box the last device is device 0: every entry point still runs once).
+    In a child process: torch initialises its runtime before the engine, as bench.py does."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    code = f"ROOT={ROOT!r}\nPARAMS={list(CONFIGS[0][2])!r}\n" + _DEVICE_CHILD
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["seen"] and all(d == out["n"] - 1 for d in out["seen"]), out

@@ -261,6 +261,13 @@ def test_binary_dataset_roundtrip(tmp_path, example_paths):
         g.Dataset.load(p2)
     with pytest.raises(g.GGPError, match="GGPD0001"):
         g.Dataset.load(example_paths["params"])
+    # a header whose counts exceed the file (valid offsets, 2^33 rows claimed) is refused before
+    # anything is allocated from it (the columns alone would be 64 GB)
+    import struct
+    nr = 1 << 33
+    open(p2, "wb").write(b"GGPD0001" + struct.pack("<qqd", 1, nr, 0.0) + struct.pack("<qq", 0, nr) + b"\0" * 64)
+    with pytest.raises(g.GGPError, match="exceed"):
+        g.Dataset.load(p2)
 
 
 def test_dataset_csv_writer_roundtrip(tmp_path, example_paths):

@@ -44,7 +44,9 @@ for kind, c in acc.items():
     res[kind] = {"rows": rows, "launches": len(n_disp[kind]), "valu_wave_insts": c["SQ_INSTS_VALU"],
                  "f64_wave_insts": c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] +
                  c["SQ_INSTS_VALU_TRANS_F64"] + c["SQ_INSTS_VALU_FMA_F64"],
-                 "flops_per_update": 64.0 * f64 / rows, "valu_wave_insts_per_update": c["SQ_INSTS_VALU"] / rows}
+                 "flops_per_update": 64.0 * f64 / rows, "valu_wave_insts_per_update": c["SQ_INSTS_VALU"] / rows,
+                 "f64_wave_insts_per_update": (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] +
+                                               c["SQ_INSTS_VALU_TRANS_F64"] + c["SQ_INSTS_VALU_FMA_F64"]) / rows}
 res["issued_flops_per_update"] = res.get("wave", {}).get("flops_per_update")
 res["useful_flops_per_update"] = res.get("lane", {}).get("flops_per_update")
 json.dump(res, open(out_path, "w"), indent=1)
