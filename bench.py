@@ -380,17 +380,19 @@ def main() -> int:
     inproc = None
     if world > 1 and args.inprocess:
         store = dist.distributed_c10d._get_default_store()
+        devs = [None] * world                      # the devices the ranks use (a rehearsal: all 0)
+        dist.all_gather_object(devs, local)
         barrier()
         if rank == 0:
             ha = g.HostForest.synthetic(args.trees * world, args.rows, seed=SEED)
-            fa = g.Forest(ha, devices=list(range(world)), kernel=args.kernel)
+            fa = g.Forest(ha, devices=[int(d) for d in devs], kernel=args.kernel)
             for _ in range(args.warmup):
                 fa.total_likelihood(P_EXAMPLE)
             t1 = time.perf_counter()
             for _ in range(args.steps):
                 fa.total_likelihood(P_EXAMPLE)
             iel = time.perf_counter() - t1
-            inproc = {"devices": world, "trees": args.trees * world, "rows": ha.n_rows, "steps": args.steps,
+            inproc = {"devices": [int(d) for d in devs], "trees": args.trees * world, "rows": ha.n_rows, "steps": args.steps,
                       "ms_per_step": 1e3 * iel / args.steps, "value": ha.n_rows * args.steps / iel,
                       "shards": len(fa.shards()),
                       "note": "one process drives every device (Forest(hf, devices=range(N)), the CLI's -g all): "

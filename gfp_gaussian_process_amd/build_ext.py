@@ -53,7 +53,7 @@ def build(verbose: bool = False, force: bool = False) -> dict:
     eng_deps = [eng_src, os.path.join(CSRC, "ggp_device.h"), os.path.join(CSRC, "dawson_table.inc"),
                 os.path.join(INC, "ggp.h")]
     for extra in ("ggp_prop.h", "ggp_group.h", "ggp_predict.h", "ggp_joints.h", "ggp_outtab.h",
-                  "ggp_out_tables.inc", "ggp_wave.h", "ggp_wave2.h"):
+                  "ggp_out_tables.inc", "ggp_wave.h"):
         p = os.path.join(CSRC, extra)
         if os.path.exists(p):
             eng_deps.append(p)

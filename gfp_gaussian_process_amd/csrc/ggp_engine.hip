@@ -35,7 +35,6 @@
 #include "ggp_prop.h"
 #include "ggp_outtab.h"
 #include "ggp_wave.h"
-#include "ggp_wave2.h"
 #include "ggp_predict.h"
 #include "ggp_joints.h"
 
@@ -83,17 +82,6 @@ GGP_DEV void lds_fill(double *dst, const int lane, const SRC &src)
 GGP_DEV void load_dawson_table(double *s_tab, int lane)
 {
     lds_fill<kDawsonTab>(s_tab, lane, [](const int k) { return ggp_dawson_coef[k]; });
-}
-
-// the wave schedule's copy: rows padded to ggp::wave::kDawsonRow doubles (128-bit reads)
-constexpr int kDawsonTabP = GGP_DAWSON_NINT * ggp::wave::kDawsonRow;
-GGP_DEV void load_dawson_table_padded(double *s_tab, int lane)
-{
-    lds_fill<kDawsonTabP>(s_tab, lane, [](const int k) {
-        const int row = k / ggp::wave::kDawsonRow, j = k % ggp::wave::kDawsonRow;
-        const double c = ggp_dawson_coef[GGP_DAWSON_NCOEF * row + min(j, GGP_DAWSON_NCOEF - 1)];
-        return j < GGP_DAWSON_NCOEF ? c : 0.0;
-    });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -684,22 +672,19 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 
 
 // ------------------------------------------------------------------------------------------
-// WAVE schedule: one 64-lane wave per cell, every stage of a step spread over the lanes
-// (ggp_wave.h): one exponential and one Dawson value per lane (lane 0: the tauint
-// denominators), then one integral per lane, then the outputs as the sparse trilinear form of
-// ggp_outtab.h (59 lanes x 4 terms, summed by a DPP butterfly inside power-of-two lane blocks
-// and broadcast through LDS); the Kalman update runs redundantly in all lanes (the state stays
-// in registers).  A step costs about its instruction count (one per ~4 shader cycles per
-// wave), so every stage is kept to the fewest instructions.
-// Every stage is straight-line code (ggp_wave.h says why).  What depends on the parameters
-// and dt only -- exp(s t) and the 18 exp-derived basis values of the outputs -- is formed
-// when dt changes and kept in LDS.  The determinant and log of the ll term are off the
-// critical path: x and S go to an LDS ring, and every 64 rows (or at the cell's end) 64
-// lanes take the quadratic forms, determinants and logs at once and one lane adds the terms in
-// row order (the reference's summation order; the first NaN row is found there).
-// The outputs are the same polynomial as ggp::outputs summed in another order, four exp(c)
-// are products of exponentials, and the update uses fused multiply-adds, so results agree with
-// the lane/group schedules to ~1e-10 relative on the total, not bitwise (DESIGN.md "Parity").
+// WAVE schedule: one 64-lane wave per cell (ggp_wave.h).  Every stage of a step is one task per
+// lane -- the 46 state-dependent exponentials and 14 Dawson values in one Horner stream, the 45
+// integrals, the outputs' trilinear form over 60 state monomials (a DPP butterfly per output
+// block) -- and the 20-double state is distributed over lanes 0-19 (lane e owns entry e: the
+// innovation runs in every lane, the posterior one entry per lane).  What depends on the
+// parameters and dt only (exp(s t), the 18 exp-derived basis values) is formed when dt changes
+// and kept in LDS.  The determinant and log of the ll term are off the critical path: x and S go
+// to an LDS ring, and every 64 rows (or at the cell's end) 64 lanes take the quadratic forms,
+// determinants and logs at once and one lane adds the terms in row order (the reference's
+// summation order; the first NaN row is found there).  The outputs are the same polynomial as
+// ggp::outputs summed in another order, 22 exponentials are products exp(c + ...) exp(k t), and
+// the update uses fused multiply-adds, so results agree with the lane/group schedules to ~1e-10
+// relative on the total, not bitwise (DESIGN.md "Parity").
 // ------------------------------------------------------------------------------------------
 template <int CTRL>
 GGP_DEV double dpp_f64(const double v)
@@ -711,81 +696,21 @@ GGP_DEV double dpp_f64(const double v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-template <int LANE>
-GGP_DEV double readlane_f64(const double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), LANE);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), LANE);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-
-// ll terms of rows [base, base + n) from the LDS ring (x0, x1, S00, S01, S11 per row) into cl,
-// in row order (ggp_ll_term: q - 0.5 log(det S) - 2 log(2 pi)); false at the first NaN (nan_row set)
-GGP_DEV bool wave_flush_ll(const double (*ring_x)[64], const double (*ring_s)[64], double *ring_t, const int n,
-                           const int64_t base, const double two_log_2pi, const int lane, double &cl, int &nan_row)
-{
-    __syncthreads();
-    if (lane < n) {
-        const double s00 = ring_s[0][lane], s01 = ring_s[1][lane], s11 = ring_s[2][lane];
-        ring_t[lane] = ggp::wave::ll_quad(ring_x[0][lane], ring_x[1][lane], s00, s01, s11) -
-                       0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - two_log_2pi;
-    }
-    __syncthreads();
-    bool ok = true;
-    if (lane == 0) {
-        // the same adds in the same order; the scan for the first NaN row only when the chunk's
-        // sum is NaN (no compare and branch per row on the common path)
-        double acc = cl;
-        for (int k = 0; k < n; ++k) acc += ring_t[k];
-        if (acc != acc) {
-            acc = cl;
-            for (int k = 0; k < n; ++k) {
-                acc += ring_t[k];
-                if (acc != acc) {
-                    nan_row = (int)(base + k);
-                    ok = false;
-                    break;
-                }
-            }
-        }
-        cl = acc;
-    }
-    // every lane returns lane 0's verdict
-    return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
-}
-
 // Level launches: block b runs cell cells[b].  Path launches (one launch for a whole forest
 // whose levels all take the wave schedule): block b runs the path cells[seq[b] .. seq[b+1]),
 // a root or second daughter followed by first daughters down to a leaf; each cell after the
-// first inherits its parent's posterior in registers.  The Dawson table and the lane tasks
-// are set up once per block.  A path's first cell, if a second daughter, waits for its
-// parent's done flag (this evaluation's epoch; relaxed polls, then an agent-scope acquire);
-// a cell with a second daughter publishes its state and then its flag (agent-scope release).
-// Paths are ordered by the depth of their first cell, so a parent's path has a lower block
-// index: blocks are dispatched in index order, a waiting block only waits on a lower one, and
-// the lowest unfinished path never waits -- no deadlock, whatever the occupancy.
-// chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c}.
-constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling: a broken chain ends as NaN, not a hang
+// first inherits its parent's posterior in LDS.  The tables and the lane constants are set up
+// once per block.  A path's first cell, if a second daughter, waits for its parent's done flag
+// (this evaluation's epoch: relaxed agent-scope polls); a cell with a second daughter publishes
+// its state (lanes 0-19, agent-scope stores), waits for the stores (s_waitcnt vmcnt(0)), then
+// its flag.  Paths are ordered by the depth of their first cell, so a parent's path has a lower
+// block index; progress relies on the waiting block and its parent's block being resident
+// together (the path launch holds at most as many blocks as the device keeps resident, sized by
+// the occupancy query), and a wait that exceeds spin_max polls ends as a stall (GGP_ETIMEOUT),
+// never as a hang or a model NaN.  chain[c] = {parent to wait for or -1, 1 if a second daughter
+// waits for c}.
+constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling (GGP_CHAIN_SPIN_MAX)
 constexpr unsigned kChainQuietPerRow = 1100;    // s_memtime units (~0.5 us) of unpolled sleep per parent row
-
-// The state a second daughter takes over crosses XCDs: agent-scope atomic (sc1) stores and
-// loads, coherent without the L2 writeback / invalidate of a release / acquire (a writeback per
-// finishing parent cost more than the launch gap the path launch saves).  The writer waits for
-// its stores to complete before the flag store; the reader loads after seeing the flag.
-GGP_DEV void chain_publish(double *st, const double *m, const double *C, unsigned *flag, const unsigned epoch)
-{
-    unsigned long long *q = reinterpret_cast<unsigned long long *>(st);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        __hip_atomic_store(q + k, (unsigned long long)__double_as_longlong(m[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        __hip_atomic_store(q + 4 + k, (unsigned long long)__double_as_longlong(C[k]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0): the state is at the coherence point
-    __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // In-launch reduction of a path launch (replaces k_reduce_blocks there, with the same sums):
 // the last path of a reduction block to finish forms the block's tree sums (each in DFS order)
@@ -866,323 +791,45 @@ GGP_DEV void chain_reduce(const ChainRed &R, const int64_t seq, const int b, con
     __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-GGP_DEV void chain_take(const double *st, double *m, double *C)
-{
-    const unsigned long long *q = reinterpret_cast<const unsigned long long *>(st);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        m[k] = __longlong_as_double((long long)__hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        C[k] = __longlong_as_double((long long)__hip_atomic_load(q + 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(DevForest F, ggp_params P, const int32_t *__restrict__ cells,
-                                                    int n, double *__restrict__ state,
-                                                    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan,
-                                                    const int2 *__restrict__ chain, unsigned *cell_done,
-                                                    const unsigned epoch, const int32_t *__restrict__ seq,
-                                                    const ChainRed *__restrict__ red, const int64_t call_seq)
-{
-    namespace W = ggp::wave;
-    [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // stamp slot 3: <= 1 wave per SIMD, 2: more (GGP_STAMPS builds only)
-    __shared__ double lds[W::kLds];
-    __shared__ __attribute__((aligned(16))) double s_tab[kDawsonTabP];
-    __shared__ double ring_x[2][64], ring_s[3][64], ring_t[64];
-    __shared__ double row_l[64], row_f[64], row_t[65];   // this 64-row chunk's data (+ next time)
-    const int lane = threadIdx.x;
-    GGP_PSTAMP_DECL;
-    GGP_PSTAMP(0);
-    load_dawson_table_padded(s_tab, lane);
-    GGP_PSTAMP(1);
-    double *Xl = lds + W::L_X, *Dl = lds + W::L_D, *Pl = lds + W::L_P;
-    double *Bv = lds + W::L_BV, *Vl = lds + W::L_V;
-    const double *p = P.p;
-    const ggp::OU ou = W::pin_ou(ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]));
-    const W::LaneTasks T = W::lane_tasks(lane, ou);   // this lane's tasks, registers for the launch
-    const double var_x = W::pin(p[7]), var_g = W::pin(p[8]);
-    const double var_dx = p[9], var_dg = p[10];   // first step of a daughter only: not pinned
-    double kap[ggp::kOutL];
-    ggp::OutTerm tt[ggp::kOutL];
-#pragma unroll
-    for (int q = 0; q < ggp::kOutL; ++q) {
-        tt[q] = ggp::kOutTerm[lane][q];
-        kap[q] = ggp::out_kappa(ou, tt[q].kap);
-    }
-    const int bs = ggp::kOutBlock[lane];
-    GGP_PSTAMP(2);
-    if (lane == 0) {
-        Xl[ggp::X_ONE] = 1.0;
-        Bv[ggp::BV_ONE] = 1.0;
-        Vl[ggp::V_ONE] = 1.0;
-    }
-    // the exp(s t) block in LDS depends on the parameters and dt only: it stays valid from one
-    // cell of this wave to the next.  dt is wave-uniform: compared by its bits in scalar
-    // registers (a NaN pattern no time difference produces: nothing cached yet)
-    unsigned long long dt_cached = 0x7ff4dead0000beefULL;
-    GGP_STAMP_DECL;
-    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
-    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
-    double m[4] = {0, 0, 0, 0}, C[16] = {0};
-    int64_t prev_last = -1;   // the previous cell's last row (its daughter's division interval)
-    for (int i = i_lo; i < i_hi; ++i) {
-        int c = 0;
-        int64_t r1 = 0, r0 = 0;
-        double dt = 0.0, t_cur = 0.0;
-        bool pending = false, divide = false;
-        int2 ch = {-1, 0};
-        bool chain_broken = false;
-        {
-            c = cells[i];
-            ch = chain[c];
-            if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-                // the parent runs in this launch and is not done: it needs >= ~1.3 us per row, so
-                // sleep through half a microsecond per parent row without polling (each poll is a
-                // memory read past the L2), then poll
-                const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-                const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
-                while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
-                unsigned spins = 0;
-                while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-                    __builtin_amdgcn_s_sleep(8);
-                    if (++spins > kChainSpinMax) {
-                        chain_broken = true;
-                        break;
-                    }
-                }
-            }
-            r0 = F.row_off[c];
-            r1 = F.row_off[c + 1];
-            if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in m, C
-                pending = true;
-                dt = F.time[r0] - F.time[prev_last];
-            } else if (ch.x >= 0) {   // a second daughter of a cell in another path
-                chain_take(state + (size_t)20 * ch.x, m, C);
-                pending = true;
-                dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
-            } else {
-                pending = cell_prologue(F, p, state, c, r0, m, C, dt);
-            }
-            divide = pending;
-            t_cur = F.time[r0];
-            prev_last = r1 - 1;
-        }
-        GGP_PSTAMP(3);
-        // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane), so
-        // the step loop issues no global loads and never waits on one
-        auto load_chunk = [&](const int64_t base) {
-            const int64_t rr = base + lane;
-            double a = 0.0, b = 0.0, t = 0.0;
-            if (rr < r1) {
-                a = F.logl[rr];
-                b = F.fp[rr];
-                t = F.time[rr];
-            }
-            row_l[lane] = a;
-            row_f[lane] = b;
-            row_t[lane] = t;
-            if (lane == 0) row_t[64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
-        };
-        load_chunk(r0);
-        __syncthreads();
-        double cl = 0.0;
-        int nan_row = kNanNone;
-        int slot = 0;                                                   // rows in the ll ring = row - chunk base
-        const int nrows = (int)(r1 - r0);
-        int left = nrows;                                               // rows from the current one on
-        bool live = !chain_broken;
-        if (chain_broken) {
-            cl = __longlong_as_double(0x7ff8000000000000LL);
-            nan_row = 0;
-        }
-        // One step (one row).  The first step of the cell is peeled (FIRST): only it can skip the
-        // propagation (a root's first row) or apply the division map (a daughter's), so the steady
-        // loop has neither branch -- nor the register copies the compiler put at their joins.
-        // Every later step propagates: the loop continues only while rows remain.  false = stop
-        // (a NaN term; nan_row set).
-        auto step = [&](auto first) -> bool {
-            constexpr bool FIRST = decltype(first)::value;
-            GGP_STAMP(0);
-            GGP_STAMP_STEP();
-            const double y_l = row_l[slot], y_f = row_f[slot];
-            const double t_next = left > 1 ? row_t[slot + 1] : 0.0;
-            if (!FIRST || pending) {
-                const W::WStep S = W::wstep(m, C, dt, ou.b);   // every lane: the same step scalars, in registers
-                if (lane == 0) {   // stage D's variables and stage C's denominators, one masked region
-                    W::store_v(m, C, dt, ou, Vl);
-                    W::store_pw(S, Pl);
-                }
-                const long long db = __double_as_longlong(dt);
-                const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
-                                                 (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
-                if (dbits != dt_cached) {
-                    // exp(s t) and the exp-derived basis of the outputs (parameters and dt only)
-                    lds[W::xs_dst_of(lane)] = exp(W::sv_of(ou, lane < 6 ? lane : 0) * dt);
-                    __syncthreads();
-                    lds[W::dv_dst_of(lane)] = ggp::derived_generic(W::dv_of(lane), Xl, ou.gl, dt);
-                    __syncthreads();
-                    dt_cached = dbits;
-                }
-                GGP_STAMP(1);
-                {   // stage B: one exponential and one Dawson value per lane
-                    const double xa = W::exp_arg(S, T);
-                    double ev = ggp::exp_ocml(xa);
-                    const double dv = W::dawson_bf(W::dawson_arg(S, T), s_tab);
-                    if (__builtin_amdgcn_ballot_w64(!(fabs(xa) < ggp::kExpFastMax)))   // ocml's exp beyond 2^50 (rare)
-                        ev = fabs(xa) < ggp::kExpFastMax ? ev : exp(xa);
-                    lds[T.x_dst] = ev;
-                    lds[T.d_dst] = dv;
-                    lds[T.prod_dst] = readlane_f64<0>(ev) * lds[T.mult_off];
-                }
-                GGP_STAMP(2);
-                __syncthreads();
-                GGP_STAMP(3);
-                // stage D's state monomials kappa V1 V2 V3 need no stage-C value: their 12 LDS reads
-                // are issued here, beside stage C, and the products formed after it
-                double vv[ggp::kOutL][3];
-#pragma unroll
-                for (int q = 0; q < ggp::kOutL; ++q) {
-                    vv[q][0] = Vl[tt[q].v1];
-                    vv[q][1] = Vl[tt[q].v2];
-                    vv[q][2] = Vl[tt[q].v3];
-                }
-                lds[T.i_dst] = W::tau_bf(S, T, Xl, Dl, Pl);   // stage C: one integral per lane
-                double kv[ggp::kOutL];
-#pragma unroll
-                for (int q = 0; q < ggp::kOutL; ++q) kv[q] = ((kap[q] * vv[q][0]) * vv[q][1]) * vv[q][2];
-                GGP_STAMP(4);
-                __syncthreads();
-                GGP_STAMP(5);
-                double bv[ggp::kOutL];   // stage D: this lane's output terms; the four reads issue together
-#pragma unroll
-                for (int q = 0; q < ggp::kOutL; ++q) bv[q] = Bv[tt[q].basis];
-                asm volatile("" ::"v"(bv[0]), "v"(bv[1]), "v"(bv[2]), "v"(bv[3]));
-                static_assert(ggp::kOutL == 4, "stage D issues kOutL reads together");
-                double acc = kv[0] * bv[0];   // the lane's terms, fused (the table's sums, not bitwise ggp::outputs)
-#pragma unroll
-                for (int q = 1; q < ggp::kOutL; ++q) acc = __builtin_fma(kv[q], bv[q], acc);
-                GGP_STAMP(6);
-                {   // block sums: DPP butterfly (ggp::out_partner)
-                    double w;
-                    w = dpp_f64<0xB1>(acc);  acc = bs > 1 ? acc + w : acc;
-                    w = dpp_f64<0x4E>(acc);  acc = bs > 2 ? acc + w : acc;
-                    w = dpp_f64<0x141>(acc); acc = bs > 4 ? acc + w : acc;
-                    w = dpp_f64<0x140>(acc); acc = bs > 8 ? acc + w : acc;
-                }
-                lds[T.out_dst] = acc;   // block sums to LDS, read back by every lane
-                GGP_STAMP(7);
-                __syncthreads();
-                double o[ggp::kOutN];
-#pragma unroll
-                for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
-#pragma unroll
-                for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j, one rounding
-                    if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
-                ggp::out_store(o, m, C);
-                if (FIRST && divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
-                GGP_STAMP(8);
-            }
-            const double x0 = y_l - m[0];
-            const double x1 = y_f - m[1];
-            const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
-            if (lane == 0) {   // the ll term's inputs into the ring (its q, det and log at the flush)
-                ring_x[0][slot] = x0;
-                ring_x[1][slot] = x1;
-                ring_s[0][slot] = v.S00;
-                ring_s[1][slot] = v.S01;
-                ring_s[2][slot] = v.S11;
-            }
-            ++slot;
-            W::posterior(m, C, x0, x1, v, left == 1);   // lower triangle only on the cell's last row
-            pending = left > 1;
-            if (pending) dt = t_next - t_cur;
-            t_cur = t_next;
-            --left;
-            live = left > 0;
-            GGP_STAMP(9);
-            if (slot == 64 || !live) {
-                const int done = nrows - left;
-                if (!wave_flush_ll(ring_x, ring_s, ring_t, slot, done - slot, F.two_log_2pi, lane, cl, nan_row))
-                    return false;
-                slot = 0;
-                if (live) load_chunk(r0 + done);
-            }
-            GGP_STAMP(10);
-            __syncthreads();   // LDS slots are rewritten by the next step
-            GGP_STAMP(11);
-            return true;
-        };
-        GGP_PSTAMP(4);
-        const bool more = live && step(std::true_type{});
-        GGP_PSTAMP(5);
-        if (more)
-            while (live && step(std::false_type{})) {
-            }
-        GGP_PSTAMP(6);
-        if (lane == 0) {
-            double *st = state + (size_t)20 * c;
-            st_agent(cell_ll + F.dfs_rank[c], cl);          // coherent: a path launch sums them in-launch
-            st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
-            if (ch.y) {
-                chain_publish(st, m, C, cell_done + c, epoch);   // for the second daughter
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) st[k] = m[k];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
-            }
-        }
-        GGP_PSTAMP(7);
-        __syncthreads();   // the LDS rows and ring are the next cell's
-    }
-    GGP_STAMP_FLUSH();
-    GGP_PSTAMP_FLUSH();
-    if (red) chain_reduce(*red, call_seq, blockIdx.x, lane, cell_ll, cell_nan);
-}
-
 // ------------------------------------------------------------------------------------------
-// WAVE schedule with the distributed state (ggp_wave2.h): one 64-lane wave per cell, the
-// 20-double state spread over lanes 0-19 (lane e owns entry e), stage B's exponentials and
-// Dawson values in one Horner stream, products for the 22 exponentials exp(c + ...) that differ
-// from a computed one by a cached exp(k t).  Same launch forms as k_loglik_wave (path launch:
-// seq != nullptr; level launch: one cell per block), same chain hand-offs and in-launch reduction.
-// A second daughter whose parent does not finish within spin_max polls ends as a stall (NaN
-// total, row kRowStall: GGP_ETIMEOUT on the host), never as a model NaN.
+// k_loglik_wave: the wave schedule.  Path launch: seq != nullptr, block b runs the path
+// cells[seq[b] .. seq[b+1]) and the sum is formed in-launch (red); level launch: one cell per
+// block.  A second daughter whose parent does not finish within spin_max polls ends as a stall
+// (NaN total, row kRowStall: GGP_ETIMEOUT on the host).
 // ------------------------------------------------------------------------------------------
 constexpr int kRowStall = 0xffffff;   // a cell never has 2^24 - 1 rows (ggp_forest_create checks)
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave2(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
     const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed *__restrict__ red, const int64_t call_seq,
     const unsigned spin_max)
 {
     namespace W = ggp::wave;
-    namespace W2 = ggp::w2;
     [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // GGP_STAMPS builds only
-    __shared__ __attribute__((aligned(16))) double lds[W2::kLds];
+    __shared__ __attribute__((aligned(16))) double lds[W::kLds];
     const int lane = threadIdx.x;
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
-    lds_fill<W2::kTabRows * W2::kTabRow>(lds + W2::L_TAB, lane, [](const int k) { return W2::tab_entry(k); });
+    lds_fill<W::kTabRows * W::kTabRow>(lds + W::L_TAB, lane, [](const int k) { return W::tab_entry(k); });
     GGP_PSTAMP(1);
     const double *p = P.p;
-    const W2::LaneC LC = W2::kLaneTab.l[lane];   // this lane's row of the compile-time table
-    W2::Lane L;
+    const W::LaneC LC = W::kLaneTab.l[lane];   // this lane's row of the compile-time table
+    W::Lane L;
     {
         const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
-        lds[W2::L_MONO + lane] = W2::lane_kappa(lane, ou);   // the 33 kappas, one per lane (MONO is free here)
+        lds[W::L_MONO + lane] = W::lane_kappa(lane, ou);   // the 33 kappas, one per lane (MONO is free here)
         __syncthreads();
-        L = W2::lane_from(lane, LC, ou, lds + W2::L_MONO);
+        L = W::lane_from(lane, LC, ou, lds + W::L_MONO);
         __syncthreads();
     }
     const double var_x = p[7], var_g = p[8], var_dx = p[9], var_dg = p[10], b = p[6];
     if (lane == 0) {
-        lds[W2::L_X + ggp::X_ONE] = 1.0;
-        lds[W2::L_BV + ggp::BV_ONE] = 1.0;
-        lds[W2::L_V + ggp::V_ONE] = 1.0;
-        lds[W2::L_ONE1] = 1.0;
-        lds[W2::L_ZERO] = 0.0;
+        lds[W::L_X + ggp::X_ONE] = 1.0;
+        lds[W::L_BV + ggp::BV_ONE] = 1.0;
+        lds[W::L_V + ggp::V_ONE] = 1.0;
+        lds[W::L_ONE1] = 1.0;
+        lds[W::L_ZERO] = 0.0;
     }
     GGP_PSTAMP(2);
     // exp(s t) and the exp-derived basis depend on the parameters and dt only; dt compared by its
@@ -1210,32 +857,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
                                          (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
         if (dbits != dt_cached) {   // lane constants and kernel arguments only: no OU values live in the loop
-            if (lane < 7) lds[lane < 6 ? W2::L_X + ggp::XS_bt + lane : W2::L_XPGQ] = exp(L.c_sv * dt);
+            if (lane < 7) lds[lane < 6 ? W::L_X + ggp::XS_bt + lane : W::L_XPGQ] = exp(L.c_sv * dt);
             __syncthreads();
             if (lane < ggp::kNDerived)
-                lds[W2::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W2::L_X, p[1], dt);
-            if (lane == 0) lds[W2::L_V + ggp::V_T] = dt;
+                lds[W::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W::L_X, p[1], dt);
+            if (lane == 0) lds[W::L_V + ggp::V_T] = dt;
             __syncthreads();
             dt_cached = dbits;
         }
-        const double *po = lds + W2::L_POST;
-        const W::WStep S = W2::wstep2(po[0], po[2], po[4], po[6], po[14], dt, b);
-        lds[L.mo_dst] = W2::mono(L, lds);   // stage D's monomials of this state
+        const double *po = lds + W::L_POST;
+        const W::WStep S = W::wstep2(po[0], po[2], po[4], po[6], po[14], dt, b);
+        lds[L.mo_dst] = W::mono(L, lds);   // stage D's monomials of this state
         GGP_STAMP(1);
         {   // stage B: one exponential or Dawson value per lane
-            const W2::BOut o = W2::stageB(S, L, lds);
+            const W::BOut o = W::stageB(S, L, lds);
             double v = o.v;
-            if (o.rare) v = W2::stageB_rare(L.b_isD, o.arg, o.z, o.v);   // skipped (execz) when no lane needs it
+            if (o.rare) v = W::stageB_rare(L.b_isD, o.arg, o.z, o.v);   // skipped (execz) when no lane needs it
             lds[L.b_dst] = v;
         }
         GGP_STAMP(2);
         __syncthreads();
         GGP_STAMP(3);
-        lds[L.i_dst] = W2::stageC(S, L, lds);   // stage C: one integral per lane
+        lds[L.i_dst] = W::stageC(S, L, lds);   // stage C: one integral per lane
         GGP_STAMP(4);
         __syncthreads();
         GGP_STAMP(5);
-        double acc = W2::stageD(L, lds);   // stage D: the lane's output terms
+        double acc = W::stageD(L, lds);   // stage D: the lane's output terms
         GGP_STAMP(6);
         {   // block sums: DPP butterfly (ggp::out_partner)
             const int bs = L.d_bs;
@@ -1302,10 +949,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 bb = F.fp[rr];
                 t = F.time[rr];
             }
-            lds[W2::L_ROWL + lane] = a;
-            lds[W2::L_ROWF + lane] = bb;
-            lds[W2::L_ROWT + lane] = t;
-            if (lane == 0) lds[W2::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
+            lds[W::L_ROWL + lane] = a;
+            lds[W::L_ROWF + lane] = bb;
+            lds[W::L_ROWT + lane] = t;
+            if (lane == 0) lds[W::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
         };
         load_chunk(r0);
         __syncthreads();
@@ -1330,8 +977,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 const int64_t base = done - slot;
                 __syncthreads();
                 if (lane < slot) {
-                    const double s00 = lds[W2::L_RS0 + lane], s01 = lds[W2::L_RS1 + lane], s11 = lds[W2::L_RS2 + lane];
-                    lds[W2::L_RT + lane] = W::ll_quad(lds[W2::L_RX0 + lane], lds[W2::L_RX1 + lane], s00, s01, s11) -
+                    const double s00 = lds[W::L_RS0 + lane], s01 = lds[W::L_RS1 + lane], s11 = lds[W::L_RS2 + lane];
+                    lds[W::L_RT + lane] = W::ll_quad(lds[W::L_RX0 + lane], lds[W::L_RX1 + lane], s00, s01, s11) -
                                            0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - F.two_log_2pi;
                 }
                 __syncthreads();
@@ -1342,14 +989,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     double acc = cl;
                     if (slot == 64) {
 #pragma unroll
-                        for (int k = 0; k < 64; ++k) acc += lds[W2::L_RT + k];
+                        for (int k = 0; k < 64; ++k) acc += lds[W::L_RT + k];
                     } else {
-                        for (int k = 0; k < slot; ++k) acc += lds[W2::L_RT + k];
+                        for (int k = 0; k < slot; ++k) acc += lds[W::L_RT + k];
                     }
                     if (acc != acc) {
                         acc = cl;
                         for (int k = 0; k < slot; ++k) {
-                            acc += lds[W2::L_RT + k];
+                            acc += lds[W::L_RT + k];
                             if (acc != acc) {
                                 nan_row = (int)(base + k);
                                 ok = false;
@@ -1369,14 +1016,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         };
         GGP_PSTAMP(4);
         if (live) {   // the cell's first step: uniform registers (no propagation / division map)
-            const double y_l = lds[W2::L_ROWL], y_f = lds[W2::L_ROWF];
-            const double t_next = left > 1 ? lds[W2::L_ROWT + 1] : 0.0;
+            const double y_l = lds[W::L_ROWL], y_f = lds[W::L_ROWF];
+            const double t_next = left > 1 ? lds[W::L_ROWT + 1] : 0.0;
             double m[4], C[16];
             if (pending) {
                 propagate(dt);
                 double o[ggp::kOutN];
 #pragma unroll
-                for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W2::L_OUT + k];
+                for (int k = 0; k < ggp::kOutN; ++k) o[k] = lds[W::L_OUT + k];
 #pragma unroll
                 for (int k = 0; k < ggp::kOutN; ++k)   // out_finish: the covariances' sum - nm_i nm_j
                     if (ggp::kOutNm[k][0] >= 0) o[k] = __builtin_fma(-o[ggp::kOutNm[k][0]], o[ggp::kOutNm[k][1]], o[k]);
@@ -1384,18 +1031,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 if (divide) ggp::division_map(m, C, var_dx, var_dg, F.binomial, F.log2);
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) m[k] = lds[W2::L_POST + k];
+                for (int k = 0; k < 4; ++k) m[k] = lds[W::L_POST + k];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) C[k] = lds[W2::L_POST + 4 + k];
+                for (int k = 0; k < 16; ++k) C[k] = lds[W::L_POST + 4 + k];
             }
             const double x0 = y_l - m[0], x1 = y_f - m[1];
             const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
             if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
-                lds[W2::L_RX0 + slot] = x0;
-                lds[W2::L_RX1 + slot] = x1;
-                lds[W2::L_RS0 + slot] = v.S00;
-                lds[W2::L_RS1 + slot] = v.S01;
-                lds[W2::L_RS2 + slot] = v.S11;
+                lds[W::L_RX0 + slot] = x0;
+                lds[W::L_RX1 + slot] = x1;
+                lds[W::L_RS0 + slot] = v.S00;
+                lds[W::L_RS1 + slot] = v.S01;
+                lds[W::L_RS2 + slot] = v.S11;
             }
             W::posterior(m, C, x0, x1, v, true);
             scatter(m, C);
@@ -1407,30 +1054,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         GGP_PSTAMP(5);
         while (live) {   // steady steps: the state distributed over lanes 0-19
             GGP_STAMP_STEP();
-            const double t_next = left > 1 ? lds[W2::L_ROWT + slot + 1] : 0.0;
+            const double t_next = left > 1 ? lds[W::L_ROWT + slot + 1] : 0.0;
             propagate(dt);
             {
                 // every lane forms the innovation from the raw outputs (the values lanes 1, 4, 5, 9,
                 // 20, 24 finish: fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11), its loads issued
                 // with the finish's before any store
-                const double *o = lds + W2::L_OUT;
+                const double *o = lds + W::L_OUT;
                 const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
-                const double yl = lds[W2::L_ROWL + slot], yf = lds[W2::L_ROWF + slot];
-                const double fv = W2::finish(L, lds, slot);   // the prior's entries, -x0, -x1
+                const double yl = lds[W::L_ROWL + slot], yf = lds[W::L_ROWF + slot];
+                const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
                 lds[L.f_dst] = fv;
                 const double nx0 = o0 - yl, nx1 = o1 - yf;
-                const W2::UInnov v = W2::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, var_g,
+                const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, var_g,
                                                 F.scaled, F.fp_auto);
                 if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
-                    lds[W2::L_RX0 + slot] = nx0;
-                    lds[W2::L_RX1 + slot] = nx1;
-                    lds[W2::L_RS0 + slot] = v.S00;
-                    lds[W2::L_RS1 + slot] = v.S01;
-                    lds[W2::L_RS2 + slot] = v.S11;
+                    lds[W::L_RX0 + slot] = nx0;
+                    lds[W::L_RX1 + slot] = nx1;
+                    lds[W::L_RS0 + slot] = v.S00;
+                    lds[W::L_RS1 + slot] = v.S01;
+                    lds[W::L_RS2 + slot] = v.S11;
                 }
                 GGP_STAMP(8);
                 __syncthreads();
-                const double up = W2::upost(L, lds, v);
+                const double up = W::upost(L, lds, v);
                 lds[L.u_post] = up;
                 lds[L.u_v] = up - L.u_vshift;
             }
@@ -1448,7 +1095,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             st_agent_i(cell_nan + F.dfs_rank[c], nan_row);
         }
         if (lane < 20) {
-            const double v = lds[W2::L_POST + lane];
+            const double v = lds[W::L_POST + lane];
             if (ch.y)
                 st_agent(state + (size_t)20 * c + lane, v);
             else
@@ -2243,15 +1890,30 @@ __global__ void k_rank_sum(const double *__restrict__ g, int nranks, double *out
 __global__ __launch_bounds__(64) void k_debug_dawson(const double *__restrict__ x, int64_t n, int variant,
                                                      double *__restrict__ out)
 {
+    namespace W = ggp::wave;
     __shared__ double s_tab[kDawsonTab];
-    __shared__ __attribute__((aligned(16))) double s_tabp[kDawsonTabP];
+    __shared__ __attribute__((aligned(16))) double s_w[W::kTabRows * W::kTabRow];
     load_dawson_table(s_tab, threadIdx.x);
-    load_dawson_table_padded(s_tabp, threadIdx.x);
+    lds_fill<W::kTabRows * W::kTabRow>(s_w, threadIdx.x, [](const int k) { return W::tab_entry(k); });
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     const double v = i < n ? x[i] : 0.0;
-    // every lane of the wave takes part (the wave form's ballots are wave-wide)
-    const double r = variant == 0 ? ggp_dawson_tab(v, s_tab) : ggp::wave::dawson_bf(v, s_tabp);
+    double r;
+    if (variant == 0) {
+        r = ggp_dawson_tab(v, s_tab);
+    } else {
+        // the wave schedule's stage B on a Dawson lane (ggp_wave.h stageB): z = rdiv(B + 2a 0, 1, 1)
+        // = B = fma(0, 1, v) + 0 = v exactly, then the lane's reduction, table row, Horner, sign
+        // and, where needed, the rare branches -- the same instructions the kernel runs
+        W::WStep S{};
+        S.t = 0.0; S.a = 1.0; S.two_a = 2.0; S.four_a = 4.0; S.four_aa = 4.0; S.two_sa = 1.0; S.m2sa = -1.0;
+        S.r_two_sa = 1.0; S.r_four_a = 0.25; S.bbl = v; S.Cxl = 0.0; S.bx = 0.0; S.Cxx = 0.0;
+        W::Lane L{};
+        L.b_tau = 0.0; L.b_km = 1.0; L.b_gqks = 0.0; L.b_m1 = 1.0; L.b_m2 = 0.5; L.b_kc = 0.0;
+        L.b_mult = GGP_SPI2; L.b_isE = 0; L.b_isA = 0; L.b_isD = 1; L.b_exmask = 0;
+        const W::BOut o = W::stageB(S, L, s_w);
+        r = o.rare ? W::stageB_rare(true, o.arg, o.z, o.v) : o.v;
+    }
     if (i < n) out[i] = r;
 }
 
@@ -2415,7 +2077,6 @@ struct Shard {
     unsigned *d_cell_done = nullptr;
     unsigned epoch = 0;
     int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
-    int wave_v1 = 0;                   // GGP_WAVE_V1=1: the r20 wave kernel (k_loglik_wave), A/B only
     unsigned spin_max = 1u << 24;      // GGP_CHAIN_SPIN_MAX: polls of a waiting second daughter (~20 s)
     int32_t *d_path_cells = nullptr, *d_path_seq = nullptr;   // path launch: cells, [n_paths + 1] starts
     int64_t n_paths = 0;               // 0: level launches
@@ -2573,14 +2234,9 @@ int launch_levels(Shard *f, const ggp_params &P)
     };
     if (f->n_paths > 0) {   // every level on the wave schedule: one launch, one block per path
         HIPCHK(prof_begin());
-        if (f->wave_v1)
-            hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
-                               f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
-                               f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq);
-        else
-            hipLaunchKernelGGL(k_loglik_wave2, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
-                               f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
-                               f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max);
+        hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
+                           f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
+                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max);
         HIPCHK(hipGetLastError());
         f->kernel_used = GGP_KERNEL_WAVE;
         f->last_code = GGP_KERNEL_WAVE << 8 | 64;
@@ -2595,14 +2251,9 @@ int launch_levels(Shard *f, const ggp_params &P)
         const int64_t n_simd = (int64_t)f->n_cu * 4;
         const int kind = f->level_kind[L];
         if (kind == GGP_KERNEL_WAVE) {
-            if (f->wave_v1)
-                hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                                   f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
-                                   (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0);
-            else
-                hipLaunchKernelGGL(k_loglik_wave2, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
-                                   f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
-                                   (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max);
+            hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+                               f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
+                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
         } else if (kind == GGP_KERNEL_PAIR) {
@@ -2876,7 +2527,6 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     f->group_max_cells = (int64_t)f->n_cu * 4 * 8;   // 8 cells per wave, one wave per SIMD
     f->pair_max_cells = (int64_t)f->n_cu * 64 * 2;   // r13 scan: two rounds of 64-cell pair workgroups
     if (const char *e = getenv("GGP_WAVE_MAX_CELLS")) f->wave_max_cells = atoll(e);
-    if (const char *e = getenv("GGP_WAVE_V1")) f->wave_v1 = atoi(e) != 0;
     if (const char *e = getenv("GGP_CHAIN_SPIN_MAX")) f->spin_max = (unsigned)strtoul(e, nullptr, 10);
     if (const char *e = getenv("GGP_SPIN")) f->spin = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_CPW")) f->tune_lane_cpw = std::max(0, std::min(64, atoi(e)));
@@ -3022,9 +2672,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             all_wave = all_wave && f->level_kind[L] == GGP_KERNEL_WAVE;
         }
         int per_cu = 0;
-        const hipError_t oe = f->wave_v1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0)
-                                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave2, 64, 0);
-        if (oe == hipSuccess && per_cu > 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0) == hipSuccess && per_cu > 0)
             f->wave_resident = per_cu * f->n_cu;
         if (const char *e = getenv("GGP_WAVE_PATHS_MAX")) f->wave_resident = atoi(e);
         std::vector<int2> ch(nc, int2{-1, 0});

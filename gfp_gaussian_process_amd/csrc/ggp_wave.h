@@ -1,26 +1,35 @@
-// ggp_wave.h -- per-lane task bodies of the WAVE schedule (k_loglik_wave, ggp_engine.hip):
-// one 64-lane wave per cell; in every stage of a step each lane runs ONE task:
+// ggp_wave.h -- task tables and per-lane bodies of the WAVE schedule (k_loglik_wave,
+// ggp_engine.hip): one 64-lane wave per cell, every stage of a step one task per lane.
 //
-//   stage B   lane l: exponential kXW[l] (64 state-dependent exponentials), Dawson value l
-//             (l < 14); lane 0 stores the tauint denominators and their reciprocals; then
-//             lanes 0..3 form exp(c_B), exp(c_J), exp(c_G), exp(c_I) as exp(c_A) times a
-//             cached exponential
-//   stage C   lane l: integral l (l < 45)
-//   per dt    exp(s t) (6) and the 18 exp-derived basis values of the outputs depend on the
-//             parameters and dt only: formed when dt changes, kept in LDS
+// A step (one row, likelihood.h:53-102 with mean_cov_model.h:211-274 in between) is five
+// stages separated by LDS hand-offs inside the wave:
 //
-// Why separate bodies: the task kind differs between the lanes of one wave, and the
-// compiler turns a per-kind ternary into divergent branches, sinking each candidate's
-// arithmetic into its own branch -- the branches then issue one after another and their
-// latency chains cannot overlap (measured: ~2.8k cycles for stage B).  Here
-// every candidate is computed unconditionally and pinned (an empty asm keeps it at that
-// point in the instruction stream) and a select picks the lane's value: one straight-line
-// stream whose chains interleave.  Stores to a slot the lane does not own go to a per-lane
-// dummy slot instead of being predicated (a predicated store would bring the branch back).
+//   B   lanes 0-45: one of the 46 exponentials that depend on the state (the other 28 of the
+//       step's 74 are exp(s t) cached per dt, or products exp(c) * exp(k t) of a computed one
+//       and a cached one: argument O(1), no cancellation, <= 2 ulp); lanes 46-59: one of the
+//       14 Dawson values.  Both kinds run ONE instruction stream: a reduction (exp: rint,
+//       two fma; Dawson: y = 100 / (1 + |x|), interval, Chebyshev variable), then one 11-step
+//       Horner over a 12-coefficient LDS row (the exp row holds ocml's constants, a Dawson row
+//       its interval's polynomial with three leading zeros: bitwise the same Horner), then
+//       ldexp / sign.  The rare branches (exp beyond 2^50, Dawson Taylor / continued fraction)
+//       only when a lane needs them (one ballot).
+//   C   lanes 0-44: one of the 45 tauint integrals; the four kinds (k = 0..3) in one stream, the
+//       per-kind operands formed by fused multiply-adds with 0/1 lane constants (no selects);
+//       the product exponentials multiplied in as they are read.
+//   D   the outputs' sparse trilinear form (ggp_outtab.h): 4 terms per lane over 60 state
+//       monomials formed once per step (one per lane), a DPP butterfly per output block.
+//   F   finish: lane e forms state entry e of the propagated prior (the covariances' sum -
+//       nm_i nm_j), and lanes 20 and 24 -x0 = m0 - y_l, -x1 = m1 - y_f.
+//   U   update (ggp_innovation + ggp_posterior): the 2x2 innovation in every lane (uniform),
+//       then lane e forms posterior entry e (4 means, 16 covariances) from five LDS reads:
+//       the 20-double state is DISTRIBUTED over the lanes, never held whole in registers.
 //
-// The expressions are those of ggp_prop.h (bitwise the same value for every exponential,
-// Dawson value, power and integral, given the same operands), except the four exp(c)
-// products, which differ from exp(c) by ~1 ulp (DESIGN.md "Parity").
+// The first step of a cell (no propagation for a root's first row, the division map for a
+// daughter's) runs the update uniformly in every lane (ggp_wave.h innovation / posterior,
+// the same expressions) and scatters the state to the lanes.
+//
+// Everything here compiles for the host too (GGP_HOST_SIM: tools/hostsim.cpp emulates the
+// 64 lanes stage by stage to measure the numerics against the oracle).
 #pragma once
 #include "ggp_outtab.h"
 #include "ggp_prop.h"
@@ -35,54 +44,11 @@ GGP_DEV double pin(double x)
     return x;
 }
 
-// the parameter-only constants in VGPRs: kept uniform they occupy ~40 SGPRs for the whole
-// loop and push the kernel into SGPR spills (v_writelane / v_readlane traffic every step)
-GGP_DEV OU pin_ou(OU P)
-{
-    P.ml = pin(P.ml); P.gl = pin(P.gl); P.sl2 = pin(P.sl2); P.mq = pin(P.mq); P.gq = pin(P.gq);
-    P.sq2 = pin(P.sq2); P.b = pin(P.b); P.r_gl = pin(P.r_gl); P.r_gq = pin(P.r_gq); P.gq2 = pin(P.gq2);
-    P.gqq2 = pin(P.gqq2); P.r_gq2 = pin(P.r_gq2); P.r_gqq2 = pin(P.r_gqq2); P.gl2 = pin(P.gl2);
-    P.r_gl2 = pin(P.r_gl2); P.k_xl = pin(P.k_xl); P.k_xx = pin(P.k_xx); P.k_ll = pin(P.k_ll);
-    P.k_qq = pin(P.k_qq);
-    return P;
-}
-
-// ---- the per-step exponential list ----------------------------------------------------
-constexpr bool x_cached(const int j)
-{
-    return j == XC_B || j == XC_J || j == XC_G || j == XC_I || (j >= XS_bt && j <= XS_gq);
-}
-struct XWList {
-    unsigned char j[64];
-    int n;
-};
-constexpr XWList make_xw()
-{
-    XWList L{};
-    for (int j = 0; j < NXT; ++j)
-        if (!x_cached(j)) L.j[L.n++] = (unsigned char)j;
-    return L;
-}
-constexpr XWList kXW = make_xw();
-static_assert(kXW.n == 64, "one state-dependent exponential per lane");
-static_assert(kXW.j[0] == XC_A, "lane 0 holds exp(c_A) for the products");
-
 // the B values as ((b + bl) + Cxl km) + gq ks (step_init's B0..B5, same rounding)
 constexpr double kKm[6] = {1., 1., 2., 2., 1., 2.};
 constexpr double kKs[6] = {0., -1., 0., -1., 1., 1.};
 
-// ---- LDS layout (doubles) --------------------------------------------------------------
-enum {
-    L_X = 0,                  // exponentials (NX, incl. X_ONE = 1)
-    L_D = L_X + NX,           // Dawson values
-    L_P = L_D + ND,           // tauint denominators 2 sqrt a, 4 a^1.5, 8 a^2.5, 16 a^3.5, then reciprocals
-    L_BV = L_P + 8,           // outputs basis: 1, the 45 integrals, 18 exp-derived values
-    L_V = L_BV + BV_N,        // outputs variables: 1, state, t
-    L_OUT = L_V + V_N,        // the step's 14 outputs (block sums, written by the lead lanes)
-    L_DUMMY = L_OUT + kOutN,  // one slot per lane for stores of lanes without a task
-    kLds = L_DUMMY + 64
-};
-
+// ---- the step scalars every lane holds, and the measurement step -------------------------------
 // ---- the step scalars every lane holds (wave-uniform values, formed from the state) ------
 // Only what the lanes' tasks read: a = Cll/2 and its roots and reciprocals, b + bl, Cxl, and
 // the two bases of the c values.  sqrt(a) is ocml's own iteration (bitwise its value for
@@ -127,24 +93,6 @@ GGP_DEV WStep wstep(const double *m, const double *C, const double t, const doub
     return S;
 }
 
-// ---- one lane's tasks (registers for the whole launch) ---------------------------------
-// Operands are formed from lane constants instead of select chains:
-//   B  = fma(Cxl, km, b + bl) + gq ks   (km in {1, 2} makes the fma exact: step_init's B bitwise)
-//   ti = t * tau                        (tau in {0, 1, 2}: 0, t, 2t exactly)
-//   c  = fma(kc, t, fma(Cxx, m2, bx m1)) (m1, m2 = 1, 1/2 or 2, 2: the base bx + Cxx/2 or
-//        2 (bx + Cxx) exactly; kc t folds step_init's -b t - gl t ... into one rounding)
-struct LaneTasks {
-    int x_dst, x_isE, x_isA;
-    double x_tau, x_km, x_gqks, x_m1, x_m2, x_kc;
-    int d_dst;
-    double d_tau, d_km, d_gqks;
-    int prod_dst, mult_off;
-    ITask it;
-    double i_tau0, i_tau1, i_km, i_gqks, i_s1;
-    int i_dst;
-    int out_dst;
-};
-
 // kc of c value ic (step_init's c0..c9 as base + kc t)
 GGP_DEV double c_slope(const int ic, const OU &P)
 {
@@ -163,187 +111,10 @@ GGP_DEV double c_slope(const int ic, const OU &P)
     }
 }
 
-GGP_DEV LaneTasks lane_tasks(const int lane, const OU &P)
-{
-    LaneTasks L;
-    const int xj = kXW.j[lane];
-    const XTask xt = kXT[xj];
-    L.x_dst = L_X + xj;
-    L.x_isE = xt.kind == KX_E;
-    L.x_isA = xt.kind == KX_A;
-    L.x_tau = (double)xt.it;
-    const int xb = xt.iB < 6 ? xt.iB : 0;
-    L.x_km = kKm[xb];
-    L.x_gqks = P.gq * kKs[xb];
-    const bool half = xt.ic == cA || xt.ic == cB || xt.ic == cJ || xt.ic == cG || xt.ic == cI;
-    L.x_m1 = half ? 1.0 : 2.0;
-    L.x_m2 = half ? 0.5 : 2.0;
-    L.x_kc = c_slope(xt.ic, P);
-    const DTask dk = kDT[lane < ND ? lane : 0];
-    L.d_dst = lane < ND ? L_D + lane : L_DUMMY + lane;
-    L.d_tau = (double)dk.it;
-    L.d_km = kKm[dk.iB];
-    L.d_gqks = P.gq * kKs[dk.iB];
-    // exp(c_B) = exp(c_A) exp(-gl t), exp(c_J) = exp(c_I) = exp(c_A) exp(-gq t),
-    // exp(c_G) = exp(c_A) / exp(b t)   (c_* of step_init)
-    const int prod_slot = lane == 0 ? XC_B : lane == 1 ? XC_J : lane == 2 ? XC_G : XC_I;
-    const int mult = lane == 0 ? L_X + XS_gl : lane == 2 ? L_BV + BV_R_EBT : L_X + XS_gq;
-    L.prod_dst = lane < 4 ? L_X + prod_slot : L_DUMMY + lane;
-    L.mult_off = lane < 4 ? mult : L_X + X_ONE;
-    L.it = kIT[lane < NI ? lane : 0];
-    L.i_s1 = L.it.k == 2 ? 1.0 : -1.0;
-    L.i_tau0 = (double)L.it.it0;
-    L.i_tau1 = (double)L.it.it1;
-    L.i_km = kKm[L.it.iB];
-    L.i_gqks = P.gq * kKs[L.it.iB];
-    L.i_dst = lane < NI ? L_BV + BV_I + lane : L_DUMMY + lane;
-    // the lead lane of output k's block stores the block sum
-    int out = L_DUMMY + lane;
-#pragma unroll
-    for (int k = 0; k < kOutN; ++k) out = kOutLead[k] == lane ? L_OUT + k : out;
-    L.out_dst = out;
-    return L;
-}
-
-// The per-dt block (exp(s t) and the exp-derived basis of the outputs, formed when dt changes):
-// its lane tasks are formed there from the lane number, not kept in registers for the launch
-GGP_DEV int xs_dst_of(const int lane) { return lane < 6 ? L_X + XS_bt + lane : L_DUMMY + lane; }
-GGP_DEV int dv_dst_of(const int lane) { return lane < kNDerived ? L_BV + BV_R_EBT + lane : L_DUMMY + lane; }
-GGP_DEV DTaskB dv_of(const int lane) { return kDerived[lane < kNDerived ? lane : 0]; }
-
 // the exponents s of exp(s t) (pickSV, ggp_prop.h)
 GGP_DEV double sv_of(const OU &P, const int s)
 {
     return s == 0 ? P.b : s == 1 ? P.b + P.gl : s == 2 ? 2 * P.b : s == 3 ? P.b + P.gq : s == 4 ? -P.gl : -P.gq;
-}
-
-GGP_DEV double bval(const WStep &S, const double km, const double gqks)
-{
-    return __builtin_fma(S.Cxl, km, S.bbl) + gqks;
-}
-
-// the argument of exponential task x (exp_body, ggp_prop.h): exp(c) is the Z form at ti = 0
-// (a 0 + B 0 + c == c)
-GGP_DEV double exp_arg(const WStep &S, const LaneTasks &T)
-{
-    const double ti = S.t * T.x_tau;
-    const double B = pin(bval(S, T.x_km, T.x_gqks));
-    const double c = pin(__builtin_fma(T.x_kc, S.t, __builtin_fma(S.Cxx, T.x_m2, S.bx * T.x_m1)));
-    const double n = pin(rdiv(-(B * B), S.four_a, S.r_four_a));
-    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
-    const double argA = pin(ti * (B + S.a * ti));
-    const double argE = pin(n + c + z * z);
-    const double argZ = pin(S.a * (ti * ti) + B * ti + c);
-    return T.x_isE ? argE : T.x_isA ? argA : argZ;
-}
-
-// the argument of Dawson task d (zval, ggp_prop.h; ti = 0: B + 0 == B)
-GGP_DEV double dawson_arg(const WStep &S, const LaneTasks &T)
-{
-    const double B = bval(S, T.d_km, T.d_gqks);
-    return rdiv(B + S.two_a * (S.t * T.d_tau), S.two_sa, S.r_two_sa);
-}
-
-// exp_ocml: ggp_prop.h (shared with the lane schedule)
-
-// ggp_dawson_tab without branches: one division for the continued fraction, a NaN falls
-// through the polynomial (same values as ggp_dawson_tab).  tab: rows of kDawsonRow doubles
-// (the 9 coefficients, zero-padded to 10), 16-B aligned: five 128-bit LDS reads per value;
-// Horner with fused multiply-adds (<= 1 ulp from the separate-rounding form; the device
-// Dawson stays within the reference's bound, tests/test_gpu_device_math.py)
-constexpr int kDawsonRow = 10;
-#ifndef GGP_HOST_SIM
-GGP_DEV double dawson_bf(const double x, const double *tab)
-{
-    const double ax = fabs(x);
-    const double d1 = 1.0 + ax;
-    const double y100 = rdiv(100.0, d1, frcp(d1));   // IEEE 100 / (1 + ax) for finite ax
-#if defined(__HIP_DEVICE_COMPILE__)
-    int kt;   // v_cvt_i32_f64: NaN -> 0 (then t and the value are NaN), no guard needed
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(kt) : "v"(y100));
-    const int k = min(kt, GGP_DAWSON_NINT - 1);
-    const double2 *c2 = reinterpret_cast<const double2 *>(tab + __mul24(k, kDawsonRow));
-#else
-    const int k = min((int)(y100 >= 0.0 ? y100 : 0.0), GGP_DAWSON_NINT - 1);
-    const double2 *c2 = reinterpret_cast<const double2 *>(tab + kDawsonRow * k);
-#endif
-    const double2 a01 = c2[0], a23 = c2[1], a45 = c2[2], a67 = c2[3], a89 = c2[4];
-    const double t = 2.0 * y100 - (double)(2 * k + 1);
-    double h = __builtin_fma(a89.x, t, a67.y);
-    h = __builtin_fma(h, t, a67.x);
-    h = __builtin_fma(h, t, a45.y);
-    h = __builtin_fma(h, t, a45.x);
-    h = __builtin_fma(h, t, a23.y);
-    h = __builtin_fma(h, t, a23.x);
-    h = __builtin_fma(h, t, a01.y);
-    double w = pin(__builtin_fma(h, t, a01.x));
-    // the Taylor and continued-fraction branches are rare (|x| < ~0.03, |x| > 45; exclusive):
-    // formed, and selected, only when some lane of the wave needs them (a wave-uniform branch;
-    // NaN takes neither)
-    const bool use_taylor = y100 >= (double)GGP_DAWSON_NINT, use_cf = ax > 45.0;
-    if (__builtin_amdgcn_ballot_w64(use_taylor)) {
-        const double x2 = ax * ax;
-        const double *tc = ggp_dawson_taylor;
-        const double taylor = pin(ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4])))));
-        w = use_taylor ? taylor : w;
-    }
-    if (__builtin_amdgcn_ballot_w64(use_cf)) {
-        const bool far = ax > 5e7;
-        const double num = far ? GGP_ISPI : pin(GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2));
-        const double den = far ? ax : pin(ax * ((ax * ax) * (ax * ax - 5) + 3.75));
-        const double cf = pin(num / den);
-        w = use_cf ? cf : w;
-    }
-    return GGP_SPI2 * (x < 0.0 ? -w : w);
-}
-
-#endif  // GGP_HOST_SIM
-
-// The tauint denominators of k = 0..3 (2 sqrt a, then pow_task's 4 a^1.5, 8 a^2.5, 16 a^3.5)
-// and their rdiv seeds (r_two_sa, then 1/(4 a^1.5) = 2 r4a r2sa and each next power one factor
-// 2 r4a = 1/(2a) more: seeds only, rdiv's residual correction makes the quotient independent of
-// a few ulp in them).  Uniform values: lane 0 stores them (no per-lane select).
-GGP_DEV void store_pw(const WStep &S, double *PW)
-{
-    const double sa = S.two_sa * 0.5, a = S.a;   // sqrt(a) exactly
-    const double r0 = 2. * (S.r_four_a * S.r_two_sa);
-    const double r1 = 2. * (S.r_four_a * r0);
-    const double r2 = 2. * (S.r_four_a * r1);
-    PW[0] = S.two_sa;
-    PW[1] = 4. * (a * sa);
-    PW[2] = 8. * ((a * a) * sa);
-    PW[3] = 16. * (((a * a) * a) * sa);
-    PW[4] = S.r_two_sa;
-    PW[5] = r0;
-    PW[6] = r1;
-    PW[7] = r2;
-}
-
-// tau_unified without branches (X, Dw, PW: the LDS arrays)
-GGP_DEV double tau_bf(const WStep &S, const LaneTasks &L, const double *X, const double *Dw, const double *PW)
-{
-    const ITask T = L.it;
-    const double D0 = Dw[T.d0], D1 = Dw[T.d1];
-    const double E0 = X[T.x0], E1 = X[T.x1];
-    const double ec = X[T.xc], ea0 = X[T.xa0], ea1 = X[T.xa1];
-    const int k = T.k;
-    const double den = PW[k], rden = PW[4 + k];
-    const double B = pin(bval(S, L.i_km, L.i_gqks));
-    const double t0 = S.t * L.i_tau0, t1 = S.t * L.i_tau1;
-    const double BB = pin(B * B);
-    const double al3 = pin(BB - 2. * S.two_a);
-    const double al = k == 1 ? 1.0 : k == 2 ? B : al3;
-    const double be2 = pin(-S.two_a), be3 = pin(-S.two_a * B);
-    const double be = k == 1 ? 0.0 : k == 2 ? be2 : be3;
-    const double ga = k == 3 ? S.four_aa : 0.0;
-    const double P0 = al + t0 * (be + ga * t0), P1 = al + t1 * (be + ga * t1);
-    const double q1 = pin(B * 2.), q2 = pin((S.two_a - BB) * 2.), q3 = pin(B * (-6. * S.a + BB) * 2.);
-    const double Q = k == 0 ? -2.0 : k == 1 ? q1 : k == 2 ? q2 : q3;
-    const double S1 = S.two_sa * L.i_s1;   // 2 sqrt a (k = 2) or -2 sqrt a
-    const double dterm = pin(Q * (E0 * D0 - E1 * D1));
-    const double xfull = pin(S1 * ec * (ea0 * P0 - ea1 * P1) + dterm);
-    const double x = k == 0 ? dterm : xfull;
-    return rdiv(x, den, rden);
 }
 
 // The measurement step of the wave schedule (ggp_innovation + ggp_posterior, likelihood.h:53-69,
@@ -408,14 +179,668 @@ GGP_DEV double ll_quad(const double x0, const double x1, const double S00, const
     return (h0 * si00 + h1 * si01) * x0 + (h0 * si01 + h1 * si11) * x1;
 }
 
-// the outputs' variables V (ggp_outtab.h): lane 0 stores them, stage D reads them
-GGP_DEV void store_v(const double *m, const double *C, const double t, const OU &P, double *V)
+
+// ---- exponentials: computed in stage B, cached per dt, or products ----------------------
+// factor kinds of a product exponential X[j] = X[rep] * factor
+enum { F_ONE = 0, F_EGL, F_EGQ, F_REBT, F_EPGQ };
+struct XMap {
+    unsigned char rep, fac;
+};
+// c_B = c_A - gl t, c_J = c_I = c_A - gq t, c_G = c_A - b t (half base); c_E = c_C,
+// c_D = c_C - gq t, c_F = c_C + gq t (double base): exp(c + ...) = exp(c_rep + ...) exp(+-k t)
+constexpr XMap xmap(const int j)
 {
-    const double v[V_N - 1] = {m[0], m[1], m[2] - P.ml, m[3] - P.mq, C[0], C[1], C[2], C[3],
-                               C[5], C[6], C[7], C[10], C[11], C[15], t};
-#pragma unroll
-    for (int k = 0; k < V_N - 1; ++k) V[1 + k] = v[k];
+    switch (j) {
+    case XC_B: return {XC_A, F_EGL};
+    case XC_J: return {XC_A, F_EGQ};
+    case XC_G: return {XC_A, F_REBT};
+    case XC_I: return {XC_A, F_EGQ};
+    case XC_D: return {XC_C, F_EGQ};
+    case XC_E: return {XC_C, F_ONE};
+    case XC_F: return {XC_C, F_EPGQ};
+    case XZ_1Bt: return {XZ_1At, F_EGL};
+    case XZ_1Jt: return {XZ_1At, F_EGQ};
+    case XZ_1Gt: return {XZ_1At, F_REBT};
+    case XZ_2Bt: return {XZ_2At, F_EGL};
+    case XZ_2Jt: return {XZ_2At, F_EGQ};
+    case XZ_2It: return {XZ_2At, F_EGQ};
+    case XZ_2Gt: return {XZ_2At, F_REBT};
+    case XZ_3Et: return {XZ_3Ct, F_ONE};
+    case XZ_3Dt: return {XZ_3Ct, F_EGQ};
+    case XZ_4Et: return {XZ_4Ct, F_ONE};
+    case XZ_4Ft: return {XZ_4Ct, F_EPGQ};
+    case XZ_3E2: return {XZ_3C2, F_ONE};
+    case XZ_3D2: return {XZ_3C2, F_EGQ};
+    case XZ_4E2: return {XZ_4C2, F_ONE};
+    case XZ_4F2: return {XZ_4C2, F_EPGQ};
+    default: return {(unsigned char)j, F_ONE};
+    }
 }
+constexpr bool x_computed(const int j)
+{
+    return j < NXT && !(j >= XS_bt && j <= XS_gq) && xmap(j).rep == j;
+}
+
+constexpr int kNExp = 46, kNDaw = ND, kLaneD0 = kNExp;   // lanes 46..59: Dawson values
+struct XList {
+    unsigned char j[kNExp];
+    int n;
+};
+constexpr XList make_xlist()
+{
+    XList L{};
+    for (int j = 0; j < NXT; ++j)
+        if (x_computed(j)) L.j[L.n++] = (unsigned char)j;
+    return L;
+}
+constexpr XList kXL = make_xlist();
+static_assert(kXL.n == kNExp, "46 state-dependent exponentials are computed per step");
+static_assert(kNExp + kNDaw <= 64, "stage B: one task per lane");
+
+// ---- the outputs' state monomials (stage D): V[v1] V[v2] V[v3] of every term, deduplicated --
+struct MonoList {
+    unsigned char v[64][3];
+    unsigned char term[64][kOutL];   // monomial index of lane l's term q
+    int n;
+};
+constexpr MonoList make_monos()
+{
+    MonoList M{};
+    for (int l = 0; l < 64; ++l)
+        for (int q = 0; q < kOutL; ++q) {
+            const OutTerm T = kOutTerm[l][q];
+            int f = -1;
+            for (int i = 0; i < M.n; ++i)
+                if (M.v[i][0] == T.v1 && M.v[i][1] == T.v2 && M.v[i][2] == T.v3) f = i;
+            if (f < 0) {
+                f = M.n++;
+                M.v[f][0] = T.v1;
+                M.v[f][1] = T.v2;
+                M.v[f][2] = T.v3;
+            }
+            M.term[l][q] = (unsigned char)f;
+        }
+    return M;
+}
+constexpr MonoList kMono = make_monos();
+static_assert(kMono.n <= 64, "one monomial per lane");
+
+// ---- LDS layout (doubles, one array) --------------------------------------------------
+constexpr int kTabRow = 12;                       // Horner coefficients per row (exp row: ocml's)
+constexpr int kTabRows = GGP_DAWSON_NINT + 1;     // Dawson rows 0..96, then the exp row
+constexpr int kExpRow = GGP_DAWSON_NINT;
+enum {
+    L_TAB = 0,                                    // 16-B aligned rows
+    L_X = L_TAB + kTabRows * kTabRow,             // exponentials (NX slots: X_ONE = 1), then exp(+gq t)
+    L_XPGQ = L_X + NX,
+    L_D = L_XPGQ + 1,                             // Dawson values
+    L_BV = L_D + ND,                              // outputs basis: 1, the 45 integrals, 18 exp-derived
+    L_V = L_BV + BV_N,                            // outputs variables: 1, state, t
+    L_MONO = L_V + V_N,                           // the step's state monomials
+    L_OUT = L_MONO + 64,                          // the 14 raw outputs (block sums)
+    L_ZERO = L_OUT + kOutN,                       // 0.0 and 1.0 for the finish fma
+    L_ONE1 = L_ZERO + 1,
+    L_ST = L_ONE1 + 1,                            // prior: m[4], C[16], -x0 at 20, -x1 at 24
+    L_POST = L_ST + 28,                           // posterior: m[4], C[16]
+    L_RX0 = L_POST + 20,                          // ll ring: -x0, -x1, S00, S01, S11 per row
+    L_RX1 = L_RX0 + 64,
+    L_RS0 = L_RX1 + 64,
+    L_RS1 = L_RS0 + 64,
+    L_RS2 = L_RS1 + 64,
+    L_RT = L_RS2 + 64,                            // ll terms of the chunk
+    L_ROWL = L_RT + 64,                           // this 64-row chunk's data (+ next time)
+    L_ROWF = L_ROWL + 64,
+    L_ROWT = L_ROWF + 64,
+    L_DUMMY = L_ROWT + 66,                        // one slot per lane for stores without a task
+    kLds = L_DUMMY + 64
+};
+static_assert(L_X % 2 == 0 && L_TAB == 0, "128-bit table rows");
+static_assert(L_RT % 2 == 0, "128-bit ll-term reads");
+
+// the exp row: ocml's exp polynomial (ggp_prop.h exp_ocml), Horner from the top, the two
+// trailing fma(t, p, 1.0) steps as coefficients 1.0
+constexpr double kExpCoef[kTabRow] = {0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22, 0x1.71dee623fde64p-19,
+                                      0x1.a01997c89e6b0p-16, 0x1.a01a014761f6ep-13, 0x1.6c16c1852b7b0p-10,
+                                      0x1.1111111122322p-7,  0x1.55555555502a1p-5,  0x1.5555555555511p-3,
+                                      0x1.000000000000bp-1,  1.0,                   1.0};
+// table entry k of the LDS copy: Dawson row r = [0, 0, 0, c8 .. c0] (three leading zeros keep
+// the 8-step Horner bitwise: fma(0, t, 0) = 0, fma(0, t, c8) = c8), then the exp row
+GGP_DEV double tab_entry(const int k)
+{
+    const int r = k / kTabRow, i = k % kTabRow;
+    if (r == kExpRow) return kExpCoef[i];
+    return i < 3 ? 0.0 : ggp_dawson_coef[GGP_DAWSON_NCOEF * r + (kTabRow - 1 - i)];
+}
+
+// ---- lane constants -------------------------------------------------------------------------
+// LaneC: everything that does not depend on the parameters, a compile-time table (kLaneTab, one
+// row per lane, loaded once per launch); Lane: the registers the step reads, completed from
+// the row and the parameters (lane_from).  Slots are indices into the one LDS array.
+struct LaneC {
+    // stage B: argument forms (ggp_wave.h exp_arg); Dawson lanes use z only.  The c slope is
+    // kb b + kgl gl + kgq gq (c_slope's value: the integer coefficients are exact)
+    double b_tau, b_km, b_ks, b_m1, b_m2, b_kb, b_kgl, b_kgq, b_mult;
+    int b_isE, b_isA, b_isD, b_exmask, b_dst;
+    // stage C: the integral (tau_unified) with 0/1 selectors
+    double i_tau0, i_tau1, i_km, i_ks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
+    int i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
+    // stage D: monomial task, terms (kappa index; 255 = padding)
+    int mo_v0, mo_v1, mo_v2, mo_dst;
+    int d_mono[kOutL], d_basis[kOutL], d_kap[kOutL];
+    int d_bs, d_out;
+    // finish / update (vshift = fml ml + fmq mq)
+    int f_src, f_na, f_nb, f_row, f_dst;
+    int u_ub, u_wb, u_c, u_post, u_v;
+    double u_fml, u_fmq;
+};
+
+struct Lane {
+    double b_tau, b_km, b_gqks, b_m1, b_m2, b_kc, b_mult;
+    int b_isE, b_isA, b_isD, b_exmask, b_dst;
+    double i_tau0, i_tau1, i_km, i_gqks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
+    int i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
+    int mo_v0, mo_v1, mo_v2, mo_dst;
+    int d_mono[kOutL], d_basis[kOutL];
+    double d_kap[kOutL];
+    int d_bs, d_out;
+    int f_src, f_na, f_nb, f_row, f_dst;
+    int u_ub, u_wb, u_c, u_post, u_v;
+    double u_vshift;
+    double c_sv;   // the per-dt block: exp(c_sv t) for lanes 0-6 (exp(s t) of pickSV, then exp(+gq t))
+};
+
+// c_slope (ggp_wave.h) as integer coefficients of (b, gl, gq)
+constexpr void c_coef(const int ic, double &kb, double &kgl, double &kgq)
+{
+    kb = (ic == cA || ic == cB || ic == cJ || ic == cI) ? -1.0 : -2.0;
+    kgl = ic == cB ? -1.0 : 0.0;
+    kgq = (ic == cJ || ic == cI || ic == cD) ? -1.0 : ic == cF ? 1.0 : ic == cH ? -2.0 : 0.0;
+}
+
+constexpr int fac_slot(const int f)
+{
+    return f == F_EGL ? L_X + XS_gl : f == F_EGQ ? L_X + XS_gq : f == F_REBT ? L_BV + BV_R_EBT : f == F_EPGQ ? L_XPGQ : L_X + X_ONE;
+}
+
+constexpr LaneC make_lane_c(const int lane)
+{
+    LaneC L{};
+    // ---- stage B
+    {
+        const bool isD = lane >= kLaneD0 && lane < kLaneD0 + kNDaw;
+        const bool isX = lane < kNExp;
+        const int xj = kXL.j[isX ? lane : 0];
+        const XTask xt = kXT[xj];
+        if (isD) {
+            const DTask dk = kDT[lane - kLaneD0];
+            L.b_tau = (double)dk.it;
+            L.b_km = wave::kKm[dk.iB];
+            L.b_ks = wave::kKs[dk.iB];
+            L.b_m1 = 1.0;
+            L.b_m2 = 0.5;
+            L.b_isD = 1;
+            L.b_exmask = 0;
+            L.b_mult = GGP_SPI2;
+            L.b_dst = L_D + (lane - kLaneD0);
+        } else {
+            const int xb = xt.iB < 6 ? xt.iB : 0;
+            L.b_tau = (double)xt.it;
+            L.b_km = wave::kKm[xb];
+            L.b_ks = wave::kKs[xb];
+            const bool half = xt.ic == cA || xt.ic == cB || xt.ic == cJ || xt.ic == cG || xt.ic == cI;
+            L.b_m1 = half ? 1.0 : 2.0;
+            L.b_m2 = half ? 0.5 : 2.0;
+            c_coef(xt.ic, L.b_kb, L.b_kgl, L.b_kgq);
+            L.b_isE = xt.kind == KX_E;
+            L.b_isA = xt.kind == KX_A;
+            L.b_exmask = -1;
+            L.b_mult = 1.0;
+            L.b_dst = isX ? L_X + xj : L_DUMMY + lane;
+        }
+    }
+    // ---- stage C
+    {
+        const bool has = lane < NI;
+        const ITask T = kIT[has ? lane : 0];
+        L.i_tau0 = (double)T.it0;
+        L.i_tau1 = (double)T.it1;
+        L.i_km = wave::kKm[T.iB];
+        L.i_ks = wave::kKs[T.iB];
+        const int k = T.k;
+        L.i_u0 = k == 1 ? 1.0 : 0.0;
+        L.i_u1 = k == 2 ? 1.0 : 0.0;
+        L.i_u2 = k == 3 ? 1.0 : 0.0;
+        L.i_w2 = k == 2 ? 1.0 : 0.0;
+        L.i_w3 = k == 3 ? 1.0 : 0.0;
+        L.i_g = k == 3 ? 1.0 : 0.0;
+        L.i_s0 = k == 0 ? -2.0 : 0.0;
+        L.i_s1 = k == 1 ? 1.0 : 0.0;
+        L.i_s2 = k == 2 ? 1.0 : 0.0;
+        L.i_s3 = k == 3 ? 1.0 : 0.0;
+        L.i_S1 = k == 0 ? 0.0 : k == 2 ? 1.0 : -1.0;
+        L.i_d0 = L_D + T.d0;
+        L.i_d1 = L_D + T.d1;
+        L.i_e0r = L_X + xmap(T.x0).rep;
+        L.i_e0f = fac_slot(xmap(T.x0).fac);
+        L.i_e1r = L_X + xmap(T.x1).rep;
+        L.i_e1f = fac_slot(xmap(T.x1).fac);
+        L.i_ecr = L_X + xmap(T.xc).rep;
+        L.i_ecf = fac_slot(xmap(T.xc).fac);
+        L.i_a0 = L_X + T.xa0;
+        L.i_a1 = L_X + T.xa1;
+        L.i_dst = has ? L_BV + BV_I + lane : L_DUMMY + lane;
+    }
+    // ---- stage D
+    {
+        const bool mo = lane < kMono.n;
+        L.mo_v0 = L_V + kMono.v[mo ? lane : 0][0];
+        L.mo_v1 = L_V + kMono.v[mo ? lane : 0][1];
+        L.mo_v2 = L_V + kMono.v[mo ? lane : 0][2];
+        L.mo_dst = mo ? L_MONO + lane : L_DUMMY + lane;
+        for (int q = 0; q < kOutL; ++q) {
+            const OutTerm T = kOutTerm[lane][q];
+            L.d_mono[q] = L_MONO + kMono.term[lane][q];
+            L.d_basis[q] = L_BV + T.basis;
+            L.d_kap[q] = T.kap;
+        }
+        L.d_bs = kOutBlock[lane];
+        int out = L_DUMMY + lane;
+        for (int k = 0; k < kOutN; ++k) out = kOutLead[k] == lane ? L_OUT + k : out;
+        L.d_out = out;
+    }
+    // ---- finish (lane e: prior entry e) and update (posterior entry e)
+    {
+        // output index of each C entry (out_store)
+        constexpr int kCo[16] = {4, 5, 6, 7, 5, 8, 9, 10, 6, 9, 11, 12, 7, 10, 12, 13};
+        const int e = lane;
+        L.f_row = 0;
+        if (e < 4) {
+            L.f_src = L_OUT + e;
+            L.f_na = L_ZERO;
+            L.f_nb = L_ZERO;
+            L.f_dst = L_ST + e;
+        } else if (e < 20) {
+            const int o = kCo[e - 4];
+            L.f_src = L_OUT + o;
+            L.f_na = kOutNm[o][0] >= 0 ? L_OUT + kOutNm[o][0] : L_ZERO;
+            L.f_nb = kOutNm[o][0] >= 0 ? L_OUT + kOutNm[o][1] : L_ZERO;
+            L.f_dst = L_ST + e;
+        } else if (e == 20 || e == 24) {   // -x0 = m0 - y_l, -x1 = m1 - y_f (the row slot added per step)
+            L.f_src = L_OUT + (e == 20 ? 0 : 1);
+            L.f_na = L_ONE1;
+            L.f_nb = e == 20 ? L_ROWL : L_ROWF;
+            L.f_row = 1;
+            L.f_dst = L_ST + e;
+        } else {
+            L.f_src = L_ZERO;
+            L.f_na = L_ZERO;
+            L.f_nb = L_ZERO;
+            L.f_dst = L_DUMMY + lane;
+        }
+        // posterior entry e: c - fma(KS1[i], z, KS0[i] * w), KS from u = C[0][i], v = C[1][i]
+        // (u, v at ST[4 + i], ST[8 + i]); w, z = C[0][j], C[1][j] for a covariance, -x0, -x1 for a mean
+        if (e < 20) {
+            const int i = e < 4 ? e : (e - 4) / 4, j = e < 4 ? -1 : (e - 4) % 4;
+            L.u_ub = L_ST + 4 + i;
+            L.u_wb = j < 0 ? L_ST + 20 : L_ST + 4 + j;
+            L.u_c = L_ST + e;
+            L.u_post = L_POST + e;
+            // stage D's variables: the means (bl - ml, bq - mq) and the upper triangle
+            constexpr int kCv[16] = {V_CXX, V_CXG, V_CXL, V_CXQ, -1, V_CGG, V_CGL, V_CGQ, -1, -1, V_CLL, V_CLQ, -1, -1, -1, V_CQQ};
+            const int vs = e < 4 ? V_BX + e : kCv[e - 4];
+            L.u_v = vs >= 0 ? L_V + vs : L_DUMMY + lane;
+            L.u_fml = e == 2 ? 1.0 : 0.0;
+            L.u_fmq = e == 3 ? 1.0 : 0.0;
+        } else {
+            L.u_ub = L_ST + 4;
+            L.u_wb = L_ST + 4;
+            L.u_c = L_ST;
+            L.u_post = L_DUMMY + lane;
+            L.u_v = L_DUMMY + lane;
+        }
+    }
+    return L;
+}
+
+struct LaneTab {
+    LaneC l[64];
+};
+constexpr LaneTab make_lane_tab()
+{
+    LaneTab T{};
+    for (int l = 0; l < 64; ++l) T.l[l] = make_lane_c(l);
+    return T;
+}
+constexpr LaneTab kLaneTab = make_lane_tab();
+
+// the lane's registers from its row and the parameters; kap: the 33 kappas (LDS, lane_kappa)
+GGP_DEV Lane lane_from(const int lane, const LaneC &C, const OU &P, const double *kap)
+{
+    Lane L;
+    L.b_tau = C.b_tau; L.b_km = C.b_km; L.b_gqks = P.gq * C.b_ks; L.b_m1 = C.b_m1; L.b_m2 = C.b_m2;
+    L.b_kc = __builtin_fma(C.b_kgq, P.gq, __builtin_fma(C.b_kgl, P.gl, C.b_kb * P.b));
+    L.b_mult = C.b_mult;
+    L.b_isE = C.b_isE; L.b_isA = C.b_isA; L.b_isD = C.b_isD; L.b_exmask = C.b_exmask; L.b_dst = C.b_dst;
+    L.i_tau0 = C.i_tau0; L.i_tau1 = C.i_tau1; L.i_km = C.i_km; L.i_gqks = P.gq * C.i_ks;
+    L.i_u0 = C.i_u0; L.i_u1 = C.i_u1; L.i_u2 = C.i_u2; L.i_w2 = C.i_w2; L.i_w3 = C.i_w3; L.i_g = C.i_g;
+    L.i_s0 = C.i_s0; L.i_s1 = C.i_s1; L.i_s2 = C.i_s2; L.i_s3 = C.i_s3; L.i_S1 = C.i_S1;
+    L.i_d0 = C.i_d0; L.i_d1 = C.i_d1; L.i_e0r = C.i_e0r; L.i_e0f = C.i_e0f; L.i_e1r = C.i_e1r; L.i_e1f = C.i_e1f;
+    L.i_ecr = C.i_ecr; L.i_ecf = C.i_ecf; L.i_a0 = C.i_a0; L.i_a1 = C.i_a1; L.i_dst = C.i_dst;
+    L.mo_v0 = C.mo_v0; L.mo_v1 = C.mo_v1; L.mo_v2 = C.mo_v2; L.mo_dst = C.mo_dst;
+#pragma unroll
+    for (int q = 0; q < kOutL; ++q) {
+        L.d_mono[q] = C.d_mono[q];
+        L.d_basis[q] = C.d_basis[q];
+        L.d_kap[q] = C.d_kap[q] == 255 ? 0.0 : kap[C.d_kap[q]];
+    }
+    L.d_bs = C.d_bs; L.d_out = C.d_out;
+    L.f_src = C.f_src; L.f_na = C.f_na; L.f_nb = C.f_nb; L.f_row = C.f_row; L.f_dst = C.f_dst;
+    L.u_ub = C.u_ub; L.u_wb = C.u_wb; L.u_c = C.u_c; L.u_post = C.u_post; L.u_v = C.u_v;
+    L.u_vshift = __builtin_fma(C.u_fmq, P.mq, C.u_fml * P.ml);
+    L.c_sv = lane < 6 ? wave::sv_of(P, lane) : P.gq;
+    return L;
+}
+
+// kappa k of the outputs (out_kappa's value) for lanes k < kOutNK: one per lane instead of four
+GGP_DEV double lane_kappa(const int lane, const OU &P) { return out_kappa(P, lane < kOutNK ? lane : 0); }
+
+// ---- step scalars from the posterior (every lane the same values) --------------------------
+// bx, bl, Cxx, Cxl, Cll as stored by the update (POST[0], [2], [4], [6], [14])
+GGP_DEV wave::WStep wstep2(const double bx, const double bl, const double Cxx, const double Cxl, const double Cll,
+                           const double t, const double b)
+{
+    double m[4] = {bx, 0.0, bl, 0.0}, C[16] = {};
+    C[0] = Cxx;
+    C[2] = Cxl;
+    C[10] = Cll;
+    return wave::wstep(m, C, t, b);
+}
+
+// 1/d: v_rcp_f64 and one Newton step -- an rdiv seed (the residual step makes the quotient
+// independent of an ulp or two in it)
+GGP_DEV double rcp1(const double d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double r = __builtin_amdgcn_rcp(d);
+    return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+#else
+    return 1.0 / d;
+#endif
+}
+
+GGP_DEV int mul24(const int a, const int b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);   // v_mul_i32_i24: full rate (v_mul_lo_u32 is quarter rate)
+#else
+    return a * b;
+#endif
+}
+
+GGP_DEV int cvt_i32(const double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int k;   // v_cvt_i32_f64: NaN -> 0, saturating
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(k) : "v"(x));
+    return k;
+#else
+    if (x != x) return 0;
+    return x >= 2147483647.0 ? 2147483647 : x <= -2147483648.0 ? (-2147483647 - 1) : (int)x;
+#endif
+}
+
+// ---- stage B: one transcendental per lane ---------------------------------------------------
+// the rare branches: exp beyond 2^50 (ocml's exp), Dawson Taylor (y100 >= 97) and continued
+// fraction (|x| > 45), as ggp_wave.h dawson_bf
+GGP_DEV double stageB_rare(const bool isD, const double arg, const double z, const double v)
+{
+    if (!isD) return fabs(arg) < kExpFastMax ? v : exp(arg);
+    const double ax = fabs(z);
+    const double y100 = 100.0 / (1.0 + ax);
+    double w;
+    if (ax > 45.0) {
+        const bool far = ax > 5e7;
+        const double num = far ? GGP_ISPI : GGP_ISPI * ((ax * ax) * (ax * ax - 4.5) + 2);
+        const double den = far ? ax : ax * ((ax * ax) * (ax * ax - 5) + 3.75);
+        w = num / den;
+    } else if (y100 >= (double)GGP_DAWSON_NINT) {
+        const double x2 = ax * ax;
+        const double *tc = ggp_dawson_taylor;
+        w = ax * (tc[0] - x2 * (tc[1] - x2 * (tc[2] - x2 * (tc[3] - x2 * tc[4]))));
+    } else {
+        return v;
+    }
+    return GGP_SPI2 * (z < 0.0 ? -w : w);
+}
+
+struct BOut {
+    double v, arg, z;
+    bool rare;
+};
+
+GGP_DEV void sched_fence()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
+{
+    // the Dawson argument and interval first, so the table row's six 128-bit LDS reads are in
+    // flight while the exponential's argument and reduction are formed (exp lanes read the exp row)
+    const double ti = S.t * L.b_tau;
+    const double B = wave::pin(__builtin_fma(S.Cxl, L.b_km, S.bbl) + L.b_gqks);
+    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
+    const double ax = fabs(z);
+    // y100 = 100 / (1 + |z|) to the correctly rounded quotient (frcp seed, Markstein step): near
+    // small |z| an ulp of y100 is tens of ulp of the value (dx/dy ~ 1e-2, x ~ 0.05)
+    const double d1 = 1.0 + ax;
+    const double y100 = rdiv(100.0, d1, frcp(d1));
+    const int k = min(cvt_i32(y100), GGP_DAWSON_NINT - 1);
+    const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
+    const double *A = lds + L_TAB + row;
+    double a[kTabRow];
+#pragma unroll
+    for (int i = 0; i < kTabRow; ++i) a[i] = A[i];
+    sched_fence();
+    const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
+    const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
+    const double argA = wave::pin(ti * (B + S.a * ti));
+    const double argE = wave::pin(n + c + z * z);
+    const double argZ = wave::pin(S.a * (ti * ti) + B * ti + c);
+    const double arg = L.b_isE ? argE : L.b_isA ? argA : argZ;
+    // exp reduction (exp_ocml); Dawson: the Chebyshev variable of interval k
+    const double dn = __builtin_rint(arg * 0x1.71547652b82fep+0);
+    double r = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, arg);
+    r = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, r);
+    const double td = __builtin_fma(2.0, y100, -(double)(2 * k + 1));
+    const double tv = L.b_isD ? td : r;
+    double h = __builtin_fma(a[0], tv, a[1]);
+#pragma unroll
+    for (int i = 2; i < kTabRow; ++i) h = __builtin_fma(h, tv, a[i]);
+    // no branches below: the exponent masked to 0 on Dawson lanes, the rare flags by bitwise ops
+    double v = __builtin_ldexp(h * L.b_mult, cvt_i32(dn) & L.b_exmask);
+    v = ((L.b_isD != 0) & (z < 0.0)) ? -v : v;
+    BOut o;
+    o.v = v;
+    o.arg = arg;
+    o.z = z;
+    const bool rare_d = (y100 >= (double)GGP_DAWSON_NINT) | (ax > 45.0);
+    const bool rare_e = !(fabs(arg) < kExpFastMax);
+    o.rare = ((L.b_isD != 0) & rare_d) | ((L.b_isD == 0) & rare_e);
+    return o;
+}
+
+// ---- stage C: one integral per lane (tau_unified; mean_cov_model.h:9-67) --------------------
+GGP_DEV double stageC(const wave::WStep &S, const Lane &L, const double *lds)
+{
+    const double D0 = lds[L.i_d0], D1 = lds[L.i_d1];
+    const double E0 = lds[L.i_e0r] * lds[L.i_e0f];
+    const double E1 = lds[L.i_e1r] * lds[L.i_e1f];
+    const double ec = lds[L.i_ecr] * lds[L.i_ecf];
+    const double ea0 = lds[L.i_a0], ea1 = lds[L.i_a1];
+    const double B = wave::pin(__builtin_fma(S.Cxl, L.i_km, S.bbl) + L.i_gqks);
+    const double t0 = S.t * L.i_tau0, t1 = S.t * L.i_tau1;
+    const double BB = wave::pin(B * B);
+    const double al3 = BB - S.four_a;
+    const double al = __builtin_fma(L.i_u2, al3, __builtin_fma(L.i_u1, B, L.i_u0));
+    const double be = -S.two_a * __builtin_fma(L.i_w3, B, L.i_w2);
+    const double ga = L.i_g * S.four_aa;
+    const double P0 = al + t0 * (be + ga * t0), P1 = al + t1 * (be + ga * t1);
+    const double q1 = B * 2., q2 = (S.two_a - BB) * 2., q3 = B * (-6. * S.a + BB) * 2.;
+    const double Q = __builtin_fma(L.i_s3, q3, __builtin_fma(L.i_s2, q2, __builtin_fma(L.i_s1, q1, L.i_s0)));
+    const double S1 = S.two_sa * L.i_S1;
+    const double dterm = wave::pin(Q * (E0 * D0 - E1 * D1));
+    const double x = S1 * ec * (ea0 * P0 - ea1 * P1) + dterm;
+    // the denominator 2^(k+1) a^k sqrt(a) as two_sa (2a)^k: the products of store_pw's
+    // denominators (scaling by powers of two is exact), and an rdiv seed from v_rcp_f64
+    const double p1 = S.two_a, p2 = p1 * p1, p3 = p2 * p1;
+    const double qk = __builtin_fma(L.i_s3, p3, __builtin_fma(L.i_s2, p2, __builtin_fma(L.i_s1, p1, -0.5 * L.i_s0)));
+    const double den = S.two_sa * qk;
+    return rdiv(x, den, rcp1(den));
+}
+
+// ---- stage D: the lane's output terms over the step's monomials ------------------------------
+GGP_DEV double stageD(const Lane &L, const double *lds)
+{
+    double kv[kOutL], bv[kOutL];
+#pragma unroll
+    for (int q = 0; q < kOutL; ++q) {
+        kv[q] = L.d_kap[q] * lds[L.d_mono[q]];
+        bv[q] = lds[L.d_basis[q]];
+    }
+    double acc = kv[0] * bv[0];
+#pragma unroll
+    for (int q = 1; q < kOutL; ++q) acc = __builtin_fma(kv[q], bv[q], acc);
+    return acc;
+}
+
+GGP_DEV double mono(const Lane &L, const double *lds) { return (lds[L.mo_v0] * lds[L.mo_v1]) * lds[L.mo_v2]; }
+
+// ---- finish and update ------------------------------------------------------------------------
+GGP_DEV double finish(const Lane &L, const double *lds, const int slot)
+{
+    return __builtin_fma(-lds[L.f_na], lds[L.f_nb + (L.f_row ? slot : 0)], lds[L.f_src]);
+}
+
+struct UInnov {
+    double S00, S01, S11, si00, si01, si11;
+};
+// ggp_wave.h innovation from the prior's C00, C01, C11 and m1 (the same expressions)
+GGP_DEV UInnov uinnov(const double m1, const double C00, const double C01, const double C11, const double var_x,
+                      const double var_g, const int scaled, const double fp_auto)
+{
+    UInnov v;
+    const double d11 = scaled ? var_g * (m1 + fp_auto) : var_g;
+    v.S00 = C00 + var_x;
+    v.S01 = C01 + 0.0;
+    v.S11 = C11 + d11;
+    const double det = v.S00 * v.S11 - v.S01 * v.S01;
+    const double invdet = 1.0 / det;
+    v.si00 = v.S11 * invdet;
+    v.si01 = -v.S01 * invdet;
+    v.si11 = v.S00 * invdet;
+    return v;
+}
+
+// posterior entry of lane e (ggp_wave.h posterior: C_ij - fma(KS1_i, C1j, KS0_i C0j);
+// m_i + fma(KS1_i, x1, KS0_i x0) == m_i - fma(KS1_i, -x1, KS0_i (-x0)) bitwise)
+GGP_DEV double upost(const Lane &L, const double *lds, const UInnov &v)
+{
+    const double u = lds[L.u_ub], vv = lds[L.u_ub + 4];
+    const double w = lds[L.u_wb], z = lds[L.u_wb + 4];
+    const double c = lds[L.u_c];
+    const double KS0 = __builtin_fma(vv, v.si01, u * v.si00);
+    const double KS1 = __builtin_fma(vv, v.si11, u * v.si01);
+    return c - __builtin_fma(KS1, z, KS0 * w);
+}
+
+#ifdef GGP_HOST_SIM
+// ---- host emulation of one propagation + update step over the 64 lanes -----------------------
+// lds: the wave's LDS (table filled), state in POST / V; dt cache filled for t.  Returns the
+// posterior in lds POST.  Used by tools/hostsim.cpp to compare against the oracle.
+struct HostWave {
+    double lds[kLds];
+    Lane L[64];
+    OU P;
+    double b, t_cached = -1.0;
+    HostWave(const double *p)
+    {
+        P = make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+        b = P.b;
+        for (int i = 0; i < kLds; ++i) lds[i] = 0.0;
+        for (int k = 0; k < kTabRows * kTabRow; ++k) lds[L_TAB + k] = tab_entry(k);
+        double kap[kOutNK];
+        for (int k = 0; k < kOutNK; ++k) kap[k] = lane_kappa(k, P);
+        for (int l = 0; l < 64; ++l) L[l] = lane_from(l, kLaneTab.l[l], P, kap);
+        lds[L_X + X_ONE] = 1.0;
+        lds[L_BV + BV_ONE] = 1.0;
+        lds[L_V + V_ONE] = 1.0;
+        lds[L_ONE1] = 1.0;
+        lds[L_ZERO] = 0.0;
+    }
+    void dt_cache(const double t)
+    {
+        if (t == t_cached) return;
+        for (int s = 0; s < 6; ++s) lds[L_X + XS_bt + s] = exp(wave::sv_of(P, s) * t);
+        lds[L_XPGQ] = exp(P.gq * t);
+        double X[NX];
+        for (int k = 0; k < NX; ++k) X[k] = lds[L_X + k];
+        for (int j = 0; j < kNDerived; ++j) lds[L_BV + BV_R_EBT + j] = derived_generic(kDerived[j], X, P.gl, t);
+        lds[L_V + V_T] = t;
+        t_cached = t;
+    }
+    // propagate the state in POST over t: raw outputs to OUT
+    void propagate(const double t)
+    {
+        dt_cache(t);
+        const double *po = lds + L_POST;
+        const wave::WStep S = wstep2(po[0], po[2], po[4], po[6], po[14], t, b);
+        for (int l = 0; l < 64; ++l) lds[L[l].mo_dst] = mono(L[l], lds);
+        double vb[64];
+        for (int l = 0; l < 64; ++l) {
+            const BOut o = stageB(S, L[l], lds);
+            vb[l] = o.rare ? stageB_rare(L[l].b_isD, o.arg, o.z, o.v) : o.v;
+        }
+        for (int l = 0; l < 64; ++l) lds[L[l].b_dst] = vb[l];
+        double vc[64];
+        for (int l = 0; l < 64; ++l) vc[l] = stageC(S, L[l], lds);
+        for (int l = 0; l < 64; ++l) lds[L[l].i_dst] = vc[l];
+        double part[64];
+        for (int l = 0; l < 64; ++l) part[l] = stageD(L[l], lds);
+        for (int st = 0; st < 4; ++st) {
+            double nx[64];
+            for (int l = 0; l < 64; ++l) nx[l] = kOutBlock[l] > (1 << st) ? part[l] + part[out_partner(l, st)] : part[l];
+            for (int l = 0; l < 64; ++l) part[l] = nx[l];
+        }
+        for (int l = 0; l < 64; ++l) lds[L[l].d_out] = part[l];
+    }
+    // finish + distributed update with row data (y_l, y_f) at slot 0; returns the ll ring inputs
+    void update(const double y_l, const double y_f, const double var_x, const double var_g, const int scaled,
+                const double fp_auto, double *ring5)
+    {
+        lds[L_ROWL] = y_l;
+        lds[L_ROWF] = y_f;
+        double f[64];
+        for (int l = 0; l < 64; ++l) f[l] = finish(L[l], lds, 0);
+        for (int l = 0; l < 64; ++l) lds[L[l].f_dst] = f[l];
+        const double *st = lds + L_ST;
+        const UInnov v = uinnov(st[1], st[4], st[5], st[9], var_x, var_g, scaled, fp_auto);
+        double u[64];
+        for (int l = 0; l < 64; ++l) u[l] = upost(L[l], lds, v);
+        for (int l = 0; l < 64; ++l) {
+            lds[L[l].u_post] = u[l];
+            lds[L[l].u_v] = u[l] - L[l].u_vshift;
+        }
+        ring5[0] = st[20];
+        ring5[1] = st[24];
+        ring5[2] = v.S00;
+        ring5[3] = v.S01;
+        ring5[4] = v.S11;
+    }
+};
+#endif
 
 }  // namespace wave
 }  // namespace ggp

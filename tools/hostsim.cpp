@@ -83,30 +83,30 @@ int hs_check_derived(void)
 }
 }
 
-// ---- the redesigned wave step (ggp_wave2.h): 46 computed exponentials + 22 products,
+// ---- the wave step (ggp_wave.h): 46 computed exponentials + 22 products,
 // unified exp / Dawson Horner, monomial outputs -- propagation only (the oracle updates) ----
-#include "ggp_wave2.h"
+#include "ggp_wave.h"
 #include <memory>
 
 extern "C" {
-void hs_mcm_w2(double *m, double *C, double t, const double *p)
+void hs_mcm_wave(double *m, double *C, double t, const double *p)
 {
     using namespace ggp;
-    static std::unique_ptr<w2::HostWave> W;
+    static std::unique_ptr<wave::HostWave> W;
     static double pc[11] = {0};
     if (!W || memcmp(pc, p, sizeof(pc))) {
-        W.reset(new w2::HostWave(p));
+        W.reset(new wave::HostWave(p));
         memcpy(pc, p, sizeof(pc));
     }
     double *lds = W->lds;
-    for (int k = 0; k < 4; ++k) lds[w2::L_POST + k] = m[k];
-    for (int k = 0; k < 16; ++k) lds[w2::L_POST + 4 + k] = C[k];
-    double *V = lds + w2::L_V;
+    for (int k = 0; k < 4; ++k) lds[wave::L_POST + k] = m[k];
+    for (int k = 0; k < 16; ++k) lds[wave::L_POST + 4 + k] = C[k];
+    double *V = lds + wave::L_V;
     const double v[14] = {m[0], m[1], m[2] - W->P.ml, m[3] - W->P.mq, C[0], C[1], C[2], C[3], C[5], C[6], C[7], C[10], C[11], C[15]};
     for (int k = 0; k < 14; ++k) V[1 + k] = v[k];
     W->propagate(t);
     double o[kOutN];
-    out_finish([&](int k) { return lds[w2::L_OUT + k]; }, o);
+    out_finish([&](int k) { return lds[wave::L_OUT + k]; }, o);
     out_store(o, m, C);
 }
 }

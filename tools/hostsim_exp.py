@@ -23,7 +23,7 @@ FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, c
 L.ora_set_mcm_hook.argtypes = [ctypes.c_void_p]
 HOOKS = {"oracle": None, "lane": ctypes.cast(HS.hs_mcm_lane, ctypes.c_void_p).value,
          "tab": ctypes.cast(HS.hs_mcm_tab, ctypes.c_void_p).value,
-         "w2": ctypes.cast(HS.hs_mcm_w2, ctypes.c_void_p).value}
+         "wave": ctypes.cast(HS.hs_mcm_wave, ctypes.c_void_p).value}
 
 G = os.path.join(ROOT, "tests", "golden")
 tmp = tempfile.mkdtemp()
@@ -68,4 +68,4 @@ for name, a, p in cases:
     base = res["oracle"]
     print(f"{name:28s} ll {base[0]:.10g}  lane rel {np.max(np.abs(res['lane'] - base) / np.abs(base)):.2e}"
           f"  tab rel {np.max(np.abs(res['tab'] - base) / np.abs(base)):.2e}"
-          f"  w2 rel {np.max(np.abs(res['w2'] - base) / np.abs(base)):.2e}")
+          f"  wave rel {np.max(np.abs(res["wave"] - base) / np.abs(base)):.2e}")

@@ -35,15 +35,10 @@ int main(int argc, char **argv)
     (void)hipMemcpyFromSymbol(all, HIP_SYMBOL(g_stamp), sizeof all);
     const char *gnames[8] = {"prefetch+step_init", "B exp/dawson/pow", "barrier 1", "C integrals",
                              "barrier 2", "D outputs+division", "update", "barrier 3"};
-    const bool v1 = getenv("GGP_WAVE_V1") && atoi(getenv("GGP_WAVE_V1"));
-    const char *wnames1[11] = {"step_init+V+dt cache", "B exp/dawson/pow", "barrier B", "C integrals",
-                               "barrier C", "D output terms", "E butterfly", "readlane+division", "update",
-                               "ll flush (every 64)", "end-of-step barrier"};
-    // k_loglik_wave2 (ggp_wave2.h): stamps 0..10
-    const char *wnames2[11] = {"scalars+PW+monomials", "B exp/dawson", "barrier B", "C integrals",
-                               "barrier C", "D output terms", "butterfly+OUT", "barrier+finish", "barrier+update",
-                               "end step (flush/64)", "-"};
-    const char *const *wnames = v1 ? wnames1 : wnames2;
+    // k_loglik_wave (ggp_wave.h): stamps 0..10
+    const char *wnames[11] = {"scalars+monomials", "B exp/dawson", "barrier B", "C integrals",
+                              "barrier C", "D output terms", "butterfly+OUT", "finish+innovation", "barrier+update",
+                              "end step (flush/64)", "-"};
     for (int slot = 0; slot < 4; ++slot) {
         const unsigned long long *acc = all + 16 * slot;
         const double steps = (double)acc[15];
