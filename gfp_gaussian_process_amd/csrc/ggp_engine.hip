@@ -799,6 +799,16 @@ GGP_DEV void chain_reduce(const ChainRed &R, const int64_t seq, const int b, con
 // ------------------------------------------------------------------------------------------
 constexpr int kRowStall = 0xffffff;   // a cell never has 2^24 - 1 rows (ggp_forest_create checks)
 
+// k_loglik_wave's workgroups are one wave: the LDS executes a wave's DS instructions in issue
+// order, so a write is seen by every later read of the same wave without waiting for it (no
+// lgkmcnt(0) drain, which __syncthreads' workgroup fence would emit); this keeps the compiler from
+// moving LDS accesses across the point and costs no instruction.
+GGP_DEV void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
@@ -819,9 +829,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     {
         const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
         lds[W::L_MONO + lane] = W::lane_kappa(lane, ou);   // the 33 kappas, one per lane (MONO is free here)
-        __syncthreads();
+        wave_sync();
         L = W::lane_from(lane, LC, ou, lds + W::L_MONO);
-        __syncthreads();
+        wave_sync();
     }
     const double var_x = p[7], var_g = p[8], var_dx = p[9], var_dg = p[10], b = p[6];
     if (lane == 0) {
@@ -858,11 +868,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                                          (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
         if (dbits != dt_cached) {   // lane constants and kernel arguments only: no OU values live in the loop
             if (lane < 7) lds[lane < 6 ? W::L_X + ggp::XS_bt + lane : W::L_XPGQ] = exp(L.c_sv * dt);
-            __syncthreads();
+            wave_sync();
             if (lane < ggp::kNDerived)
                 lds[W::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W::L_X, p[1], dt);
             if (lane == 0) lds[W::L_V + ggp::V_T] = dt;
-            __syncthreads();
+            wave_sync();
             dt_cached = dbits;
         }
         const double *po = lds + W::L_POST;
@@ -876,11 +886,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             lds[L.b_dst] = v;
         }
         GGP_STAMP(2);
-        __syncthreads();
+        wave_sync();
         GGP_STAMP(3);
         lds[L.i_dst] = W::stageC(S, L, lds);   // stage C: one integral per lane
         GGP_STAMP(4);
-        __syncthreads();
+        wave_sync();
         GGP_STAMP(5);
         double acc = W::stageD(L, lds);   // stage D: the lane's output terms
         GGP_STAMP(6);
@@ -894,7 +904,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         lds[L.d_out] = acc;
         GGP_STAMP(7);
-        __syncthreads();
+        wave_sync();
     };
     for (int i = i_lo; i < i_hi; ++i) {
         const int c = cells[i];
@@ -955,7 +965,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (lane == 0) lds[W::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
         };
         load_chunk(r0);
-        __syncthreads();
+        wave_sync();
         double cl = 0.0;
         int nan_row = kNanNone;
         int slot = 0;                    // row - chunk base
@@ -975,13 +985,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (slot == 64 || !live) {
                 const int done = nrows - left;
                 const int64_t base = done - slot;
-                __syncthreads();
+                wave_sync();
                 if (lane < slot) {
                     const double s00 = lds[W::L_RS0 + lane], s01 = lds[W::L_RS1 + lane], s11 = lds[W::L_RS2 + lane];
                     lds[W::L_RT + lane] = W::ll_quad(lds[W::L_RX0 + lane], lds[W::L_RX1 + lane], s00, s01, s11) -
                                            0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - F.two_log_2pi;
                 }
-                __syncthreads();
+                wave_sync();
                 bool ok = true;
                 if (lane == 0) {
                     // the terms in row order (the reference's running sum), unrolled for a full chunk;
@@ -1011,7 +1021,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 if (live) load_chunk(r0 + done);
             }
             GGP_STAMP(10);
-            __syncthreads();   // the LDS slots are rewritten by the next step
+            wave_sync();   // the LDS slots are rewritten by the next step
             return true;
         };
         GGP_PSTAMP(4);
@@ -1076,8 +1086,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     lds[W::L_RS2 + slot] = v.S11;
                 }
                 GGP_STAMP(8);
-                __syncthreads();
-                const double up = W::upost(L, lds, v);
+                wave_sync();
+                const W::UOps q = W::upost_load(L, lds);
+                W::sched_fence();   // the operand reads issued before the update's arithmetic
+                const double up = W::upost(q, fv, v);
                 lds[L.u_post] = up;
                 lds[L.u_v] = up - L.u_vshift;
             }
@@ -1087,7 +1099,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (!end_step()) break;
         }
         GGP_PSTAMP(6);
-        __syncthreads();
+        wave_sync();
         // the cell's results; its state from lanes 0-19 (one coalesced store), agent-coherent with
         // the flag after it when a second daughter waits for it
         if (lane == 0) {
@@ -1106,7 +1118,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (lane == 0) __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         GGP_PSTAMP(7);
-        __syncthreads();   // the LDS rows and ring are the next cell's
+        wave_sync();   // the LDS rows and ring are the next cell's
     }
     GGP_STAMP_FLUSH();
     GGP_PSTAMP_FLUSH();
@@ -1907,7 +1919,7 @@ __global__ __launch_bounds__(64) void k_debug_dawson(const double *__restrict__ 
         // and, where needed, the rare branches -- the same instructions the kernel runs
         W::WStep S{};
         S.t = 0.0; S.a = 1.0; S.two_a = 2.0; S.four_a = 4.0; S.four_aa = 4.0; S.two_sa = 1.0; S.m2sa = -1.0;
-        S.r_two_sa = 1.0; S.r_four_a = 0.25; S.bbl = v; S.Cxl = 0.0; S.bx = 0.0; S.Cxx = 0.0;
+        S.r_two_sa = 1.0; S.r_two_sa0 = 1.0; S.r_four_a = 0.25; S.bbl = v; S.Cxl = 0.0; S.bx = 0.0; S.Cxx = 0.0;
         W::Lane L{};
         L.b_tau = 0.0; L.b_km = 1.0; L.b_gqks = 0.0; L.b_m1 = 1.0; L.b_m2 = 0.5; L.b_kc = 0.0;
         L.b_mult = GGP_SPI2; L.b_isE = 0; L.b_isA = 0; L.b_isD = 1; L.b_exmask = 0;
@@ -2077,7 +2089,7 @@ struct Shard {
     unsigned *d_cell_done = nullptr;
     unsigned epoch = 0;
     int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
-    unsigned spin_max = 1u << 24;      // GGP_CHAIN_SPIN_MAX: polls of a waiting second daughter (~20 s)
+    unsigned spin_max = kChainSpinMax; // GGP_CHAIN_SPIN_MAX: polls of a waiting second daughter
     int32_t *d_path_cells = nullptr, *d_path_seq = nullptr;   // path launch: cells, [n_paths + 1] starts
     int64_t n_paths = 0;               // 0: level launches
     // path launch's in-launch reduction (ChainRed): path -> block, paths per block, the blocks'

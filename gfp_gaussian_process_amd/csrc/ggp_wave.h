@@ -57,6 +57,7 @@ constexpr double kKs[6] = {0., -1., 0., -1., 1., 1.};
 // makes the quotient independent of an ulp in them).
 struct WStep {
     double t, a, two_a, four_a, four_aa, two_sa, m2sa, r_two_sa, r_four_a, bbl, Cxl, bx, Cxx;
+    double r_two_sa0;   // the unrefined seed 0.5 rsq(a) of r_two_sa (stage B's table row only)
 };
 
 GGP_DEV WStep wstep(const double *m, const double *C, const double t, const double b)
@@ -71,6 +72,7 @@ GGP_DEV WStep wstep(const double *m, const double *C, const double t, const doub
     const double r = 1.0 / sqrt(a);
 #endif
     double h = 0.5 * r, s = a * r;
+    S.r_two_sa0 = h;
     const double e = __builtin_fma(-h, s, 0.5);
     s = __builtin_fma(s, e, s);
     h = __builtin_fma(h, e, h);
@@ -568,6 +570,28 @@ GGP_DEV double rcp1(const double d)
 #endif
 }
 
+// 1/d from v_rcp_f64 alone (a seed: a few 1e-8 relative)
+GGP_DEV double rcp0(const double d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcp(d);
+#else
+    return 1.0 / d;
+#endif
+}
+
+// 1/d: v_rcp_f64 and two Newton steps (within an ulp: the update's 1/det)
+GGP_DEV double rcp2(const double d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(d);
+    r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+    return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+#else
+    return 1.0 / d;
+#endif
+}
+
 GGP_DEV int mul24(const int a, const int b)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -627,34 +651,40 @@ GGP_DEV void sched_fence()
 
 GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
 {
-    // the Dawson argument and interval first, so the table row's six 128-bit LDS reads are in
-    // flight while the exponential's argument and reduction are formed (exp lanes read the exp row)
+    // The Dawson interval first, from the unrefined seeds (v_rsq, v_rcp: ~2^-26 relative each),
+    // so the table row's six 128-bit LDS reads are in flight while z, the Chebyshev variable and
+    // the exponential's argument and reduction are formed (exp lanes read the exp row).  The seed
+    // quotient is biased up by 2^-22 (more than the seeds' error): k is floor(y100) -- on an
+    // interval boundary too (x = 24: y100 = 4) -- or, for y100 within 2.4e-5 below the next
+    // integer, that integer, where td lies within 5e-5 below -1 (the row's polynomial holds there).
     const double ti = S.t * L.b_tau;
     const double B = wave::pin(__builtin_fma(S.Cxl, L.b_km, S.bbl) + L.b_gqks);
-    const double z = rdiv(B + S.two_a * ti, S.two_sa, S.r_two_sa);
-    const double ax = fabs(z);
-    // y100 = 100 / (1 + |z|) to the correctly rounded quotient (frcp seed, Markstein step): near
-    // small |z| an ulp of y100 is tens of ulp of the value (dx/dy ~ 1e-2, x ~ 0.05)
-    const double d1 = 1.0 + ax;
-    const double y100 = rdiv(100.0, d1, frcp(d1));
-    const int k = min(cvt_i32(y100), GGP_DAWSON_NINT - 1);
+    const double xz = B + S.two_a * ti;
+    const double ya = (100.0 * (1.0 + 0x1p-22)) * rcp0(1.0 + fabs(xz * S.r_two_sa0));
+    const int k = min(cvt_i32(ya), GGP_DAWSON_NINT - 1);
     const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
     const double *A = lds + L_TAB + row;
     double a[kTabRow];
 #pragma unroll
     for (int i = 0; i < kTabRow; ++i) a[i] = A[i];
     sched_fence();
+    const double z = rdiv(xz, S.two_sa, S.r_two_sa);
+    const double ax = fabs(z);
+    // td = 2 y100 - (2k + 1) as (200 - (2k + 1) d1) / d1: the numerator by one fma (exact before
+    // its rounding), so td is within ~2 ulp of itself, not of y100 (near small |z| an ulp of y100
+    // is tens of ulp of the value: dx/dy ~ 1e-2, x ~ 0.05)
+    const double d1 = 1.0 + ax;
+    const double td = __builtin_fma(-(double)(2 * k + 1), d1, 200.0) * rcp1(d1);
     const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
     const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
     const double argA = wave::pin(ti * (B + S.a * ti));
     const double argE = wave::pin(n + c + z * z);
     const double argZ = wave::pin(S.a * (ti * ti) + B * ti + c);
     const double arg = L.b_isE ? argE : L.b_isA ? argA : argZ;
-    // exp reduction (exp_ocml); Dawson: the Chebyshev variable of interval k
+    // exp reduction (exp_ocml)
     const double dn = __builtin_rint(arg * 0x1.71547652b82fep+0);
     double r = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, arg);
     r = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, r);
-    const double td = __builtin_fma(2.0, y100, -(double)(2 * k + 1));
     const double tv = L.b_isD ? td : r;
     double h = __builtin_fma(a[0], tv, a[1]);
 #pragma unroll
@@ -666,7 +696,9 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     o.v = v;
     o.arg = arg;
     o.z = z;
-    const bool rare_d = (y100 >= (double)GGP_DAWSON_NINT) | (ax > 45.0);
+    // Taylor (y100 >= 97) flagged from the seed with a margin: stageB_rare decides on the exact
+    // quotient and returns the table value when neither branch applies
+    const bool rare_d = (ya >= (double)GGP_DAWSON_NINT - 0.01) | (ax > 45.0);
     const bool rare_e = !(fabs(arg) < kExpFastMax);
     o.rare = ((L.b_isD != 0) & rare_d) | ((L.b_isD == 0) & rare_e);
     return o;
@@ -725,9 +757,10 @@ GGP_DEV double finish(const Lane &L, const double *lds, const int slot)
 }
 
 struct UInnov {
-    double S00, S01, S11, si00, si01, si11;
+    double S00, S01, S11, invdet;
 };
-// ggp_wave.h innovation from the prior's C00, C01, C11 and m1 (the same expressions)
+// the innovation covariance S from the prior's C00, C01, C11 and m1 (ggp_wave.h innovation's
+// expressions) and 1/det S by rcp2 (its Newton steps run while the update's operands load)
 GGP_DEV UInnov uinnov(const double m1, const double C00, const double C01, const double C11, const double var_x,
                       const double var_g, const int scaled, const double fp_auto)
 {
@@ -737,23 +770,33 @@ GGP_DEV UInnov uinnov(const double m1, const double C00, const double C01, const
     v.S01 = C01 + 0.0;
     v.S11 = C11 + d11;
     const double det = v.S00 * v.S11 - v.S01 * v.S01;
-    const double invdet = 1.0 / det;
-    v.si00 = v.S11 * invdet;
-    v.si01 = -v.S01 * invdet;
-    v.si11 = v.S00 * invdet;
+    v.invdet = rcp2(det);
     return v;
 }
 
-// posterior entry of lane e (ggp_wave.h posterior: C_ij - fma(KS1_i, C1j, KS0_i C0j);
-// m_i + fma(KS1_i, x1, KS0_i x0) == m_i - fma(KS1_i, -x1, KS0_i (-x0)) bitwise)
-GGP_DEV double upost(const Lane &L, const double *lds, const UInnov &v)
+// the update's operands of lane e: u = C[0][i], v = C[1][i] and w, z = C[0][j], C[1][j] (a
+// covariance) or -x0, -x1 (a mean); its own prior entry c is the lane's finish value
+struct UOps {
+    double u, vv, w, z;
+};
+GGP_DEV UOps upost_load(const Lane &L, const double *lds)
 {
-    const double u = lds[L.u_ub], vv = lds[L.u_ub + 4];
-    const double w = lds[L.u_wb], z = lds[L.u_wb + 4];
-    const double c = lds[L.u_c];
-    const double KS0 = __builtin_fma(vv, v.si01, u * v.si00);
-    const double KS1 = __builtin_fma(vv, v.si11, u * v.si01);
-    return c - __builtin_fma(KS1, z, KS0 * w);
+    UOps q;
+    q.u = lds[L.u_ub];
+    q.vv = lds[L.u_ub + 4];
+    q.w = lds[L.u_wb];
+    q.z = lds[L.u_wb + 4];
+    return q;
+}
+
+// posterior entry of lane e, C_ij - (KS1_i C1j + KS0_i C0j) with K S^-1 = K adj(S) / det S: the
+// adjugate products first, the reciprocal determinant applied once by the last fma (ggp_wave.h
+// posterior's terms; m_i + (KS1_i x1 + KS0_i x0) == m_i - (KS1_i (-x1) + KS0_i (-x0)))
+GGP_DEV double upost(const UOps &q, const double c, const UInnov &v)
+{
+    const double A0 = __builtin_fma(q.vv, -v.S01, q.u * v.S11);
+    const double A1 = __builtin_fma(q.vv, v.S00, q.u * -v.S01);
+    return __builtin_fma(-__builtin_fma(A1, q.z, A0 * q.w), v.invdet, c);
 }
 
 #ifdef GGP_HOST_SIM
@@ -828,7 +871,7 @@ struct HostWave {
         const double *st = lds + L_ST;
         const UInnov v = uinnov(st[1], st[4], st[5], st[9], var_x, var_g, scaled, fp_auto);
         double u[64];
-        for (int l = 0; l < 64; ++l) u[l] = upost(L[l], lds, v);
+        for (int l = 0; l < 64; ++l) u[l] = upost(upost_load(L[l], lds), f[l], v);
         for (int l = 0; l < 64; ++l) {
             lds[L[l].u_post] = u[l];
             lds[L[l].u_v] = u[l] - L[l].u_vshift;

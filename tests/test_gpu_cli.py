@@ -7,6 +7,7 @@ with 6 significant digits by the reference's writer, so they are compared after 
 test_gpu_parity.py).  The -m trajectory is compared with the same Nelder-Mead restatement
 driven by the oracle objective.
 """
+import math
 import os
 import subprocess
 
@@ -247,3 +248,104 @@ def test_cli_sparse_joints_rebuild_the_dense_file(tmp_path, example_paths):
     out = tmp_path / "rebuilt.csv"
     J.sparse_to_dense(str(sp), str(tmp_path / "sparse" / "small_f_b_prediction.csv"), str(out))
     assert out.read_bytes() == dense
+
+
+def test_cli_two_segments_matches_oracle(tmp_path, example_paths):
+    """Two segments (segment_col) with two -b files through -e -m -s -p in one CLI run
+    (main.cpp:402-443).  -e, -m and -s run per segment on get_segment copies (moma_input.h:
+    580-620: a cell keeps its segment's rows; a parent without rows there leaves a new root),
+    with _segment<i> file names (get_segment_file_number); -p runs the whole forest with each
+    row's segment parameters, after -m has set the final values (run_minimization takes the
+    parameter set by reference).  Checked against the oracle: -e and the -s samples (each on the
+    carried state of the previous one) at 1e-9, the -m iteration log against the Nelder-Mead
+    restatement driven by the oracle objective at 1e-9, and -p (6 significant digits printed)
+    at 1e-4 of the standard deviations with the restatement's final parameters."""
+    import glob
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as Opt
+    from oracle import oracle as O
+    hf0 = g.HostForest.synthetic(4, 60)   # per tree: a root (t 0-29) and two daughters (t 30-44)
+    a = hf0.a
+    ro, par = a["row_offset"], a["parent"]
+    csv = tmp_path / "small.csv"
+    with open(csv, "w") as f:
+        f.write(",cell_id,time_min,parent_id,lane,length,gfp,seg\n")
+        k = 0
+        for c in range(hf0.n_cells):
+            pid = int(par[c]) + 11 if par[c] >= 0 else 7
+            for r in range(ro[c], ro[c + 1]):
+                t = float(a["time"][r])
+                seg = 1 if t >= 20.0 else 0        # roots split inside the cell, daughters all in 1
+                f.write(f"{k},{c + 11},{t!r},{pid},1,{math.exp(float(a['log_length'][r]))!r},"
+                        f"{float(a['fp'][r])!r},{seg}\n")
+                k += 1
+    cfg = tmp_path / "cfg.txt"
+    cfg.write_text(open(example_paths["config"]).read() + "\nsegment_col = seg\n")
+    bound = "6.0E-01, 1.0E-01, 4.0E-01, 1.3E+00"
+    pf0 = _param_file(tmp_path / "p0.txt", {8: bound})
+    pf1 = _param_file(tmp_path / "p1.txt", {0: repr(INIT[0] * 1.1), 8: bound})
+    out = tmp_path / "o"
+    stdout = _run(["-i", str(csv), "-b", f"{pf0} {pf1}", "-c", str(cfg), "-e", "-m", "-t", "1e-4", "-s", "-p",
+                   "-o", str(out)], tmp_path)
+    ds = g.Dataset.read(str(csv), g.CSVConfig.load(str(cfg)))
+    assert ds.segment_indices() == [0, 1]
+    segs = [g.HostForest.build(ds, s) for s in (0, 1)]
+    assert segs[1].a["parent"].tolist().count(-1) == 4    # the split roots stay parents in segment 1
+    assert segs[0].n_cells == 4 and segs[1].n_cells == 12
+    finals = []
+    for i, (pf, hs) in enumerate(zip((pf0, pf1), segs)):
+        P = g.ParameterSet.load(pf)
+        p_init = np.array(P.init)
+        # -e: fresh copy, initial values
+        ll = float(stdout.split(f"segment {i}: total log likelihood = ")[1].split()[0])
+        ref = O.OracleForest(hs.a).total_likelihood(p_init)[0]
+        assert abs(ll - ref) / abs(ref) < 1e-9, (i, ll, ref)
+        # -m: the iteration log follows the restatement's steps on a fresh copy
+        of = O.OracleForest(hs.a)
+        seen = []
+
+        def objective(p, of=of, seen=seen):
+            v = of.total_likelihood(p)[0]
+            seen.append((np.array(p), v))
+            return v
+
+        x, llmax, rc = Opt.minimize_wrapper(objective, P, tolerance=1e-4, search_space="log")
+        finals.append(x)
+        it = glob.glob(str(out / f"small_segment{i}_*_iterations.csv"))
+        assert len(it) == 1, it
+        rows = _ll_table(it[0])
+        n = min(len(rows), len(seen))
+        assert n >= 5 and len(rows) >= len(seen) - 1
+        for k in range(n):
+            assert np.allclose(rows[k][1:12], seen[k][0], rtol=1e-9), (i, k)
+            assert abs(rows[k][12] - seen[k][1]) / abs(seen[k][1]) < 1e-9, (i, k)
+        fin = open(it[0].replace("_iterations.csv", "_final.csv")).read()
+        assert abs(float(fin.split("total_log_likelihoood,")[1].split()[0]) - llmax) / abs(llmax) < 1e-8
+        assert f"n_data_points, {hs.n_rows}" in fin
+        # -s: after -m (the scanned parameter replaces its final value), a fresh copy, chained
+        rows = _ll_table(str(out / f"small_segment{i}_scan_var_g.csv"))
+        samples = Opt.arange(0.4, 1.3, 0.1)
+        assert len(rows) == len(samples)
+        of = O.OracleForest(hs.a)
+        for k, (row, v) in enumerate(zip(rows, samples)):
+            p = x.copy()
+            p[8] = v
+            ref = of.total_likelihood(p)[0]
+            assert row[9] == v and abs(row[-1] - ref) / abs(ref) < 1e-9, (i, k, row[-1], ref)
+    # -p: the whole forest, row segment -> that segment's final parameters
+    pred = glob.glob(str(out / "small*_prediction.csv"))
+    assert len(pred) == 1, pred
+    text = open(pred[0]).read()
+    body = text.split("\ncell_id,parent_id,time,log_length,fp,")[1]
+    lines = body.strip().splitlines()[1:]
+    hf = g.HostForest.build(ds, -1)
+    assert hf.a["segment"].tolist() == [1 if t >= 20.0 else 0 for t in hf.a["time"]]
+    _, _, comb = O.OracleForest(hf.a).predict(np.stack(finals))
+    got = np.array([[float(v) for v in ln.split(",")[5:]] for ln in lines])
+    assert got.shape == (hf.n_rows, 14)
+    iu = np.triu_indices(4)
+    ref_m, ref_c = comb[:, :4], comb[:, 4:].reshape(-1, 4, 4)
+    sd = np.sqrt(np.abs(np.einsum("nii->ni", ref_c)))
+    em = np.max(np.abs(got[:, :4] - ref_m) / (np.abs(ref_m) + sd))
+    ec = np.max(np.abs(got[:, 4:] - ref_c[:, iu[0], iu[1]]) / (sd[:, iu[0]] * sd[:, iu[1]]))
+    assert em < 1e-4 and ec < 1e-4, (em, ec)

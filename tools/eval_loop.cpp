@@ -32,6 +32,27 @@ int main(int argc, char **argv)
     const auto t1 = std::chrono::steady_clock::now();
     printf("trees=%lld kernel=%d: %.4f ms/eval (C++ loop) ll=%.17g\n", (long long)trees, kernel,
            std::chrono::duration<double, std::milli>(t1 - t0).count() / reps, ll);
+    // the host's own share: time inside ggp_total_loglik_async (enqueue) and inside
+    // ggp_loglik_result (wait), and the kernel's device time (events)
+    double t_enq = 0, t_wait = 0;
+    float ms[16];
+    int64_t rows[16];
+    int32_t kk[16], nk = 0;
+    ggp_last_launch_profile(f, ms, rows, kk, 16, &nk);   // switches the events on
+    double t_dev = 0;
+    for (int k = 0; k < reps; ++k) {
+        const auto a = std::chrono::steady_clock::now();
+        ggp_total_loglik_async(f, P);
+        const auto b = std::chrono::steady_clock::now();
+        ggp_loglik_result(f, &ll, &nc, &nr);
+        const auto c = std::chrono::steady_clock::now();
+        t_enq += std::chrono::duration<double, std::micro>(b - a).count();
+        t_wait += std::chrono::duration<double, std::micro>(c - b).count();
+        if (ggp_last_launch_profile(f, ms, rows, kk, 16, &nk) == GGP_OK)
+            for (int i = 0; i < nk; ++i) t_dev += 1e3 * ms[i];
+    }
+    printf("  enqueue %.2f us, wait %.2f us, device (events) %.2f us per evaluation (profiled calls)\n", t_enq / reps,
+           t_wait / reps, t_dev / reps);
     ggp_forest_destroy(f);
     ggp_host_forest_free(hf);
     return 0;

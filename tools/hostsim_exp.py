@@ -68,4 +68,4 @@ for name, a, p in cases:
     base = res["oracle"]
     print(f"{name:28s} ll {base[0]:.10g}  lane rel {np.max(np.abs(res['lane'] - base) / np.abs(base)):.2e}"
           f"  tab rel {np.max(np.abs(res['tab'] - base) / np.abs(base)):.2e}"
-          f"  wave rel {np.max(np.abs(res["wave"] - base) / np.abs(base)):.2e}")
+          f"  wave rel {np.max(np.abs(res['wave'] - base) / np.abs(base)):.2e}")
