@@ -59,7 +59,11 @@ def build(verbose: bool = False, force: bool = False) -> dict:
             eng_deps.append(p)
     eng = os.path.join(LIB, "libggp.so")
     if force or not _newer(eng, eng_deps):
-        _run([HIPCC, *HIP_FLAGS, "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src, "-ldl"], verbose)
+        # -cuid: a fixed offload compilation-unit id (clang derives it from the source path by
+        # default), so the same sources give the same bytes in any checkout -- the PMC stamps in
+        # profiles/ are keyed on this library's sha256 (bench.py)
+        _run([HIPCC, *HIP_FLAGS, "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src, "-ldl"],
+             verbose)
     out["libggp"] = eng
     # --- host ingest ---
     host_src = os.path.join(CSRC, "host", "ggp_host.cpp")
@@ -74,7 +78,8 @@ def build(verbose: bool = False, force: bool = False) -> dict:
     cli_src = os.path.join(CSRC, "host", "ggp_cli.cpp")
     if os.path.exists(cli_src):
         cli = os.path.join(LIB, "ggp")
-        deps = [cli_src, host_src, os.path.join(INC, "ggp.h"), os.path.join(INC, "ggp_host.h")]
+        deps = [cli_src, host_src, os.path.join(INC, "ggp.h"), os.path.join(INC, "ggp_host.h"),
+                os.path.join(CSRC, "host", "ggp_text.h")]
         nm = os.path.join(CSRC, "host", "ggp_nelder_mead.h")
         if os.path.exists(nm):
             deps.append(nm)

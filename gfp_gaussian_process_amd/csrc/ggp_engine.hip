@@ -468,6 +468,8 @@ __device__ unsigned long long g_stamp[64];   // [16 * log2(cells per wave) + sta
         st_prev = st_now;                                                                  \
     } while (0)
 #define GGP_STAMP_STEP() ++st_steps
+// restart the interval clock without charging a stage (the cell's first step is not a steady one)
+#define GGP_STAMP_RESET() asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory")
 // phases of a launch (wave schedule): everything issued so far completes, then the stamp
 __device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], [.][8] = launches
 #define GGP_PSTAMP_DECL unsigned long long pst[8] = {0}
@@ -492,6 +494,7 @@ __device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], 
 #define GGP_STAMP_DECL
 #define GGP_STAMP(k) asm volatile(";@mark " #k)
 #define GGP_STAMP_STEP()
+#define GGP_STAMP_RESET()
 #define GGP_STAMP_FLUSH()
 #define GGP_PSTAMP_DECL
 #define GGP_PSTAMP(k) asm volatile(";@pmark " #k)
@@ -500,6 +503,7 @@ __device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], 
 #define GGP_STAMP_DECL
 #define GGP_STAMP(k)
 #define GGP_STAMP_STEP()
+#define GGP_STAMP_RESET()
 #define GGP_STAMP_FLUSH()
 #define GGP_PSTAMP_DECL
 #define GGP_PSTAMP(k)
@@ -1059,6 +1063,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             pending = left > 1;
             if (pending) dt = t_next - t_cur;
             t_cur = t_next;
+            GGP_STAMP_RESET();
             if (!end_step()) live = false;
         }
         GGP_PSTAMP(5);

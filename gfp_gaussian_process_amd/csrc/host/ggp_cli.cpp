@@ -33,6 +33,7 @@
 #include "ggp.h"
 #include "ggp_host.h"
 #include "ggp_nelder_mead.h"
+#include "ggp_text.h"
 
 namespace {
 
@@ -494,16 +495,6 @@ void run_bound_1dscan(Objective &o, const Params &P, std::map<std::string, std::
 }
 
 // ---- -p (main.cpp:117-146, predictions.h:522-601) -----------------------------------------
-void output_upper_triangle(std::ostream &file, const double *C)
-{
-    for (int m = 0; m < 4; ++m)
-        for (int n = 0; n < 4; ++n)
-            if (m <= n) {
-                if (n + m > 0) file << ",";
-                file << C[4 * m + n];
-            }
-}
-
 void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::string, std::string> &args)
 {
     g_log << "-> prediction" << "\n";
@@ -523,7 +514,6 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
     const int64_t span = (int64_t)1 << 18;
     std::vector<double> comb((size_t)std::min<int64_t>(span, std::max<int64_t>(nr, 1)) * 20);
-    int64_t b_lo = 0, b_hi = 0;   // rows held in comb
     if (args.count("predict_binary")) {
         // additive: the same 4 means + 10 upper-triangle covariances per row as the CSV, in input
         // order, as raw doubles: "GGPP0001", int64 n_rows, then [n_rows x 14] f64
@@ -562,26 +552,39 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     file << "\ncell_id,parent_id,time,log_length,fp,";
     file << "mean_x,mean_g,mean_l,mean_q," << "cov_xx,cov_xg,cov_xl,cov_xq," << "cov_gg,cov_gl,cov_gq,"
          << "cov_ll,cov_lq," << "cov_qq\n";
-    for (int64_t c = 0; c < nc; ++c) {
-        for (int64_t r = F.desc.row_offset[c]; r < F.desc.row_offset[c + 1]; ++r) {
-            file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
-                 << F.desc.time[r] << "," << F.desc.log_length[r] << "," << F.desc.fp[r] << ",";
-            if (r >= b_hi) {
-                b_lo = r;
-                b_hi = std::min(nr, r + span);
-                const int rr = ggp_predict_rows(F.gpu, b_lo, b_hi, comb.data());
-                if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
+    // one line per row, cells in input order and rows in time order: rows 0..nr-1 (row_offset is
+    // monotone).  Each fetched span is cut into blocks of rows formatted on every core
+    // (ggp_text.h: the same bytes as the reference's `<<`), written in order.
+    const int64_t *ro = F.desc.row_offset;
+    const int64_t blk = 4096;
+    for (int64_t lo = 0; lo < nr; lo += span) {
+        const int64_t hi = std::min(nr, lo + span);
+        const int rr = ggp_predict_rows(F.gpu, lo, hi, comb.data());
+        if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
+        ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &out) {
+            const int64_t r0 = lo + b * blk, r1 = std::min(hi, r0 + blk);
+            int64_t c = std::upper_bound(ro, ro + nc + 1, r0) - ro - 1;   // the cell of row r0
+            for (int64_t r = r0; r < r1; ++r) {
+                while (r >= ro[c + 1]) ++c;
+                out += ggp_host_forest_cell_id(F.host, c);
+                out.push_back(',');
+                out += ggp_host_forest_parent_id(F.host, c);
+                out.push_back(',');
+                ggp_text::put_num(out, F.desc.time[r]);
+                out.push_back(',');
+                ggp_text::put_num(out, F.desc.log_length[r]);
+                out.push_back(',');
+                ggp_text::put_num(out, F.desc.fp[r]);
+                out.push_back(',');
+                const double *sr = &comb[(size_t)(r - lo) * 20];
+                ggp_text::put_values(out, sr, 4);   // the 4 means
+                out.push_back(',');
+                ggp_text::put_upper(out, sr + 4, 4);   // output_upper_triangle
+                out.push_back('\n');
             }
-            const double *s = &comb[(size_t)(r - b_lo) * 20];
-            for (int k = 0; k < 4; ++k) {
-                if (k > 0) file << ",";
-                file << s[k];
-            }
-            file << ",";
-            output_upper_triangle(file, s + 4);
-            file << "\n";
-        }
+        });
     }
+    if (!file) throw std::runtime_error("write failed: " + outfile);
 }
 
 // ---- -j (main.cpp:150-186; correlation_tree.h:9-23, 96-126, 588-648, 786-791) -------------
@@ -684,7 +687,6 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
     int64_t cap = (int64_t)1 << 14, chunk = 4096;
     std::vector<int64_t> idx((size_t)(2 * cap));
     std::vector<double> val((size_t)(72 * cap));
-    std::map<int64_t, int64_t> cols;                 // column -> joint, the last add wins
     int64_t logged = -1;
     for (int64_t lo = 0; lo < nr;) {
         const int64_t hi = std::min(nr, lo + chunk);
@@ -702,54 +704,83 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             }
             continue;
         }
-        int64_t k = 0;
-        for (int64_t s = lo; s < hi; ++s) {          // sc_joint_distributions: one line per start row
-            const int64_t c = row_cell[(size_t)s];
-            if (c != logged) {
-                g_log << "-> cell: " << c << "\n";
-                logged = c;
+        // the joints of start row s are idx/val[first[s - lo], first[s - lo + 1]) (the engine emits
+        // them by start row, in add order)
+        std::vector<int64_t> first((size_t)(hi - lo + 1));
+        {
+            int64_t k = 0;
+            for (int64_t s = lo; s < hi; ++s) {
+                first[(size_t)(s - lo)] = k;
+                while (k < n_out && idx[(size_t)(2 * k)] == s) ++k;
+                const int64_t c = row_cell[(size_t)s];
+                if (c != logged) {
+                    g_log << "-> cell: " << c << "\n";
+                    logged = c;
+                }
             }
-            cols.clear();
-            for (; k < n_out && idx[(size_t)(2 * k)] == s; ++k) {
-                const int64_t tgt = idx[(size_t)(2 * k + 1)];
+            first[(size_t)(hi - lo)] = k;
+            if (k != n_out) throw std::runtime_error("ggp_joints: joints out of start-row order");
+        }
+        // sc_joint_distributions: one line per start row (dense), or one per (start row, column)
+        // (sparse); blocks of start rows formatted on every core, written in order (ggp_text.h)
+        const int64_t sblk = sparse ? 64 : 4;
+        ggp_text::write_ordered(file, (hi - lo + sblk - 1) / sblk, [&](int64_t bi, std::string &out) {
+            std::map<int64_t, int64_t> cols;   // column -> joint, the last add wins
+            const int64_t s0 = lo + bi * sblk, s1 = std::min(hi, s0 + sblk);
+            for (int64_t s = s0; s < s1; ++s) {
+                const int64_t k0 = first[(size_t)(s - lo)], k1 = first[(size_t)(s - lo + 1)];
                 if (sparse) {   // every column the add reaches, in add order
-                    const double *j = &val[(size_t)(72 * k)];
-                    auto line = [&](int64_t col) {
-                        file << s << "," << col << ",";
-                        output_values(file, j, 8);
-                        file << ",";
-                        output_upper(file, j + 8, 8);
-                        file << "\n";
-                    };
-                    if (dup[(size_t)tgt] < 0)
-                        line(tgt);
-                    else
-                        for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) line(col);
+                    for (int64_t k = k0; k < k1; ++k) {
+                        const int64_t tgt = idx[(size_t)(2 * k + 1)];
+                        const double *j = &val[(size_t)(72 * k)];
+                        auto line = [&](int64_t col) {
+                            ggp_text::put_int(out, s);
+                            out.push_back(',');
+                            ggp_text::put_int(out, col);
+                            out.push_back(',');
+                            ggp_text::put_values(out, j, 8);
+                            out.push_back(',');
+                            ggp_text::put_upper(out, j + 8, 8);
+                            out.push_back('\n');
+                        };
+                        if (dup[(size_t)tgt] < 0)
+                            line(tgt);
+                        else
+                            for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) line(col);
+                    }
                     continue;
                 }
-                if (dup[(size_t)tgt] < 0)
-                    cols[tgt] = k;
-                else
-                    for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) cols[col] = k;
+                cols.clear();
+                for (int64_t k = k0; k < k1; ++k) {
+                    const int64_t tgt = idx[(size_t)(2 * k + 1)];
+                    if (dup[(size_t)tgt] < 0)
+                        cols[tgt] = k;
+                    else
+                        for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) cols[col] = k;
+                }
+                const int64_t c = row_cell[(size_t)s];
+                out += ggp_host_forest_cell_id(F.host, c);
+                out.push_back(',');
+                out += ggp_host_forest_parent_id(F.host, c);
+                out.push_back(',');
+                ggp_text::put_num(out, time[s]);
+                int64_t prev = 0;
+                for (const auto &e : cols) {             // Joint_vector::write
+                    out.append((size_t)(44 * (e.first - prev)), ',');
+                    const double *j = &val[(size_t)(72 * e.second)];
+                    out.push_back(',');
+                    ggp_text::put_values(out, j, 8);
+                    out.push_back(',');
+                    ggp_text::put_upper(out, j + 8, 8);
+                    prev = e.first + 1;
+                }
+                out.append((size_t)(44 * (nr - prev)), ',');
+                out.push_back('\n');
             }
-            if (sparse) continue;
-            file << ggp_host_forest_cell_id(F.host, c) << "," << ggp_host_forest_parent_id(F.host, c) << ","
-                 << time[s];
-            int64_t prev = 0;
-            for (const auto &e : cols) {             // Joint_vector::write
-                write_commas(file, 44 * (e.first - prev));
-                const double *j = &val[(size_t)(72 * e.second)];
-                file << ",";
-                output_values(file, j, 8);
-                file << ",";
-                output_upper(file, j + 8, 8);
-                prev = e.first + 1;
-            }
-            write_commas(file, 44 * (nr - prev));
-            file << "\n";
-        }
+        });
         lo = hi;
     }
+    if (!file) throw std::runtime_error("write failed: " + outfile);
 }
 
 // ---- main.cpp:148-345 arg_parser ------------------------------------------------------------

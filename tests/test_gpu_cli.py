@@ -104,6 +104,40 @@ def test_cli_predict_matches_oracle(tmp_path, example_paths, oracle_example):
     assert ids[0] == hf.ids[0] and ids[-1] == hf.ids[-1]
 
 
+def _g(x):
+    """`std::ostream << double` under the default stream state: printf's "%.6g" """
+    x = float(x)
+    if x != x:
+        return "-nan" if math.copysign(1.0, x) < 0 else "nan"
+    return "%.6g" % x
+
+
+def test_cli_prediction_text_is_the_rows_formatted(tmp_path, example_paths, oracle_example):
+    """_prediction.csv byte for byte: every row's ids, time, log_length, fp and the 14 smoothed
+    values of the same run's binary rows (-pbin, the exact doubles), formatted as the reference's
+    write_predictions_to_file formats them (predictions.h:563-602); the writer's blocks are
+    formatted on 7 threads and must come out in row order"""
+    pf = _param_file(tmp_path / "p.txt", {})
+    env = dict(os.environ, GGP_IO_THREADS="7")
+    for tag, extra in (("t", ["-p"]), ("b", ["-p", "-pbin"])):
+        r = subprocess.run([CLI, "-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], *extra,
+                            "-o", str(tmp_path / tag)], capture_output=True, text=True, timeout=600, cwd=tmp_path, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(tmp_path / "b" / "input_f_b_prediction.bin", "rb").read()
+    assert raw[:8] == b"GGPP0001"
+    n = int(np.frombuffer(raw[8:16], dtype=np.int64)[0])
+    rows = np.frombuffer(raw[16:], dtype=np.float64).reshape(n, 14)
+    hf = oracle_example
+    a = hf.a
+    cell = np.repeat(np.arange(hf.n_cells), np.diff(a["row_offset"]))
+    body = open(tmp_path / "t" / "input_f_b_prediction.csv").read().split(
+        "\ncell_id,parent_id,time,log_length,fp,mean_x,mean_g,mean_l,mean_q,cov_xx,cov_xg,cov_xl,cov_xq,"
+        "cov_gg,cov_gl,cov_gq,cov_ll,cov_lq,cov_qq\n")[1]
+    want = "".join(",".join([hf.ids[cell[r]], hf.parent_ids[cell[r]], _g(a["time"][r]), _g(a["log_length"][r]),
+                             _g(a["fp"][r]), *[_g(v) for v in rows[r]]]) + "\n" for r in range(n))
+    assert n == hf.n_rows and body == want
+
+
 def test_cli_minimize_matches_oracle_trajectory(tmp_path, example_paths, oracle_example):
     """-m, log space, two free parameters: the GPU run's iteration log follows the same
     Nelder-Mead steps as the restatement driven by the oracle objective"""
@@ -205,7 +239,9 @@ def test_cli_joints_dense_matrix(tmp_path, example_paths):
         assert set(got) == set(exp), s
         for col, v in got.items():
             ref = np.concatenate([exp[col][:8], exp[col][8:].reshape(8, 8)[iu]])
-            assert np.allclose(v, ref, rtol=1e-5, atol=0), (s, col)
+            # the same doubles (the engine is deterministic), printed as the reference's `<<`
+            # prints them (printf "%.6g")
+            assert f[3 + 44 * col: 3 + 44 * (col + 1)] == [_g(x) for x in ref], (s, col)
 
 
 def _errors(path):

@@ -173,3 +173,56 @@ def test_joints_example_subset_vs_oracle(example_paths):
         print(f"example [{lo},{hi}): {n} pairs, max err {err:.2e}, median {med:.2e}, worst event {worst:.1f} tol, "
               f"stable-pair max {float(e_st.max()):.2e}")
         assert med < 1e-6, (lo, hi, med)
+
+
+def test_joints_example_full_size(example_paths):
+    """-j over ALL 22,065 start rows of the reference's example (collect_joint_distributions,
+    correlation_tree.h:629-648), in ranges of 2,048 start rows as the CLI streams them; then the
+    first and last start row of every cell (154 walks, divisions included) from single-row calls
+    -- bitwise the full run's (range invariance) -- against the oracle with the calibrated
+    bounds of test_joints_example_subset_vs_oracle"""
+    import time
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.from_csv(example_paths["csv"], example_paths["config"], -1, "scaled", "binomial")
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    ops = [O.OracleForest(hf.a, exp_ulp_noise=s) for s in (12345, 777, 4242)]
+    nr, ro = hf.n_rows, hf.a["row_offset"]
+    assert nr == 22065
+    sample = sorted({int(ro[c]) for c in range(hf.n_cells)} | {int(ro[c + 1]) - 1 for c in range(hf.n_cells)})
+    full, total, per_row = {}, 0, np.zeros(nr, np.int64)
+    t0 = time.perf_counter()
+    ranges = [(lo, min(nr, lo + 2048)) for lo in range(0, nr, 2048)]
+    while ranges:
+        lo, hi = ranges.pop(0)
+        try:
+            ig, vg = fg.joints(P, 1e-10, lo, hi, cap=1 << 20)
+        except g.GGPError:                      # more joints than the buffers hold: split the range
+            assert hi - lo > 1
+            ranges[:0] = [(lo, (lo + hi) // 2), ((lo + hi) // 2, hi)]
+            continue
+        total += len(ig)
+        np.add.at(per_row, ig[:, 0], 1)
+        for s in sample:
+            if lo <= s < hi:
+                m = ig[:, 0] == s
+                full[s] = (ig[m], vg[m])
+    el = time.perf_counter() - t0
+    print(f"example full: {total} joints over {nr} start rows in {el:.2f} s ({total / el:.3g} joints/s)")
+    assert total > 0 and (per_row > 0).sum() > 0.9 * nr
+    G, Ov, Nz = [], [], [[], [], []]
+    for s in sample:
+        ig, vg = fg.joints(P, 1e-10, s, s + 1, cap=1 << 16)
+        assert np.array_equal(ig, full[s][0]) and np.array_equal(vg, full[s][1]), s
+        G.append((ig, vg))
+        Ov.append(of.joints(P, 1e-10, s, s + 1, cap=1 << 16))
+        for k, op in enumerate(ops):
+            Nz[k].append(op.joints(P, 1e-10, s, s + 1, cap=1 << 16))
+
+    def cat(parts):
+        return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+    (ig, vg), (io, vo) = cat(G), cat(Ov)
+    err, med, n, worst = _compare(ig, vg, io, vo, band=100.0, noise=[cat(z) for z in Nz])
+    print(f"example full: {len(sample)} sampled start rows, {n} pairs compared, max err {err:.2e}, "
+          f"median {med:.2e}, worst event {worst:.1f} tol")
+    assert med < 1e-6, med
