@@ -512,7 +512,7 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     // the combined rows stay in HBM; the writer streams them by row ranges (bounded host memory)
     const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, nullptr);
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
-    const int64_t span = (int64_t)1 << 18;
+    const int64_t span = (int64_t)1 << 20;
     std::vector<double> comb((size_t)std::min<int64_t>(span, std::max<int64_t>(nr, 1)) * 20);
     if (args.count("predict_binary")) {
         // additive: the same 4 means + 10 upper-triangle covariances per row as the CSV, in input
@@ -561,26 +561,27 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         const int64_t hi = std::min(nr, lo + span);
         const int rr = ggp_predict_rows(F.gpu, lo, hi, comb.data());
         if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
-        ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &out) {
+        ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &buf) {
+            ggp_text::Sink out(buf);
             const int64_t r0 = lo + b * blk, r1 = std::min(hi, r0 + blk);
             int64_t c = std::upper_bound(ro, ro + nc + 1, r0) - ro - 1;   // the cell of row r0
             for (int64_t r = r0; r < r1; ++r) {
                 while (r >= ro[c + 1]) ++c;
-                out += ggp_host_forest_cell_id(F.host, c);
-                out.push_back(',');
-                out += ggp_host_forest_parent_id(F.host, c);
-                out.push_back(',');
-                ggp_text::put_num(out, F.desc.time[r]);
-                out.push_back(',');
-                ggp_text::put_num(out, F.desc.log_length[r]);
-                out.push_back(',');
-                ggp_text::put_num(out, F.desc.fp[r]);
-                out.push_back(',');
+                out.str(ggp_host_forest_cell_id(F.host, c));
+                out.ch(',');
+                out.str(ggp_host_forest_parent_id(F.host, c));
+                out.ch(',');
+                out.num(F.desc.time[r]);
+                out.ch(',');
+                out.num(F.desc.log_length[r]);
+                out.ch(',');
+                out.num(F.desc.fp[r]);
+                out.ch(',');
                 const double *sr = &comb[(size_t)(r - lo) * 20];
-                ggp_text::put_values(out, sr, 4);   // the 4 means
-                out.push_back(',');
-                ggp_text::put_upper(out, sr + 4, 4);   // output_upper_triangle
-                out.push_back('\n');
+                out.values(sr, 4);   // the 4 means
+                out.ch(',');
+                out.upper(sr + 4, 4);   // output_upper_triangle
+                out.ch('\n');
             }
         });
     }
@@ -594,23 +595,6 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
 // 44 empty fields.  Joint_vector::add stores a joint in every column whose (cell_id, time)
 // equals the target's, the last add winning.  The joints come from the GPU (ggp_joints) in
 // the reference's add order, a bounded range of start rows per call.
-void output_values(std::ostream &file, const double *v, int n)   // output_vector (predictions.h:553-560)
-{
-    for (int k = 0; k < n; ++k) {
-        if (k > 0) file << ",";
-        file << v[k];
-    }
-}
-
-void output_upper(std::ostream &file, const double *C, int n)    // output_upper_triangle (predictions.h:540-551)
-{
-    for (int m = 0; m < n; ++m)
-        for (int k = m; k < n; ++k) {
-            if (k + m > 0) file << ",";
-            file << C[n * m + k];
-        }
-}
-
 void write_commas(std::ostream &file, int64_t count)
 {
     static const std::string block(44 * 1024, ',');
@@ -724,7 +708,8 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
         // sc_joint_distributions: one line per start row (dense), or one per (start row, column)
         // (sparse); blocks of start rows formatted on every core, written in order (ggp_text.h)
         const int64_t sblk = sparse ? 64 : 4;
-        ggp_text::write_ordered(file, (hi - lo + sblk - 1) / sblk, [&](int64_t bi, std::string &out) {
+        ggp_text::write_ordered(file, (hi - lo + sblk - 1) / sblk, [&](int64_t bi, std::string &buf) {
+            ggp_text::Sink out(buf);
             std::map<int64_t, int64_t> cols;   // column -> joint, the last add wins
             const int64_t s0 = lo + bi * sblk, s1 = std::min(hi, s0 + sblk);
             for (int64_t s = s0; s < s1; ++s) {
@@ -734,14 +719,14 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
                         const int64_t tgt = idx[(size_t)(2 * k + 1)];
                         const double *j = &val[(size_t)(72 * k)];
                         auto line = [&](int64_t col) {
-                            ggp_text::put_int(out, s);
-                            out.push_back(',');
-                            ggp_text::put_int(out, col);
-                            out.push_back(',');
-                            ggp_text::put_values(out, j, 8);
-                            out.push_back(',');
-                            ggp_text::put_upper(out, j + 8, 8);
-                            out.push_back('\n');
+                            out.i64(s);
+                            out.ch(',');
+                            out.i64(col);
+                            out.ch(',');
+                            out.values(j, 8);
+                            out.ch(',');
+                            out.upper(j + 8, 8);
+                            out.ch('\n');
                         };
                         if (dup[(size_t)tgt] < 0)
                             line(tgt);
@@ -759,23 +744,23 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
                         for (int64_t col : groups[(size_t)dup[(size_t)tgt]]) cols[col] = k;
                 }
                 const int64_t c = row_cell[(size_t)s];
-                out += ggp_host_forest_cell_id(F.host, c);
-                out.push_back(',');
-                out += ggp_host_forest_parent_id(F.host, c);
-                out.push_back(',');
-                ggp_text::put_num(out, time[s]);
+                out.str(ggp_host_forest_cell_id(F.host, c));
+                out.ch(',');
+                out.str(ggp_host_forest_parent_id(F.host, c));
+                out.ch(',');
+                out.num(time[s]);
                 int64_t prev = 0;
                 for (const auto &e : cols) {             // Joint_vector::write
-                    out.append((size_t)(44 * (e.first - prev)), ',');
+                    out.fill((size_t)(44 * (e.first - prev)), ',');
                     const double *j = &val[(size_t)(72 * e.second)];
-                    out.push_back(',');
-                    ggp_text::put_values(out, j, 8);
-                    out.push_back(',');
-                    ggp_text::put_upper(out, j + 8, 8);
+                    out.ch(',');
+                    out.values(j, 8);
+                    out.ch(',');
+                    out.upper(j + 8, 8);
                     prev = e.first + 1;
                 }
-                out.append((size_t)(44 * (nr - prev)), ',');
-                out.push_back('\n');
+                out.fill((size_t)(44 * (nr - prev)), ',');
+                out.ch('\n');
             }
         });
         lo = hi;

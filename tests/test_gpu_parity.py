@@ -251,6 +251,25 @@ def test_baseline_size_properties():
     assert _rel(s, v) < 1e-12
 
 
+@pytest.mark.timeout(300)
+def test_c3_full_size_chain_vs_oracle():
+    """BASELINE configs[2]'s forest at full size (10k trees x 200 = 2e6 rows) on the default
+    (auto) schedule -- the one -m runs on it -- against the oracle: three chained evaluations
+    (carried state, SURVEY finding 0.2) with different parameters, each at the 1e-9 bar"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    c3 = g.HostForest.synthetic(10000, 200)
+    assert c3.n_rows == 2_000_000
+    fg, of = g.Forest(c3), O.OracleForest(c3.a)
+    P = CONFIGS[0][2]
+    for k, scale in enumerate((1.0, 1.1, 0.9)):
+        p = list(P)
+        p[8] *= scale                            # var_g
+        p[1] *= 2.0 - scale                      # gamma_lambda
+        vg, vo = fg.total_likelihood(p), of.total_likelihood(p)[0]
+        assert _rel(vg, vo) < REL, (k, vg, vo)
+
+
 @pytest.mark.parametrize("which", ["example", "synthetic", "ragged"])
 @pytest.mark.parametrize("other", ["group", "pair-q2", "pair-q4", "pair-q2-c32", "pair-q4-c32"])
 def test_lane_group_pair_schedules_bitwise_equal(example_forests, which, other, monkeypatch):

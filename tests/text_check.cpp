@@ -29,12 +29,29 @@ static std::vector<double> values(uint64_t seed, int64_t n)
     while ((int64_t)v.size() < n) {
         const uint64_t bits = g();
         double x;
-        switch (bits % 4) {
+        switch (bits % 7) {
         case 0: std::memcpy(&x, &bits, 8); break;                               // any bit pattern
         case 1: x = std::ldexp(u(g), (int)(g() % 120) - 60); break;              // the data's scales
         case 2: x = std::round(u(g) * 1e7) / std::pow(10.0, (double)(g() % 9)); break;   // short decimals
-        default: x = (double)(int64_t)(u(g) * 1e9); break;                       // integers
+        case 3: x = (double)(int64_t)(u(g) * 1e9); break;                       // integers
+        case 4: {   // near six-digit rounding ties: (n + 1/2) 10^k and its neighbours
+            const double t = ((double)(100000 + g() % 900000) + 0.5) * std::pow(10.0, (double)((int)(g() % 41) - 25));
+            const int s = (int)(g() % 5) - 2;
+            x = t;
+            for (int i = 0; i < (s < 0 ? -s : s); ++i) x = std::nextafter(x, s < 0 ? 0.0 : 1e308);
+            break;
         }
+        case 5: {   // decade edges: 10^k, 999999.5 10^k and neighbours
+            const int k = (int)(g() % 600) - 300;
+            const double t = (g() & 1) ? std::pow(10.0, (double)k) : 9.999995 * std::pow(10.0, (double)k);
+            const int s = (int)(g() % 7) - 3;
+            x = t;
+            for (int i = 0; i < (s < 0 ? -s : s); ++i) x = std::nextafter(x, s < 0 ? 0.0 : 1e308);
+            break;
+        }
+        default: x = std::ldexp(u(g), (int)(g() % 2100) - 1075); break;        // every binade
+        }
+        if (g() & 1) x = -x;
         v.push_back(x);
     }
     return v;

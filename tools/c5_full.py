@@ -7,7 +7,7 @@ forward/backward workspace).
      forest (16 whole-tree shards, one oracle thread each) at the 1e-9 north-star bar;
   2. -p (forward + backward + combine, outputs resident), timed;
   3. every combined row streamed back by range (what the _prediction.csv writer reads): finite,
-     and a per-column sum as a checksum; 40 trees spread over the forest against the oracle
+     and a per-column sum as a checksum; 1000 trees spread over the forest against the oracle
      smoother at PRED_TOL (tests/test_gpu_parity.py).
 
 Progress lines go to stderr; one JSON line to stdout.
@@ -92,7 +92,7 @@ def main():
 
     from oracle import oracle as O
     from test_gpu_parity import PRED_TOL, _smoother_err
-    picks = list(range(0, trees, max(1, trees // 40)))[:40]
+    picks = list(range(0, trees, max(1, trees // 1000)))[:1000]   # 1000 trees spread over the forest
     sub = hf.subset_trees(hf.roots[picks])
     ref = O.OracleForest(sub.a).predict(P)[2]
     got = np.concatenate([f.predict_rows(rows * k, rows * k + rows) for k in picks])
