@@ -27,6 +27,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -512,7 +513,9 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     // the combined rows stay in HBM; the writer streams them by row ranges (bounded host memory)
     const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, nullptr);
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
-    const int64_t span = (int64_t)1 << 20;
+    // rows per device-to-host copy (GGP_PREDICT_SPAN: a test knob; two host buffers of this many rows)
+    const char *span_env = std::getenv("GGP_PREDICT_SPAN");
+    const int64_t span = span_env && std::atoll(span_env) > 0 ? std::atoll(span_env) : (int64_t)1 << 20;
     std::vector<double> comb((size_t)std::min<int64_t>(span, std::max<int64_t>(nr, 1)) * 20);
     if (args.count("predict_binary")) {
         // additive: the same 4 means + 10 upper-triangle covariances per row as the CSV, in input
@@ -554,15 +557,24 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
          << "cov_ll,cov_lq," << "cov_qq\n";
     // one line per row, cells in input order and rows in time order: rows 0..nr-1 (row_offset is
     // monotone).  Each fetched span is cut into blocks of rows formatted on every core
-    // (ggp_text.h: the same bytes as the reference's `<<`), written in order.
+    // (ggp_text.h: the same bytes as the reference's `<<`), written in order; the next span is
+    // copied from the device meanwhile (two host buffers; one thread calls the engine at a time).
     const int64_t *ro = F.desc.row_offset;
     const int64_t blk = 4096;
-    for (int64_t lo = 0; lo < nr; lo += span) {
+    std::vector<double> comb2(comb.size());
+    std::vector<double> *buf[2] = {&comb, &comb2};
+    auto fetch = [&](int64_t lo, std::vector<double> *b) {
+        return nr > 0 ? ggp_predict_rows(F.gpu, lo, std::min(nr, lo + span), b->data()) : GGP_OK;
+    };
+    int fr = fetch(0, buf[0]);
+    for (int64_t lo = 0, k = 0; lo < nr; lo += span, ++k) {
+        if (fr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(fr));
         const int64_t hi = std::min(nr, lo + span);
-        const int rr = ggp_predict_rows(F.gpu, lo, hi, comb.data());
-        if (rr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(rr));
-        ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &buf) {
-            ggp_text::Sink out(buf);
+        const double *rows = buf[k & 1]->data();
+        std::thread next;
+        if (hi < nr) next = std::thread([&, hi, k] { fr = fetch(hi, buf[(k + 1) & 1]); });
+        ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &sbuf) {
+            ggp_text::Sink out(sbuf);
             const int64_t r0 = lo + b * blk, r1 = std::min(hi, r0 + blk);
             int64_t c = std::upper_bound(ro, ro + nc + 1, r0) - ro - 1;   // the cell of row r0
             for (int64_t r = r0; r < r1; ++r) {
@@ -577,13 +589,14 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
                 out.ch(',');
                 out.num(F.desc.fp[r]);
                 out.ch(',');
-                const double *sr = &comb[(size_t)(r - lo) * 20];
+                const double *sr = rows + (size_t)(r - lo) * 20;
                 out.values(sr, 4);   // the 4 means
                 out.ch(',');
                 out.upper(sr + 4, 4);   // output_upper_triangle
                 out.ch('\n');
             }
         });
+        if (next.joinable()) next.join();
     }
     if (!file) throw std::runtime_error("write failed: " + outfile);
 }

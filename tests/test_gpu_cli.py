@@ -116,9 +116,10 @@ def test_cli_prediction_text_is_the_rows_formatted(tmp_path, example_paths, orac
     """_prediction.csv byte for byte: every row's ids, time, log_length, fp and the 14 smoothed
     values of the same run's binary rows (-pbin, the exact doubles), formatted as the reference's
     write_predictions_to_file formats them (predictions.h:563-602); the writer's blocks are
-    formatted on 7 threads and must come out in row order"""
+    formatted on 7 threads and must come out in row order, the rows fetched from the device in
+    spans of 5,000 (the next span copied while this one is formatted)"""
     pf = _param_file(tmp_path / "p.txt", {})
-    env = dict(os.environ, GGP_IO_THREADS="7")
+    env = dict(os.environ, GGP_IO_THREADS="7", GGP_PREDICT_SPAN="5000")
     for tag, extra in (("t", ["-p"]), ("b", ["-p", "-pbin"])):
         r = subprocess.run([CLI, "-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], *extra,
                             "-o", str(tmp_path / tag)], capture_output=True, text=True, timeout=600, cwd=tmp_path, env=env)
