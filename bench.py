@@ -170,6 +170,29 @@ def example_mp(tmp: str, cpu_budget: float):
                     "wall / evaluations (an upper bound per evaluation)"}
 
 
+def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: bool = False, note: str = ""):
+    """FP64 and VALU-issue fractions of a bench leg from the PMC pass of this build
+    (profiles/fp64_counts.json, tools/fp64_summary.py kind `kind`): achieved FP64 = flops per row x
+    rows/s against the FP64 peak (per_row_useful: the lane schedule's useful flops per update
+    instead of the kernel's issued ones), and the class-weighted VALU issue cycles the rate needs
+    per SIMD against the clock.  None without counters for this build."""
+    if not cnt or not cnt.get(kind) or rows_per_s <= 0:
+        return None
+    c = cnt[kind]
+    fpr = cnt.get("useful_flops_per_update") if per_row_useful else c.get("flops_per_update")
+    if not fpr:
+        return None
+    vpu, f64pu = c.get("valu_wave_insts_per_update"), c.get("f64_wave_insts_per_update")
+    out = {"kernel_counters": kind, "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "flops_per_row": fpr,
+           "achieved": fpr * rows_per_s / 1e12, "frac": fpr * rows_per_s / 1e12 / FP64_PEAK_TFLOPS,
+           "source": "profiles/fp64_counts.json (rocprofv3 PMC of this build)", "note": note}
+    if vpu and f64pu is not None:
+        cyc = VALU_ISSUE_CYCLES * f64pu + VALU32_ISSUE_CYCLES * (vpu - f64pu)
+        out["valu_issue"] = {"valu_wave_insts_per_row": vpu, "f64_wave_insts_per_row": f64pu,
+                             "issue_cycles_per_row": cyc, "frac": cyc * rows_per_s / n_simd / CLOCK_HZ}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -270,6 +293,7 @@ def main() -> int:
     # lanes and unused task candidates included -- an issue rate, not work done
     fp64 = None
     cnt = _profile_json("fp64_counts.json", args)
+    n_simd_chip = 4 * torch.cuda.get_device_properties(local).multi_processor_count
     if cnt and dom.startswith("k_loglik_wave") and avg_ms > 0 and cnt.get("useful_flops_per_update"):
         upd_s = (d_rows / d_n) / (avg_ms * 1e-3)
         useful = cnt["useful_flops_per_update"] * upd_s / 1e12
@@ -320,6 +344,8 @@ def main() -> int:
         large = {"trees_per_gpu": args.large_trees, "rows_per_gpu": hl.n_rows,
                  "ms_per_eval": 1e3 * lel, "updates_per_s_per_gpu": hl.n_rows / lel,
                  "note": "same path, per-GPU shard of BASELINE configs[3] (C4); not the headline value"}
+        large["fp64"] = leg_fp64(cnt, "pair", hl.n_rows / lel, n_simd_chip, per_row_useful=True,
+                                 note="k_loglik_pair counters x the leg's wall rate per evaluation")
         fl.close()
 
     # ---- opt-in batched objective on the C2 forest: the 4 k^2 = 484 points of an 11-parameter
@@ -372,6 +398,13 @@ def main() -> int:
                 "combine_gbs": COMBINE_BYTES_PER_ROW * nr / (cb_ms * 1e-3) / 1e9 if cb_ms > 0 else 0.0,
                 "note": "-p forward+backward+combine per GPU shard of BASELINE configs[4] (C5), outputs "
                         "resident in HBM; rows_per_s is whole-job; not the headline value"}
+        if sm > 0:
+            pred["fp64_smooth"] = leg_fp64(cnt, "smooth", nr / (sm / reps * 1e-3), n_simd_chip,
+                                           note="forward + backward smoother kernels (one row per lane: issued "
+                                                "= the work) x the device time of the levels")
+        if cb_ms > 0:
+            pred["fp64_combine"] = leg_fp64(cnt, "combine", nr / (cb_ms * 1e-3), n_simd_chip,
+                                            note="k_combine counters x its device time")
         fp_.close()
 
     # ---- N > 1: the drop-in CLI's own multi-GPU path (-g all): ONE process, the whole job's trees

@@ -9,6 +9,8 @@ summed over the launches of a kernel and divided by the rows those launches proc
                            every task candidate, so this is issue, not useful work
   useful_flops_per_update  k_loglik_level (1024 trees, full waves): one lane runs one cell's
                            whole update -- the FP64 work the algorithm itself needs
+  pair / smooth / combine  bench.py's large_forest (k_loglik_pair) and predict legs (forward +
+                           backward smoother kernels per row, k_combine per row)
 The engine library's sha256 is recorded: bench.py uses the figures only for that same build."""
 import csv
 import glob
@@ -29,6 +31,12 @@ for fn in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             kind = "wave"
         elif "k_loglik_level" in k and "batch" not in k:
             kind = "lane"
+        elif "k_loglik_pair" in k:
+            kind = "pair"
+        elif "k_fwd_" in k or "k_bwd_" in k:
+            kind = "smooth"
+        elif "k_combine" in k:
+            kind = "combine"
         else:
             continue
         acc[kind][row["Counter_Name"]] += float(row["Counter_Value"])
@@ -38,6 +46,8 @@ res = {"engine_sha256": hashlib.sha256(open(os.path.join(ROOT, "gfp_gaussian_pro
                                             "rb").read()).hexdigest(),
        "source": "rocprofv3 --pmc SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 SQ_INSTS_VALU SQ_WAVES over tools/fp64_workload.py"}
 for kind, c in acc.items():
+    if kind not in work:
+        continue
     w = work[kind]
     rows = w["rows"] * w["evals"]
     f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_TRANS_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"]

@@ -3,7 +3,10 @@
     give the ISSUED FP64 work per update (every lane of every wave-instruction counted), and
   * 1024 trees x 200 under the lane schedule -- k_loglik_level, one cell per lane and every
     wave full (levels of 1024 and 2048 cells), whose counters give the USEFUL FP64 work of one
-    update: what a single thread executing the algorithm once issues.
+    update: what a single thread executing the algorithm once issues;
+  * bench.py's large_forest leg (12.5k trees x 200, auto: k_loglik_pair) and predict leg (125k
+    trees x 500: k_fwd_* / k_bwd_* / k_combine), so every timed leg states its FP64 and VALU-issue
+    fractions from counters of the same build.
 Rows per launch are printed for the summary (tools/fp64_summary.py)."""
 import json
 import os
@@ -21,4 +24,17 @@ for name, trees, kernel in (("wave", 1000, "auto"), ("lane", 1024, "lane")):
         f.total_likelihood(P)
     out[name] = {"trees": trees, "rows": hf.n_rows, "evals": 3}
     f.close()
+hf = g.HostForest.synthetic(12500, 200)                 # bench.py large_forest (its seed is irrelevant here)
+f = g.Forest(hf)
+for _ in range(3):
+    f.total_likelihood(P)
+out["pair"] = {"trees": 12500, "rows": hf.n_rows, "evals": 3}
+f.close()
+hf = g.HostForest.synthetic(125000, 500)                # bench.py predict
+f = g.Forest(hf)
+for _ in range(2):
+    f.predict(P, outputs=(False, False, False))
+out["smooth"] = {"trees": 125000, "rows": hf.n_rows, "evals": 2}
+out["combine"] = out["smooth"]
+f.close()
 print(json.dumps(out))

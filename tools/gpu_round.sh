@@ -16,7 +16,7 @@ python3 tools/pmc_traffic.py gpurun_out/pmcf_${TAG} gpurun_out/pmcw_${TAG} gpuru
 mkdir -p profiles && cp gpurun_out/traffic_${TAG}.json profiles/traffic.json
 # FP64 work per update (issued: the wave kernel; useful: the lane kernel on full waves), one pass
 mkdir -p gpurun_out/pmc64_${TAG}
-timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES -d gpurun_out/pmc64_${TAG} -o p --output-format csv -- python3 tools/fp64_workload.py > gpurun_out/pmc64_${TAG}/workload.json 2> gpurun_out/pmc64_${TAG}.err || { echo "pmc fp64 failed"; tail -20 gpurun_out/pmc64_${TAG}.err; exit 1; }
+timeout -k 10 -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES -d gpurun_out/pmc64_${TAG} -o p --output-format csv -- python3 tools/fp64_workload.py > gpurun_out/pmc64_${TAG}/workload.json 2> gpurun_out/pmc64_${TAG}.err || { echo "pmc fp64 failed"; tail -20 gpurun_out/pmc64_${TAG}.err; exit 1; }
 python3 tools/fp64_summary.py gpurun_out/pmc64_${TAG} gpurun_out/fp64_${TAG}.json && cp gpurun_out/fp64_${TAG}.json profiles/fp64_counts.json
 timeout -k 10 300 python bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; cat gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
