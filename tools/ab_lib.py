@@ -1,4 +1,4 @@
-"""A/B timing of engine builds (diagnostic): python tools/ab_lib.py LIB_DIR [kernel] [trees]
+"""A/B timing of engine builds (diagnostic): python tools/ab_lib.py LIB_DIR [kernel] [trees; 0 = the example]
 loads libggp.so from LIB_DIR instead of the package's lib/ and prints ms per evaluation of
 C2-shaped forests and the per-level kernel times; run it alternately for two builds."""
 import os
@@ -15,7 +15,14 @@ import gfp_gaussian_process_amd as g  # noqa: E402
 kern = sys.argv[2] if len(sys.argv) > 2 else "auto"
 trees = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
 P = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e-04, 8.26e-01, 1.63e-04, 7.48e-01]
-hf = g.HostForest.synthetic(trees, 200)
+if trees > 0:
+    hf = g.HostForest.synthetic(trees, 200)
+else:   # 0: the reference's example (one tree, critical path 3,759 of 22,065 rows)
+    import gzip, shutil, tempfile
+    tmp = os.path.join(tempfile.gettempdir(), "ab_example.csv")
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "example_input.csv.gz"), "rb") as fi, open(tmp, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    hf = g.HostForest.from_csv(tmp, os.path.join(ROOT, "tests", "golden", "example_csv_config.txt"))
 f = g.Forest(hf, kernel=kern)
 for _ in range(3):
     v = f.total_likelihood(P)
