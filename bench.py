@@ -170,6 +170,28 @@ def example_mp(tmp: str, cpu_budget: float):
                     "wall / evaluations (an upper bound per evaluation)"}
 
 
+def inprocess_child(argv) -> int:
+    """`bench.py --inprocess-child TREES ROWS STEPS WARMUP KERNEL DEV[,DEV...]`: the drop-in CLI's
+    multi-GPU path (Forest(hf, devices=[...]), what `-g all` runs) timed in a process of its own,
+    so a failure there never takes the bench line with it; prints one JSON line"""
+    trees, rows, steps, warmup = (int(x) for x in argv[:4])
+    kernel, devs = argv[4], [int(d) for d in argv[5].split(",")]
+    import gfp_gaussian_process_amd as g
+    ha = g.HostForest.synthetic(trees, rows, seed=SEED)
+    fa = g.Forest(ha, devices=devs, kernel=kernel)
+    for _ in range(warmup):
+        fa.total_likelihood(P_EXAMPLE)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        v = fa.total_likelihood(P_EXAMPLE)
+    iel = time.perf_counter() - t1
+    print(json.dumps({"devices": devs, "trees": trees, "rows": ha.n_rows, "steps": steps,
+                      "ms_per_step": 1e3 * iel / steps, "value": ha.n_rows * steps / iel,
+                      "shards": len(fa.shards()), "total_log_likelihood": v}))
+    fa.close()
+    return 0
+
+
 def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: bool = False, note: str = ""):
     """FP64 and VALU-issue fractions of a bench leg from the PMC pass of this build
     (profiles/fp64_counts.json, tools/fp64_summary.py kind `kind`): achieved FP64 = flops per row x
@@ -194,6 +216,8 @@ def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: boo
 
 
 def main() -> int:
+    if len(sys.argv) > 1 and sys.argv[1] == "--inprocess-child":
+        return inprocess_child(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -417,20 +441,22 @@ def main() -> int:
         dist.all_gather_object(devs, local)
         barrier()
         if rank == 0:
-            ha = g.HostForest.synthetic(args.trees * world, args.rows, seed=SEED)
-            fa = g.Forest(ha, devices=[int(d) for d in devs], kernel=args.kernel)
-            for _ in range(args.warmup):
-                fa.total_likelihood(P_EXAMPLE)
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                fa.total_likelihood(P_EXAMPLE)
-            iel = time.perf_counter() - t1
-            inproc = {"devices": [int(d) for d in devs], "trees": args.trees * world, "rows": ha.n_rows, "steps": args.steps,
-                      "ms_per_step": 1e3 * iel / args.steps, "value": ha.n_rows * args.steps / iel,
-                      "shards": len(fa.shards()),
-                      "note": "one process drives every device (Forest(hf, devices=range(N)), the CLI's -g all): "
-                              "the whole job's forest, bitwise the single-device total; the same metric as value"}
-            fa.close()
+            import subprocess
+            # a child process of its own (started, not exec'd): a fault on any device there is
+            # reported in the line instead of ending this rank before it prints
+            cmd = [sys.executable, os.path.abspath(__file__), "--inprocess-child", str(args.trees * world),
+                   str(args.rows), str(args.steps), str(args.warmup), args.kernel, ",".join(str(int(d)) for d in devs)]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+                if r.returncode == 0:
+                    inproc = json.loads(r.stdout.strip().splitlines()[-1])
+                else:
+                    inproc = {"error": f"exit {r.returncode}: " + (r.stdout + r.stderr)[-400:]}
+            except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+                inproc = {"error": repr(e)[-400:]}
+            inproc["note"] = ("one process drives every device (Forest(hf, devices=range(N)), the CLI's -g all), "
+                              "in a child process: the whole job's forest, bitwise the single-device total; the "
+                              "same metric as value")
             store.set("ggp_inprocess_done", "1")
         else:
             store.wait(["ggp_inprocess_done"])

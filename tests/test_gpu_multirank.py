@@ -62,6 +62,18 @@ def test_bench_two_ranks_gloo_rehearsal():
         f.close()
         want = want + v
     assert out["total_log_likelihood"] == want
+    # the drop-in's own multi-GPU path, in a child process of rank 0: one handle over the device
+    # list of the ranks ([0, 0] here: two logical shards), the whole job's forest, W + K chained
+    # calls -- bitwise the single-device chain of the same forest
+    ip = out["inprocess"]
+    assert "error" not in ip, ip
+    assert ip["devices"] == [0, 0] and ip["shards"] == 2 and ip["value"] > 0
+    hw = g.HostForest.synthetic(2 * trees, rows, seed=bench.SEED)
+    fw = g.Forest(hw, device=0)
+    for _ in range(warm + steps):
+        vw = fw.total_likelihood(bench.P_EXAMPLE)
+    fw.close()
+    assert ip["total_log_likelihood"] == vw
 
 
 def _worker(rank, world, port, q):
