@@ -573,6 +573,13 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         const double *rows = buf[k & 1]->data();
         std::thread next;
         if (hi < nr) next = std::thread([&, hi, k] { fr = fetch(hi, buf[(k + 1) & 1]); });
+        struct Join {   // the prefetch joins on every way out of this span (a throw included)
+            std::thread &t;
+            ~Join()
+            {
+                if (t.joinable()) t.join();
+            }
+        } join_next{next};
         ggp_text::write_ordered(file, (hi - lo + blk - 1) / blk, [&](int64_t b, std::string &sbuf) {
             ggp_text::Sink out(sbuf);
             const int64_t r0 = lo + b * blk, r1 = std::min(hi, r0 + blk);
@@ -596,7 +603,6 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
                 out.ch('\n');
             }
         });
-        if (next.joinable()) next.join();
     }
     if (!file) throw std::runtime_error("write failed: " + outfile);
 }

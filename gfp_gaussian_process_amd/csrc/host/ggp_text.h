@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <ostream>
 #include <string>
@@ -226,7 +227,8 @@ inline int io_threads()
 
 // format blocks 0..n_blocks-1 with fmt(block, std::string &) on io_threads() threads and write
 // them to `out` in block order as they complete (the calling thread writes while the pool
-// formats).  At most `window` formatted blocks are held at once (bounded memory).
+// formats).  At most `window` formatted blocks are held at once (bounded memory).  An exception
+// in a formatting thread stops the pool and is rethrown here, after every thread has joined.
 template <class Fmt>
 void write_ordered(std::ostream &out, int64_t n_blocks, Fmt &&fmt, int64_t window = 0)
 {
@@ -237,6 +239,8 @@ void write_ordered(std::ostream &out, int64_t n_blocks, Fmt &&fmt, int64_t windo
     std::vector<std::string> slot((size_t)window);
     std::vector<int64_t> ready((size_t)window, -1);   // block held by the slot, once formatted
     int64_t written = 0;                             // blocks written so far
+    bool stop = false;                               // a thread failed (or the writer did)
+    std::exception_ptr err;
     std::atomic<int64_t> next{0};
     std::mutex mu;
     std::condition_variable cv_ready, cv_free;
@@ -244,11 +248,21 @@ void write_ordered(std::ostream &out, int64_t n_blocks, Fmt &&fmt, int64_t windo
         for (int64_t b; (b = next.fetch_add(1)) < n_blocks;) {
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv_free.wait(lk, [&] { return b - written < window; });
+                cv_free.wait(lk, [&] { return stop || b - written < window; });
+                if (stop) return;
             }
             std::string &s = slot[(size_t)(b % window)];
-            s.clear();
-            fmt(b, s);
+            try {
+                s.clear();
+                fmt(b, s);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+                stop = true;
+                cv_ready.notify_all();
+                cv_free.notify_all();
+                return;
+            }
             {
                 std::lock_guard<std::mutex> lk(mu);
                 ready[(size_t)(b % window)] = b;
@@ -261,7 +275,8 @@ void write_ordered(std::ostream &out, int64_t n_blocks, Fmt &&fmt, int64_t windo
     for (int64_t b = 0; b < n_blocks; ++b) {
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv_ready.wait(lk, [&] { return ready[(size_t)(b % window)] == b; });
+            cv_ready.wait(lk, [&] { return stop || ready[(size_t)(b % window)] == b; });
+            if (stop) break;
         }
         const std::string &s = slot[(size_t)(b % window)];
         out.write(s.data(), (std::streamsize)s.size());
@@ -272,6 +287,7 @@ void write_ordered(std::ostream &out, int64_t n_blocks, Fmt &&fmt, int64_t windo
         cv_free.notify_all();
     }
     for (auto &th : pool) th.join();
+    if (err) std::rethrow_exception(err);
 }
 
 }  // namespace ggp_text

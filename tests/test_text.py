@@ -51,3 +51,9 @@ def test_put_num_is_the_streams_default_format(text_check, seed):
 def test_write_ordered_is_the_serial_stream(text_check, threads):
     out = subprocess.run([text_check, "ordered", str(threads)], check=True, capture_output=True, text=True).stdout
     assert out.strip() == "same"
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_write_ordered_rethrows_a_formatting_error(text_check, threads):
+    out = subprocess.run([text_check, "throws", str(threads)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip() == "caught block 377", (out.stdout, out.stderr)

@@ -5,6 +5,7 @@
 //                                 mismatch count, then the first 2000 put_num strings, one a line
 //   text_check ordered THREADS  : write_ordered over 5000 blocks of different lengths against the
 //                                 same blocks concatenated serially; prints "same" or "differ"
+//   text_check throws THREADS   : a formatting thread throws; write_ordered rethrows it
 #include <cinttypes>
 #include <cmath>
 #include <cstdio>
@@ -12,6 +13,7 @@
 #include <limits>
 #include <random>
 #include <sstream>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -100,6 +102,21 @@ int main(int argc, char **argv)
         ggp_text::write_ordered(out, nb, fmt, 7);
         std::printf("%s\n", out.str() == serial ? "same" : "differ");
         return 0;
+    }
+    if (!std::strcmp(argv[1], "throws")) {   // a formatting thread throws: rethrown by write_ordered
+        setenv("GGP_IO_THREADS", argv[2], 1);
+        std::ostringstream out;
+        try {
+            ggp_text::write_ordered(out, 1000, [](int64_t b, std::string &s) {
+                if (b == 377) throw std::runtime_error("block 377");
+                ggp_text::put_int(s, b);
+            }, 5);
+        } catch (const std::runtime_error &e) {
+            std::printf("caught %s\n", e.what());
+            return 0;
+        }
+        std::printf("not thrown\n");
+        return 1;
     }
     return 2;
 }
