@@ -15,6 +15,7 @@
 // Output text is produced with the same iostream manipulators as the reference, so the files
 // are byte-identical given identical numbers.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +44,21 @@ std::ofstream g_iter;       // _file_iteration
 int g_iteration = 0;        // _iteration
 int g_print_level = 0;      // _print_level
 bool g_save_ll = false;     // _save_ll
+
+// GGP_TIMING=1 (additive, diagnostic): wall seconds of the phases to stderr; the log files keep
+// the reference's content
+struct PhaseClock {
+    const bool on = std::getenv("GGP_TIMING") && std::getenv("GGP_TIMING")[0] == '1';
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(const char *what)
+    {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ggp timing] %-28s %9.3f s\n", what, std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    }
+};
+PhaseClock g_clock;
 
 // ---- utils.h ------------------------------------------------------------------------------
 std::vector<std::string> split_string_at(std::string s, const std::string &delimiter = ",")
@@ -503,7 +519,9 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     for (const Params &P : plist) outfile += outfile_param_code(P);
     outfile += "_prediction.csv";
     Forest F;
+    g_clock.mark("-p: start");
     build_forest(F, d, -1, args["noise_model"], args["cell_division_model"]);
+    g_clock.mark("-p: forest built, on device");
     std::vector<double> pv;
     for (const Params &P : plist) {
         const auto v = P.get_final();
@@ -513,6 +531,7 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
     // the combined rows stay in HBM; the writer streams them by row ranges (bounded host memory)
     const int rc = ggp_predict(F.gpu, pv.data(), (int32_t)plist.size(), nullptr, nullptr, nullptr);
     if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_predict: ") + ggp_strerror(rc));
+    g_clock.mark("-p: smoother (GPU)");
     // rows per device-to-host copy (GGP_PREDICT_SPAN: a test knob; two host buffers of this many rows)
     const char *span_env = std::getenv("GGP_PREDICT_SPAN");
     const int64_t span = span_env && std::atoll(span_env) > 0 ? std::atoll(span_env) : (int64_t)1 << 20;
@@ -542,6 +561,7 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
             bf.write(reinterpret_cast<const char *>(row14.data()), (std::streamsize)(row14.size() * sizeof(double)));
         }
         if (!bf) throw std::runtime_error("write failed: " + binfile);
+        g_clock.mark("-p: binary rows written");
         return;
     }
     g_log << "Outfile: " << outfile << "\n";
@@ -605,6 +625,7 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         });
     }
     if (!file) throw std::runtime_error("write failed: " + outfile);
+    g_clock.mark("-p: csv rows written");
 }
 
 // ---- -j (main.cpp:150-186; correlation_tree.h:9-23, 96-126, 588-648, 786-791) -------------
@@ -950,6 +971,7 @@ int main(int argc, char **argv)
         } else if (ggp_dataset_read(args["infile"].c_str(), cfg, &data) != GGP_OK) {
             throw std::invalid_argument(ggp_host_last_error());
         }
+        g_clock.mark("read the input");
         int32_t nseg = 0;
         ggp_dataset_segments(data, nullptr, 0, &nseg);
         std::vector<int32_t> seg(nseg);

@@ -33,6 +33,9 @@ def run(args):
     t0 = time.perf_counter()
     r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=900)
     print(f"{' '.join(args[4:])}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    for ln in r.stderr.splitlines():   # the CLI's phase timings (GGP_TIMING=1)
+        if ln.startswith("[ggp timing]"):
+            print("   " + ln, file=sys.stderr, flush=True)
     if r.returncode != 0:
         raise SystemExit(r.stdout[-2000:] + r.stderr[-2000:])
     return time.perf_counter() - t0
