@@ -6,7 +6,7 @@
       is byte-identical with the forest on 8 logical shards (-g 0,...,0: the 8-GPU layout);
       every sample equals the Python handle's chained value bitwise; a 200-tree sub-forest
       keeping the full forest's init statistics follows the oracle's chain to 1e-9.
-  C5  -p on a per-GPU shard of 1M trees x 500 tp (125k trees, 6.25e7 rows): 40 sampled trees
+  C5  -p on a per-GPU shard of 1M trees x 500 tp (125k trees, 6.25e7 rows): 400 sampled trees
       against the oracle smoother at PRED_TOL (test_gpu_parity.py); the same forest in 8
       chunks through a capped workspace (max_shard_rows) bitwise equal to the one-shard run.
   C3  -m with all 11 parameters free (beta added as in SURVEY §8(d)), log space, LN_NELDERMEAD,
@@ -70,7 +70,7 @@ def test_c5_predict_shard_125k_trees():
     assert n == 62_500_000
     f = g.Forest(hf)
     f.predict(INIT, outputs=(False, False, False))
-    picks = list(range(0, 125_000, 3125))                    # 40 trees; tree k: rows [500 k, 500 k + 500)
+    picks = list(range(0, 125_000, 312))[:400]               # 400 trees; tree k: rows [500 k, 500 k + 500)
     sub = hf.subset_trees(hf.roots[picks])
     ref = O.OracleForest(sub.a).predict(INIT)[2]
     got = np.concatenate([f.predict_rows(500 * k, 500 * k + 500) for k in picks])
