@@ -87,7 +87,7 @@ GGP_DEV WStep wstep(const double *m, const double *C, const double t, const doub
     S.r_four_a = h * h;
     S.two_a = 2. * a;
     S.four_a = 4. * a;
-    S.four_aa = 4 * (a * a);
+    S.four_aa = S.two_a * S.two_a;   // 4 (a a): scaling by 4 is exact, one multiply
     S.bbl = b + m[2];
     S.Cxl = C[2];
     S.bx = m[0];
@@ -659,7 +659,7 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     // integer, that integer, where td lies within 5e-5 below -1 (the row's polynomial holds there).
     const double ti = S.t * L.b_tau;
     const double B = wave::pin(__builtin_fma(S.Cxl, L.b_km, S.bbl) + L.b_gqks);
-    const double xz = B + S.two_a * ti;
+    const double xz = __builtin_fma(S.two_a, ti, B);
     const double ya = (100.0 * (1.0 + 0x1p-22)) * rcp0(1.0 + fabs(xz * S.r_two_sa0));
     const int k = min(cvt_i32(ya), GGP_DAWSON_NINT - 1);
     const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
@@ -677,9 +677,9 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     const double td = __builtin_fma(-(double)(2 * k + 1), d1, 200.0) * rcp1(d1);
     const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
     const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
-    const double argA = wave::pin(ti * (B + S.a * ti));
-    const double argE = wave::pin(n + c + z * z);
-    const double argZ = wave::pin(S.a * (ti * ti) + B * ti + c);
+    const double argA = wave::pin(ti * __builtin_fma(S.a, ti, B));
+    const double argE = wave::pin(__builtin_fma(z, z, n + c));
+    const double argZ = wave::pin(__builtin_fma(S.a, ti * ti, __builtin_fma(B, ti, c)));
     const double arg = L.b_isE ? argE : L.b_isA ? argA : argZ;
     // exp reduction (exp_ocml)
     const double dn = __builtin_rint(arg * 0x1.71547652b82fep+0);
@@ -719,12 +719,14 @@ GGP_DEV double stageC(const wave::WStep &S, const Lane &L, const double *lds)
     const double al = __builtin_fma(L.i_u2, al3, __builtin_fma(L.i_u1, B, L.i_u0));
     const double be = -S.two_a * __builtin_fma(L.i_w3, B, L.i_w2);
     const double ga = L.i_g * S.four_aa;
-    const double P0 = al + t0 * (be + ga * t0), P1 = al + t1 * (be + ga * t1);
-    const double q1 = B * 2., q2 = (S.two_a - BB) * 2., q3 = B * (-6. * S.a + BB) * 2.;
-    const double Q = __builtin_fma(L.i_s3, q3, __builtin_fma(L.i_s2, q2, __builtin_fma(L.i_s1, q1, L.i_s0)));
+    const double P0 = __builtin_fma(t0, __builtin_fma(ga, t0, be), al), P1 = __builtin_fma(t1, __builtin_fma(ga, t1, be), al);
+    // Q = s0 + s1 2B + s2 2(2a - BB) + s3 2B(BB - 6a): one selector is nonzero (tau kind k), so
+    // the factor 2 applied once to the selected term gives the same bits as applying it per term
+    const double q2 = S.two_a - BB, q3 = B * __builtin_fma(-6., S.a, BB);
+    const double Q = __builtin_fma(2., __builtin_fma(L.i_s3, q3, __builtin_fma(L.i_s2, q2, L.i_s1 * B)), L.i_s0);
     const double S1 = S.two_sa * L.i_S1;
-    const double dterm = wave::pin(Q * (E0 * D0 - E1 * D1));
-    const double x = S1 * ec * (ea0 * P0 - ea1 * P1) + dterm;
+    const double dterm = wave::pin(Q * __builtin_fma(E0, D0, -(E1 * D1)));
+    const double x = __builtin_fma(S1 * ec, __builtin_fma(ea0, P0, -(ea1 * P1)), dterm);
     // the denominator 2^(k+1) a^k sqrt(a) as two_sa (2a)^k: the products of store_pw's
     // denominators (scaling by powers of two is exact), and an rdiv seed from v_rcp_f64
     const double p1 = S.two_a, p2 = p1 * p1, p3 = p2 * p1;
@@ -769,7 +771,7 @@ GGP_DEV UInnov uinnov(const double m1, const double C00, const double C01, const
     v.S00 = C00 + var_x;
     v.S01 = C01 + 0.0;
     v.S11 = C11 + d11;
-    const double det = v.S00 * v.S11 - v.S01 * v.S01;
+    const double det = __builtin_fma(v.S00, v.S11, -(v.S01 * v.S01));
     v.invdet = rcp2(det);
     return v;
 }
