@@ -838,6 +838,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         wave_sync();
     }
     const double var_x = p[7], var_g = p[8], var_dx = p[9], var_dg = p[10], b = p[6];
+    const double g_sc = F.scaled ? var_g : 0.0, g_0 = F.scaled ? 0.0 : var_g;   // W::uinnov's D11
     if (lane == 0) {
         lds[W::L_X + ggp::X_ONE] = 1.0;
         lds[W::L_BV + ggp::BV_ONE] = 1.0;
@@ -1081,8 +1082,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
                 lds[L.f_dst] = fv;
                 const double nx0 = o0 - yl, nx1 = o1 - yf;
-                const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, var_g,
-                                                F.scaled, F.fp_auto);
+                const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, g_sc,
+                                                g_0, F.fp_auto);
                 if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
                     lds[W::L_RX0 + slot] = nx0;
                     lds[W::L_RX1 + slot] = nx1;
@@ -1927,7 +1928,7 @@ __global__ __launch_bounds__(64) void k_debug_dawson(const double *__restrict__ 
         S.r_two_sa = 1.0; S.r_two_sa0 = 1.0; S.r_four_a = 0.25; S.bbl = v; S.Cxl = 0.0; S.bx = 0.0; S.Cxx = 0.0;
         W::Lane L{};
         L.b_tau = 0.0; L.b_km = 1.0; L.b_gqks = 0.0; L.b_m1 = 1.0; L.b_m2 = 0.5; L.b_kc = 0.0;
-        L.b_mult = GGP_SPI2; L.b_isE = 0; L.b_isA = 0; L.b_isD = 1; L.b_exmask = 0;
+        L.b_mult = GGP_SPI2; L.b_sgn = (int)0x80000000u; L.b_isE = 0; L.b_isA = 0; L.b_isD = 1; L.b_exmask = 0;
         const W::BOut o = W::stageB(S, L, s_w);
         r = o.rare ? W::stageB_rare(true, o.arg, o.z, o.v) : o.v;
     }

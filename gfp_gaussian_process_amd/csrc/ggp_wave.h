@@ -80,7 +80,8 @@ GGP_DEV WStep wstep(const double *m, const double *C, const double t, const doub
     s = __builtin_fma(d, h, s);
     d = __builtin_fma(-s, s, a);
     s = __builtin_fma(d, h, s);
-    s = (a == 0.0 || a == __builtin_huge_val()) ? a : s;   // ocml: sqrt(+-0, +inf) = the input
+    // (ocml's sqrt returns a itself for a = 0 and +inf; here a step with such an a gives NaN either
+    // way: the Dawson argument B / (2 sqrt a) and the integrals divide by sqrt a)
     S.two_sa = 2. * s;
     S.m2sa = -2. * s;
     S.r_two_sa = h;
@@ -322,7 +323,7 @@ struct LaneC {
     // stage B: argument forms (ggp_wave.h exp_arg); Dawson lanes use z only.  The c slope is
     // kb b + kgl gl + kgq gq (c_slope's value: the integer coefficients are exact)
     double b_tau, b_km, b_ks, b_m1, b_m2, b_kb, b_kgl, b_kgq, b_mult;
-    int b_isE, b_isA, b_isD, b_exmask, b_dst;
+    int b_isE, b_isA, b_isD, b_exmask, b_sgn, b_dst;
     // stage C: the integral (tau_unified) with 0/1 selectors
     double i_tau0, i_tau1, i_km, i_ks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
     int i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
@@ -338,7 +339,7 @@ struct LaneC {
 
 struct Lane {
     double b_tau, b_km, b_gqks, b_m1, b_m2, b_kc, b_mult;
-    int b_isE, b_isA, b_isD, b_exmask, b_dst;
+    int b_isE, b_isA, b_isD, b_exmask, b_sgn, b_dst;
     double i_tau0, i_tau1, i_km, i_gqks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
     int i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
     int mo_v0, mo_v1, mo_v2, mo_dst;
@@ -383,6 +384,7 @@ constexpr LaneC make_lane_c(const int lane)
             L.b_isD = 1;
             L.b_exmask = 0;
             L.b_mult = GGP_SPI2;
+            L.b_sgn = (int)0x80000000u;   // z's sign onto the value (Dawson is odd)
             L.b_dst = L_D + (lane - kLaneD0);
         } else {
             const int xb = xt.iB < 6 ? xt.iB : 0;
@@ -397,6 +399,7 @@ constexpr LaneC make_lane_c(const int lane)
             L.b_isA = xt.kind == KX_A;
             L.b_exmask = -1;
             L.b_mult = 1.0;
+            L.b_sgn = 0;
             L.b_dst = isX ? L_X + xj : L_DUMMY + lane;
         }
     }
@@ -522,7 +525,8 @@ GGP_DEV Lane lane_from(const int lane, const LaneC &C, const OU &P, const double
     L.b_tau = C.b_tau; L.b_km = C.b_km; L.b_gqks = P.gq * C.b_ks; L.b_m1 = C.b_m1; L.b_m2 = C.b_m2;
     L.b_kc = __builtin_fma(C.b_kgq, P.gq, __builtin_fma(C.b_kgl, P.gl, C.b_kb * P.b));
     L.b_mult = C.b_mult;
-    L.b_isE = C.b_isE; L.b_isA = C.b_isA; L.b_isD = C.b_isD; L.b_exmask = C.b_exmask; L.b_dst = C.b_dst;
+    L.b_isE = C.b_isE; L.b_isA = C.b_isA; L.b_isD = C.b_isD; L.b_exmask = C.b_exmask; L.b_sgn = C.b_sgn;
+    L.b_dst = C.b_dst;
     L.i_tau0 = C.i_tau0; L.i_tau1 = C.i_tau1; L.i_km = C.i_km; L.i_gqks = P.gq * C.i_ks;
     L.i_u0 = C.i_u0; L.i_u1 = C.i_u1; L.i_u2 = C.i_u2; L.i_w2 = C.i_w2; L.i_w3 = C.i_w3; L.i_g = C.i_g;
     L.i_s0 = C.i_s0; L.i_s1 = C.i_s1; L.i_s2 = C.i_s2; L.i_s3 = C.i_s3; L.i_S1 = C.i_S1;
@@ -613,6 +617,31 @@ GGP_DEV int cvt_i32(const double x)
 #endif
 }
 
+// the high 32 bits of a double, and a double with its high word replaced
+GGP_DEV int hi32(const double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __double2hiint(x);
+#else
+    long long b;
+    __builtin_memcpy(&b, &x, 8);
+    return (int)(b >> 32);
+#endif
+}
+GGP_DEV double with_hi(const double x, const int hi)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __hiloint2double(hi, __double2loint(x));
+#else
+    unsigned long long b;
+    __builtin_memcpy(&b, &x, 8);
+    b = (b & 0xffffffffULL) | ((unsigned long long)(unsigned)hi << 32);
+    double y;
+    __builtin_memcpy(&y, &b, 8);
+    return y;
+#endif
+}
+
 // ---- stage B: one transcendental per lane ---------------------------------------------------
 // the rare branches: exp beyond 2^50 (ocml's exp), Dawson Taylor (y100 >= 97) and continued
 // fraction (|x| > 45), as ggp_wave.h dawson_bf
@@ -689,9 +718,11 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     double h = __builtin_fma(a[0], tv, a[1]);
 #pragma unroll
     for (int i = 2; i < kTabRow; ++i) h = __builtin_fma(h, tv, a[i]);
-    // no branches below: the exponent masked to 0 on Dawson lanes, the rare flags by bitwise ops
+    // no branches below: the exponent masked to 0 on Dawson lanes, z's sign bit onto a Dawson
+    // value's (two 32-bit operations on the high word; an exp lane's mask is 0), the rare flags
+    // by bitwise ops
     double v = __builtin_ldexp(h * L.b_mult, cvt_i32(dn) & L.b_exmask);
-    v = ((L.b_isD != 0) & (z < 0.0)) ? -v : v;
+    v = with_hi(v, hi32(v) ^ (hi32(z) & L.b_sgn));
     BOut o;
     o.v = v;
     o.arg = arg;
@@ -732,7 +763,9 @@ GGP_DEV double stageC(const wave::WStep &S, const Lane &L, const double *lds)
     const double p1 = S.two_a, p2 = p1 * p1, p3 = p2 * p1;
     const double qk = __builtin_fma(L.i_s3, p3, __builtin_fma(L.i_s2, p2, __builtin_fma(L.i_s1, p1, -0.5 * L.i_s0)));
     const double den = S.two_sa * qk;
-    return rdiv(x, den, rcp1(den));
+    // rdiv's residual step on the v_rcp_f64 seed alone (relative error e ~ 1e-8): the quotient
+    // within e^2 + its roundings, an ulp or two -- no Newton step on the seed
+    return rdiv(x, den, rcp0(den));
 }
 
 // ---- stage D: the lane's output terms over the step's monomials ------------------------------
@@ -762,14 +795,18 @@ struct UInnov {
     double S00, S01, S11, invdet;
 };
 // the innovation covariance S from the prior's C00, C01, C11 and m1 (ggp_wave.h innovation's
-// expressions) and 1/det S by rcp2 (its Newton steps run while the update's operands load)
+// expressions) and 1/det S by rcp2 (its Newton steps run while the update's operands load).
+// D11 = var_g (m1 + fp_auto) under the scaled noise model, var_g otherwise, as one fma on the
+// launch constants g_sc = scaled ? var_g : 0, g_0 = scaled ? 0 : var_g (the same value, no select);
+// S01 = C01 (the reference's C01 + 0 differs only in the sign of a zero, which no later product
+// or sum with a nonzero value can show)
 GGP_DEV UInnov uinnov(const double m1, const double C00, const double C01, const double C11, const double var_x,
-                      const double var_g, const int scaled, const double fp_auto)
+                      const double g_sc, const double g_0, const double fp_auto)
 {
     UInnov v;
-    const double d11 = scaled ? var_g * (m1 + fp_auto) : var_g;
+    const double d11 = __builtin_fma(g_sc, m1 + fp_auto, g_0);
     v.S00 = C00 + var_x;
-    v.S01 = C01 + 0.0;
+    v.S01 = C01;
     v.S11 = C11 + d11;
     const double det = __builtin_fma(v.S00, v.S11, -(v.S01 * v.S01));
     v.invdet = rcp2(det);
@@ -871,7 +908,7 @@ struct HostWave {
         for (int l = 0; l < 64; ++l) f[l] = finish(L[l], lds, 0);
         for (int l = 0; l < 64; ++l) lds[L[l].f_dst] = f[l];
         const double *st = lds + L_ST;
-        const UInnov v = uinnov(st[1], st[4], st[5], st[9], var_x, var_g, scaled, fp_auto);
+        const UInnov v = uinnov(st[1], st[4], st[5], st[9], var_x, scaled ? var_g : 0.0, scaled ? 0.0 : var_g, fp_auto);
         double u[64];
         for (int l = 0; l < 64; ++l) u[l] = upost(upost_load(L[l], lds), f[l], v);
         for (int l = 0; l < 64; ++l) {
