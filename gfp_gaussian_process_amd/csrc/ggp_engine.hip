@@ -993,7 +993,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 wave_sync();
                 if (lane < slot) {
                     const double s00 = lds[W::L_RS0 + lane], s01 = lds[W::L_RS1 + lane], s11 = lds[W::L_RS2 + lane];
-                    lds[W::L_RT + lane] = W::ll_quad(lds[W::L_RX0 + lane], lds[W::L_RX1 + lane], s00, s01, s11) -
+                    // the ring holds the prior means: -x = m - y formed here, 64 rows at once (the
+                    // quadratic form is even in x)
+                    lds[W::L_RT + lane] = W::ll_quad(lds[W::L_RX0 + lane] - lds[W::L_ROWL + lane],
+                                                     lds[W::L_RX1 + lane] - lds[W::L_ROWF + lane], s00, s01, s11) -
                                            0.5 * log(ggp_det_pplu(s00, s01, s01, s11)) - F.two_log_2pi;
                 }
                 wave_sync();
@@ -1052,9 +1055,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             }
             const double x0 = y_l - m[0], x1 = y_f - m[1];
             const W::WInnov v = W::innovation(m, C, var_x, var_g, F.scaled, F.fp_auto);
-            if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
-                lds[W::L_RX0 + slot] = x0;
-                lds[W::L_RX1 + slot] = x1;
+            if (lane == 0) {   // the ll term's inputs: the prior means (the flush forms m - y) and S
+                lds[W::L_RX0 + slot] = m[0];
+                lds[W::L_RX1 + slot] = m[1];
                 lds[W::L_RS0 + slot] = v.S00;
                 lds[W::L_RS1 + slot] = v.S01;
                 lds[W::L_RS2 + slot] = v.S11;
@@ -1078,15 +1081,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 // with the finish's before any store
                 const double *o = lds + W::L_OUT;
                 const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
-                const double yl = lds[W::L_ROWL + slot], yf = lds[W::L_ROWF + slot];
                 const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
                 lds[L.f_dst] = fv;
-                const double nx0 = o0 - yl, nx1 = o1 - yf;
                 const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, g_sc,
                                                 g_0, F.fp_auto);
-                if (lane == 0) {   // the ll term's inputs (its quadratic form is even in x)
-                    lds[W::L_RX0 + slot] = nx0;
-                    lds[W::L_RX1 + slot] = nx1;
+                if (lane == 0) {   // the ll term's inputs: the prior means (the flush forms m - y) and S
+                    lds[W::L_RX0 + slot] = o0;
+                    lds[W::L_RX1 + slot] = o1;
                     lds[W::L_RS0 + slot] = v.S00;
                     lds[W::L_RS1 + slot] = v.S01;
                     lds[W::L_RS2 + slot] = v.S11;

@@ -285,7 +285,7 @@ enum {
     L_ONE1 = L_ZERO + 1,
     L_ST = L_ONE1 + 1,                            // prior: m[4], C[16], -x0 at 20, -x1 at 24
     L_POST = L_ST + 28,                           // posterior: m[4], C[16]
-    L_RX0 = L_POST + 20,                          // ll ring: -x0, -x1, S00, S01, S11 per row
+    L_RX0 = L_POST + 20,                          // ll ring: prior m0, m1, S00, S01, S11 per row
     L_RX1 = L_RX0 + 64,
     L_RS0 = L_RX1 + 64,
     L_RS1 = L_RS0 + 64,
@@ -788,7 +788,7 @@ GGP_DEV double mono(const Lane &L, const double *lds) { return (lds[L.mo_v0] * l
 // ---- finish and update ------------------------------------------------------------------------
 GGP_DEV double finish(const Lane &L, const double *lds, const int slot)
 {
-    return __builtin_fma(-lds[L.f_na], lds[L.f_nb + (L.f_row ? slot : 0)], lds[L.f_src]);
+    return __builtin_fma(-lds[L.f_na], lds[L.f_nb + mul24(slot, L.f_row)], lds[L.f_src]);   // f_row: 0 or 1
 }
 
 struct UInnov {
