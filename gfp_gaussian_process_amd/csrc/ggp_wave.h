@@ -680,16 +680,20 @@ GGP_DEV void sched_fence()
 
 GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
 {
-    // The Dawson interval first, from the unrefined seeds (v_rsq, v_rcp: ~2^-26 relative each),
-    // so the table row's six 128-bit LDS reads are in flight while z, the Chebyshev variable and
-    // the exponential's argument and reduction are formed (exp lanes read the exp row).  The seed
-    // quotient is biased up by 2^-22 (more than the seeds' error): k is floor(y100) -- on an
-    // interval boundary too (x = 24: y100 = 4) -- or, for y100 within 2.4e-5 below the next
-    // integer, that integer, where td lies within 5e-5 below -1 (the row's polynomial holds there).
+    // z first, then the Dawson interval from 1 / (1 + |z|) -- the reciprocal td needs anyway (v_rcp_f64
+    // and one Newton step): the quotient biased up by 2^-22 makes k floor(y100) -- on an interval
+    // boundary too (x = 24: y100 = 4) -- or, for y100 within 2.4e-5 below the next integer, that
+    // integer, where td lies within 5e-5 below -1 (the row's polynomial holds there).  The table
+    // row's six 128-bit LDS reads are then in flight while the exponential's argument and
+    // reduction are formed (exp lanes read the exp row).
     const double ti = S.t * L.b_tau;
     const double B = wave::pin(__builtin_fma(S.Cxl, L.b_km, S.bbl) + L.b_gqks);
     const double xz = __builtin_fma(S.two_a, ti, B);
-    const double ya = (100.0 * (1.0 + 0x1p-22)) * rcp0(1.0 + fabs(xz * S.r_two_sa0));
+    const double z = rdiv(xz, S.two_sa, S.r_two_sa);
+    const double ax = fabs(z);
+    const double d1 = 1.0 + ax;
+    const double r1 = rcp1(d1);
+    const double ya = (100.0 * (1.0 + 0x1p-22)) * r1;
     const int k = min(cvt_i32(ya), GGP_DAWSON_NINT - 1);
     const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
     const double *A = lds + L_TAB + row;
@@ -697,13 +701,10 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
 #pragma unroll
     for (int i = 0; i < kTabRow; ++i) a[i] = A[i];
     sched_fence();
-    const double z = rdiv(xz, S.two_sa, S.r_two_sa);
-    const double ax = fabs(z);
     // td = 2 y100 - (2k + 1) as (200 - (2k + 1) d1) / d1: the numerator by one fma (exact before
     // its rounding), so td is within ~2 ulp of itself, not of y100 (near small |z| an ulp of y100
     // is tens of ulp of the value: dx/dy ~ 1e-2, x ~ 0.05)
-    const double d1 = 1.0 + ax;
-    const double td = __builtin_fma(-(double)(2 * k + 1), d1, 200.0) * rcp1(d1);
+    const double td = __builtin_fma(-(double)(2 * k + 1), d1, 200.0) * r1;
     const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
     const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
     const double argA = wave::pin(ti * __builtin_fma(S.a, ti, B));
