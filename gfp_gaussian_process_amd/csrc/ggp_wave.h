@@ -322,7 +322,7 @@ GGP_DEV double tab_entry(const int k)
 struct LaneC {
     // stage B: argument forms (ggp_wave.h exp_arg); Dawson lanes use z only.  The c slope is
     // kb b + kgl gl + kgq gq (c_slope's value: the integer coefficients are exact)
-    double b_tau, b_km, b_ks, b_m1, b_m2, b_kb, b_kgl, b_kgq, b_mult;
+    double b_tau, b_km, b_ks, b_m1, b_m2, b_kb, b_kgl, b_kgq, b_mult, b_zc;
     int b_isE, b_isA, b_isD, b_exmask, b_sgn, b_dst;
     // stage C: the integral (tau_unified) with 0/1 selectors
     double i_tau0, i_tau1, i_km, i_ks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
@@ -338,7 +338,7 @@ struct LaneC {
 };
 
 struct Lane {
-    double b_tau, b_km, b_gqks, b_m1, b_m2, b_kc, b_mult;
+    double b_tau, b_km, b_gqks, b_m1, b_m2, b_kc, b_mult, b_zc;
     int b_isE, b_isA, b_isD, b_exmask, b_sgn, b_dst;
     double i_tau0, i_tau1, i_km, i_gqks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
     int i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
@@ -397,6 +397,8 @@ constexpr LaneC make_lane_c(const int lane)
             c_coef(xt.ic, L.b_kb, L.b_kgl, L.b_kgq);
             L.b_isE = xt.kind == KX_E;
             L.b_isA = xt.kind == KX_A;
+            // c enters the Z kind's argument (and the C kind's: t = 0 there), not the A kind's
+            L.b_zc = xt.kind == KX_A ? 0.0 : 1.0;
             L.b_exmask = -1;
             L.b_mult = 1.0;
             L.b_sgn = 0;
@@ -525,6 +527,7 @@ GGP_DEV Lane lane_from(const int lane, const LaneC &C, const OU &P, const double
     L.b_tau = C.b_tau; L.b_km = C.b_km; L.b_gqks = P.gq * C.b_ks; L.b_m1 = C.b_m1; L.b_m2 = C.b_m2;
     L.b_kc = __builtin_fma(C.b_kgq, P.gq, __builtin_fma(C.b_kgl, P.gl, C.b_kb * P.b));
     L.b_mult = C.b_mult;
+    L.b_zc = C.b_zc;
     L.b_isE = C.b_isE; L.b_isA = C.b_isA; L.b_isD = C.b_isD; L.b_exmask = C.b_exmask; L.b_sgn = C.b_sgn;
     L.b_dst = C.b_dst;
     L.i_tau0 = C.i_tau0; L.i_tau1 = C.i_tau1; L.i_km = C.i_km; L.i_gqks = P.gq * C.i_ks;
@@ -707,10 +710,11 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     const double td = __builtin_fma(-(double)(2 * k + 1), d1, 200.0) * r1;
     const double c = wave::pin(__builtin_fma(L.b_kc, S.t, __builtin_fma(S.Cxx, L.b_m2, S.bx * L.b_m1)));
     const double n = wave::pin(rdiv(-(B * B), S.four_a, S.r_four_a));
-    const double argA = wave::pin(ti * __builtin_fma(S.a, ti, B));
+    // the A and Z kinds in one form: argZ = a ti^2 + B ti + c, argA = the same without c (c times
+    // the lane's 0/1 constant), then one select against the E kind
     const double argE = wave::pin(__builtin_fma(z, z, n + c));
-    const double argZ = wave::pin(__builtin_fma(S.a, ti * ti, __builtin_fma(B, ti, c)));
-    const double arg = L.b_isE ? argE : L.b_isA ? argA : argZ;
+    const double argAZ = wave::pin(__builtin_fma(S.a, ti * ti, __builtin_fma(B, ti, c * L.b_zc)));
+    const double arg = L.b_isE ? argE : argAZ;
     // exp reduction (exp_ocml)
     const double dn = __builtin_rint(arg * 0x1.71547652b82fep+0);
     double r = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, arg);
