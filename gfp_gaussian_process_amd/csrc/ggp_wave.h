@@ -76,9 +76,9 @@ GGP_DEV WStep wstep(const double *m, const double *C, const double t, const doub
     const double e = __builtin_fma(-h, s, 0.5);
     s = __builtin_fma(s, e, s);
     h = __builtin_fma(h, e, h);
-    double d = __builtin_fma(-s, s, a);
-    s = __builtin_fma(d, h, s);
-    d = __builtin_fma(-s, s, a);
+    // one residual correction (ocml takes two: its result can differ in the last bit, which moves
+    // the step's values by an ulp -- the wave schedule is not bitwise the lane schedule anyway)
+    const double d = __builtin_fma(-s, s, a);
     s = __builtin_fma(d, h, s);
     // (ocml's sqrt returns a itself for a = 0 and +inf; here a step with such an a gives NaN either
     // way: the Dawson argument B / (2 sqrt a) and the integrals divide by sqrt a)
@@ -697,7 +697,8 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     const double d1 = 1.0 + ax;
     const double r1 = rcp1(d1);
     const double ya = (100.0 * (1.0 + 0x1p-22)) * r1;
-    const int k = min(cvt_i32(ya), GGP_DAWSON_NINT - 1);
+    const int kraw = cvt_i32(ya);
+    const int k = min(kraw, GGP_DAWSON_NINT - 1);
     const int row = L.b_isD ? mul24(k, kTabRow) : kExpRow * kTabRow;
     const double *A = lds + L_TAB + row;
     double a[kTabRow];
@@ -732,9 +733,10 @@ GGP_DEV BOut stageB(const wave::WStep &S, const Lane &L, const double *lds)
     o.v = v;
     o.arg = arg;
     o.z = z;
-    // Taylor (y100 >= 97) flagged from the seed with a margin: stageB_rare decides on the exact
-    // quotient and returns the table value when neither branch applies
-    const bool rare_d = (ya >= (double)GGP_DAWSON_NINT - 0.01) | (ax > 45.0);
+    // Taylor (y100 >= 97) flagged from the biased quotient's integer part (it is >= the exact
+    // y100, so no Taylor case is missed): stageB_rare decides on the exact quotient and returns
+    // the table value when neither branch applies
+    const bool rare_d = (kraw >= GGP_DAWSON_NINT) | (ax > 45.0);
     const bool rare_e = !(fabs(arg) < kExpFastMax);
     o.rare = ((L.b_isD != 0) & rare_d) | ((L.b_isD == 0) & rare_e);
     return o;
