@@ -587,12 +587,17 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
         return nr > 0 ? ggp_predict_rows(F.gpu, lo, std::min(nr, lo + span), b->data()) : GGP_OK;
     };
     int fr = fetch(0, buf[0]);
+    std::string fmsg = fr == GGP_OK ? "" : ggp_strerror(fr);   // the engine's message is per thread
     for (int64_t lo = 0, k = 0; lo < nr; lo += span, ++k) {
-        if (fr != GGP_OK) throw std::runtime_error(std::string("ggp_predict_rows: ") + ggp_strerror(fr));
+        if (fr != GGP_OK) throw std::runtime_error("ggp_predict_rows: " + fmsg);
         const int64_t hi = std::min(nr, lo + span);
         const double *rows = buf[k & 1]->data();
         std::thread next;
-        if (hi < nr) next = std::thread([&, hi, k] { fr = fetch(hi, buf[(k + 1) & 1]); });
+        if (hi < nr)
+            next = std::thread([&, hi, k] {
+                fr = fetch(hi, buf[(k + 1) & 1]);
+                if (fr != GGP_OK) fmsg = ggp_strerror(fr);   // read on the thread that set it
+            });
         struct Join {   // the prefetch joins on every way out of this span (a throw included)
             std::thread &t;
             ~Join()
