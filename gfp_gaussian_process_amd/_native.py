@@ -56,6 +56,8 @@ ENGINE_SYMBOLS = {
     "ggp_forest_destroy": (None, [ctypes.c_void_p]),
     "ggp_total_loglik": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p, c_int64_p, c_int64_p]),
     "ggp_total_loglik_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, c_double_p, c_double_p, c_int32_p]),
+    "ggp_total_loglik_chain": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, c_double_p, c_double_p, c_int32_p,
+                                              c_int64_p, c_int64_p]),
     "ggp_total_loglik_async": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "ggp_loglik_result": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_int64_p, c_int64_p]),
     "ggp_predict": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, c_double_p,

@@ -90,6 +90,18 @@ GGP_DEV void load_dawson_table(double *s_tab, int lane)
 // root's state from the previous evaluation (carried state).  Daughter: a copy of the
 // parent's final posterior, to be propagated over dt and mapped through the division.
 // ------------------------------------------------------------------------------------------
+GGP_DEV void root_init(const DevForest &F, const double *p, double *m, double *C)
+{
+    m[0] = F.root_mean0;
+    m[1] = F.root_mean1;
+    C[0] = F.root_var0;
+    C[5] = F.root_var1;
+    m[2] = p[0];
+    m[3] = p[3];
+    C[10] = p[2] / (2. * p[1]);
+    C[15] = p[5] / (2. * p[4]);
+}
+
 GGP_DEV bool cell_prologue(const DevForest &F, const double *p, const double *state, int c,
                            int64_t r0, double *m, double *C, double &dt_div)
 {
@@ -98,14 +110,7 @@ GGP_DEV bool cell_prologue(const DevForest &F, const double *p, const double *st
         const double *st = state + (size_t)20 * c;
 #pragma unroll
         for (int k = 0; k < 16; ++k) C[k] = st[4 + k];
-        m[0] = F.root_mean0;
-        m[1] = F.root_mean1;
-        C[0] = F.root_var0;
-        C[5] = F.root_var1;
-        m[2] = p[0];
-        m[3] = p[3];
-        C[10] = p[2] / (2. * p[1]);
-        C[15] = p[5] / (2. * p[4]);
+        root_init(F, p, m, C);
         dt_div = 0.0;
         return false;
     }
@@ -813,11 +818,12 @@ GGP_DEV void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
+template <bool CHAIN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
     const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed *__restrict__ red, const int64_t call_seq,
-    const unsigned spin_max)
+    const unsigned spin_max, const double *__restrict__ ptab, const double *__restrict__ carry)
 {
     namespace W = ggp::wave;
     [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // GGP_STAMPS builds only
@@ -828,6 +834,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     lds_fill<W::kTabRows * W::kTabRow>(lds + W::L_TAB, lane, [](const int k) { return W::tab_entry(k); });
     GGP_PSTAMP(1);
     const double *p = P.p;
+    // chained evaluations (ggp_total_loglik_chain): blockIdx.y = point; the point's parameter row
+    // and its state / ll / NaN / done slices of n cells each
+    const int pt = CHAIN ? (int)blockIdx.y : 0;
+    if constexpr (CHAIN) {
+        p = ptab + 11 * pt;
+        state += (size_t)20 * n * pt;
+        cell_ll += (size_t)n * pt;
+        cell_nan += (size_t)n * pt;
+        cell_done += (size_t)n * pt;
+    }
     const W::LaneC LC = W::kLaneTab.l[lane];   // this lane's row of the compile-time table
     W::Lane L;
     {
@@ -915,16 +931,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const int c = cells[i];
         const int2 ch = chain[c];
         bool chain_broken = false;
-        if (ch.x >= 0 && __hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            // the parent runs in this launch and is not done: sleep through ~0.5 us per parent row
+        // the cell to wait for: a second daughter's parent; in a chain also a root's own state at
+        // the end of the previous point (its carried state)
+        int wc = ch.x;
+        const unsigned *wdone = cell_done;
+        bool carried_prev = false, publish = ch.y != 0;
+        if constexpr (CHAIN) {
+            const bool root = F.parent[c] < 0;
+            carried_prev = root && pt > 0;
+            publish = publish || (root && pt + 1 < (int)gridDim.y);
+            if (carried_prev) {
+                wc = c;
+                wdone = cell_done - n;
+            }
+        }
+        if (wc >= 0 && __hip_atomic_load(wdone + wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            // the cell runs in this launch and is not done: sleep through ~0.5 us per row of it
             // without polling, then poll (relaxed agent-scope loads); spin_max polls at most
             if (spin_max > 0) {
                 const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-                const unsigned long long quiet = (unsigned long long)(F.row_off[ch.x + 1] - F.row_off[ch.x]) * kChainQuietPerRow;
+                const unsigned long long quiet = (unsigned long long)(F.row_off[wc + 1] - F.row_off[wc]) * kChainQuietPerRow;
                 while (__builtin_amdgcn_s_memtime() - t_start < quiet) __builtin_amdgcn_s_sleep(127);
             }
             unsigned spins = 0;
-            while (__hip_atomic_load(cell_done + ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            while (__hip_atomic_load(wdone + wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
                 if (++spins > spin_max) {
                     chain_broken = true;
                     break;
@@ -948,7 +978,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
         } else {
             double m[4], C[16];
-            pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+            if (CHAIN && carried_prev) {   // a root: the previous point's final state of it (coherent loads)
+                const double *st = state - (size_t)20 * n + (size_t)20 * c;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) C[k] = ld_agent(st + 4 + k);
+                root_init(F, p, m, C);
+                pending = false;
+            } else {
+                pending = cell_prologue(F, p, CHAIN && F.parent[c] < 0 ? carry : state, c, r0, m, C, dt);
+            }
             scatter(m, C);
         }
         const bool divide = pending;
@@ -1115,12 +1153,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         if (lane < 20) {
             const double v = lds[W::L_POST + lane];
-            if (ch.y)
+            if (publish)
                 st_agent(state + (size_t)20 * c + lane, v);
             else
                 state[(size_t)20 * c + lane] = v;
         }
-        if (ch.y) {
+        if (publish) {
             __builtin_amdgcn_s_waitcnt(0);   // every lane's stores at the coherence point, then the flag
             if (lane == 0) __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2148,6 +2186,7 @@ struct Shard {
     double *d_b_ptab = nullptr, *d_b_state = nullptr, *d_b_ll = nullptr, *d_b_sum = nullptr;
     int32_t *d_b_nan = nullptr;
     int64_t *d_b_code = nullptr;
+    unsigned *d_b_done = nullptr;   // ggp_total_loglik_chain: per point, the cells' done flags
     int64_t b_cap = 0;   // points the workspace holds
     // -j: the smoother and the per-row joint tables, kept for the parameters they were made with
     // (the CLI asks for many start-row ranges with the same parameters)
@@ -2253,9 +2292,10 @@ int launch_levels(Shard *f, const ggp_params &P)
     };
     if (f->n_paths > 0) {   // every level on the wave schedule: one launch, one block per path
         HIPCHK(prof_begin());
-        hipLaunchKernelGGL(k_loglik_wave, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
+        hipLaunchKernelGGL(k_loglik_wave<false>, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
                            f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
-                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max);
+                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max,
+                           (const double *)nullptr, (const double *)nullptr);
         HIPCHK(hipGetLastError());
         f->kernel_used = GGP_KERNEL_WAVE;
         f->last_code = GGP_KERNEL_WAVE << 8 | 64;
@@ -2270,9 +2310,10 @@ int launch_levels(Shard *f, const ggp_params &P)
         const int64_t n_simd = (int64_t)f->n_cu * 4;
         const int kind = f->level_kind[L];
         if (kind == GGP_KERNEL_WAVE) {
-            hipLaunchKernelGGL(k_loglik_wave, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
+            hipLaunchKernelGGL(k_loglik_wave<false>, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
                                f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
-                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max);
+                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max,
+                               (const double *)nullptr, (const double *)nullptr);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
         } else if (kind == GGP_KERNEL_PAIR) {
@@ -2431,11 +2472,12 @@ void shard_free_joints(Shard *f)
 void batch_free(Shard *f)
 {
     for (void *p : {(void *)f->d_b_ptab, (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_sum,
-                    (void *)f->d_b_nan, (void *)f->d_b_code})
+                    (void *)f->d_b_nan, (void *)f->d_b_code, (void *)f->d_b_done})
         if (p) (void)hipFree(p);
     f->d_b_ptab = f->d_b_state = f->d_b_ll = f->d_b_sum = nullptr;
     f->d_b_nan = nullptr;
     f->d_b_code = nullptr;
+    f->d_b_done = nullptr;
     f->b_cap = 0;
 }
 
@@ -2691,7 +2733,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             all_wave = all_wave && f->level_kind[L] == GGP_KERNEL_WAVE;
         }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave, 64, 0) == hipSuccess && per_cu > 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave<false>, 64, 0) == hipSuccess && per_cu > 0)
             f->wave_resident = per_cu * f->n_cu;
         if (const char *e = getenv("GGP_WAVE_PATHS_MAX")) f->wave_resident = atoi(e);
         std::vector<int2> ch(nc, int2{-1, 0});
@@ -3502,6 +3544,39 @@ int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *n
 // launch of the lane schedule with blockIdx.y = point, then the block sums of every point.
 static constexpr int64_t kBatchBytes = int64_t(4) << 30;
 
+// the per-point workspace of a batch or chain call, for up to min(n_pts, what keeps a shard's
+// slices under kBatchBytes) points; returns that chunk (<= 0: an error code, negated)
+static int64_t batch_reserve(ggp_forest *f, int32_t n_pts)
+{
+    int64_t chunk = std::min<int64_t>((int64_t)n_pts, 65535);
+    if (const char *e = std::getenv("GGP_BATCH_CHUNK"))   // tests: chunk boundaries
+        if (std::atoll(e) > 0) chunk = std::min<int64_t>(chunk, std::atoll(e));
+    for (Shard *s : f->shards)
+        if (s->n_cells) chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, kBatchBytes / (s->n_cells * (20 * 8 + 8 + 4 + 4))));
+    for (Shard *s : f->shards) {
+        if (!s->n_cells || chunk <= s->b_cap) continue;
+        if (hipSetDevice(s->device) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+            g_last_err = "HIP error before the batch workspace";
+            return -GGP_EDEV;
+        }
+        batch_free(s);
+        int rc = GGP_OK;
+        auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
+        const int64_t nc = s->n_cells;
+        check(dev_upload<double>(&s->d_b_ptab, nullptr, (size_t)chunk * 11));
+        check(dev_upload<double>(&s->d_b_state, nullptr, (size_t)chunk * nc * 20));
+        check(dev_upload<double>(&s->d_b_ll, nullptr, (size_t)chunk * nc));
+        check(dev_upload<int32_t>(&s->d_b_nan, nullptr, (size_t)chunk * nc));
+        check(dev_upload<double>(&s->d_b_sum, nullptr, (size_t)chunk * s->n_lblocks));
+        check(dev_upload<int64_t>(&s->d_b_code, nullptr, (size_t)chunk * s->n_lblocks));
+        check(dev_upload<unsigned>(&s->d_b_done, nullptr, (size_t)chunk * nc));
+        if (rc == GGP_OK && hipMemset(s->d_b_done, 0, (size_t)chunk * nc * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
+        if (rc != GGP_OK) { batch_free(s); return -rc; }
+        s->b_cap = chunk;
+    }
+    return chunk;
+}
+
 int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *status)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
@@ -3514,26 +3589,8 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
         for (int32_t i = 0; i < n_pts; ++i) { ll[i] = 0.0; status[i] = GGP_OK; }
         return GGP_OK;
     }
-    int64_t chunk = std::min<int64_t>((int64_t)n_pts, 65535);
-    for (Shard *s : f->shards)
-        if (s->n_cells) chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, kBatchBytes / (s->n_cells * (20 * 8 + 8 + 4))));
-    for (Shard *s : f->shards) {
-        if (!s->n_cells || chunk <= s->b_cap) continue;
-        HIPCHK(hipSetDevice(s->device));
-        HIPCHK(hipStreamSynchronize(s->stream));
-        batch_free(s);
-        int rc = GGP_OK;
-        auto check = [&](int r) { if (r != GGP_OK && rc == GGP_OK) rc = r; };
-        const int64_t nc = s->n_cells;
-        check(dev_upload<double>(&s->d_b_ptab, nullptr, (size_t)chunk * 11));
-        check(dev_upload<double>(&s->d_b_state, nullptr, (size_t)chunk * nc * 20));
-        check(dev_upload<double>(&s->d_b_ll, nullptr, (size_t)chunk * nc));
-        check(dev_upload<int32_t>(&s->d_b_nan, nullptr, (size_t)chunk * nc));
-        check(dev_upload<double>(&s->d_b_sum, nullptr, (size_t)chunk * s->n_lblocks));
-        check(dev_upload<int64_t>(&s->d_b_code, nullptr, (size_t)chunk * s->n_lblocks));
-        if (rc != GGP_OK) { batch_free(s); return rc; }
-        s->b_cap = chunk;
-    }
+    const int64_t chunk = batch_reserve(f, n_pts);
+    if (chunk <= 0) return (int)-chunk;
     const size_t ns = f->shards.size();
     std::vector<std::vector<double>> sums(ns);
     std::vector<std::vector<int64_t>> codes(ns);
@@ -3592,6 +3649,110 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
             bad = bad || std::isnan(v);
             status[p0 + i] = bad ? GGP_ENAN : GGP_OK;
             ll[p0 + i] = bad ? std::nan("") : v;
+        }
+    }
+    return GGP_OK;
+}
+
+// Chained objective: n_pts evaluations in order, each from the carried state the previous one
+// left -- bitwise n_pts ggp_total_loglik calls (the reference's own sequences: num_hessian_ll's
+// 4k^2 calls, likelihood.h:211-258; the -s scan, main.cpp:80-114).  Only a root's state crosses
+// from one evaluation to the next (init_sc_distribution keeps its off-diagonals,
+// predictions.h:63-82), so on path-launch shards one k_loglik_wave<true> launch runs a chunk of
+// points (blockIdx.y = point): a root of point i waits for the same root of point i - 1, every
+// other cell only for its parent within its point, and the points' trees overlap on the device.
+// Per point: k_reduce_blocks' sums (bitwise the in-launch reduction) and the host's top_sum.
+// Other handles (level launches, a communicator) run the calls one by one.
+int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *n_ok,
+                           int64_t *nan_cell, int64_t *nan_row)
+{
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
+    if (!f || n_pts < 0 || !n_ok || (n_pts > 0 && (!params || !ll))) {
+        g_last_err = "ggp_total_loglik_chain: bad arguments";
+        return GGP_EINVAL;
+    }
+    *n_ok = 0;
+    if (nan_cell) *nan_cell = -1;
+    if (nan_row) *nan_row = -1;
+    bool fused = f->comm == nullptr;
+    if (const char *e = std::getenv("GGP_CHAIN_FUSED")) fused = fused && std::atoi(e) != 0;
+    for (Shard *s : f->shards)
+        if (s->n_cells && s->n_paths == 0) fused = false;
+    if (!fused || f->n_cells == 0) {
+        for (int32_t i = 0; i < n_pts; ++i) {
+            const int rc = ggp_total_loglik(f, params + (size_t)11 * i, ll + i, nan_cell, nan_row);
+            if (rc != GGP_OK) return rc;
+            *n_ok = i + 1;
+        }
+        return GGP_OK;
+    }
+    if (n_pts == 0) return GGP_OK;
+    const int64_t chunk = batch_reserve(f, n_pts);
+    if (chunk <= 0) return (int)-chunk;
+    const size_t ns = f->shards.size();
+    std::vector<std::vector<double>> sums(ns);
+    std::vector<std::vector<int64_t>> codes(ns);
+    ggp_params P0{};
+    for (int64_t p0 = 0; p0 < n_pts; p0 += chunk) {
+        const int64_t np = std::min<int64_t>(chunk, n_pts - p0);
+        for (size_t k = 0; k < ns; ++k) {   // enqueue every shard
+            Shard *s = f->shards[k];
+            if (!s->n_cells) continue;
+            const int64_t nc = s->n_cells;
+            HIPCHK(hipSetDevice(s->device));
+            HIPCHK(hipMemcpyAsync(s->d_b_ptab, params + 11 * p0, (size_t)np * 11 * sizeof(double),
+                                  hipMemcpyHostToDevice, s->stream));
+            ++s->epoch;
+            hipLaunchKernelGGL(k_loglik_wave<true>, dim3((unsigned)s->n_paths, (unsigned)np), dim3(64), 0, s->stream, s->F,
+                               P0, s->d_path_cells, (int)nc, s->d_b_state, s->d_b_ll, s->d_b_nan, s->d_chain, s->d_b_done,
+                               s->epoch, s->d_path_seq, (const ChainRed *)nullptr, (int64_t)0, s->spin_max,
+                               (const double *)s->d_b_ptab, (const double *)s->d_state);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,
+                               s->stream, nc, s->d_b_ll, s->d_b_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt,
+                               s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
+                               (int64_t *)nullptr, (int64_t)0, (double *)nullptr, (int64_t *)nullptr);
+            HIPCHK(hipGetLastError());
+            // the carried state: the chunk's last point (every cell, as its sequential call leaves it)
+            HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)(np - 1) * nc * 20, (size_t)nc * 20 * sizeof(double),
+                                  hipMemcpyDeviceToDevice, s->stream));
+            sums[k].resize((size_t)np * s->n_lblocks);
+            codes[k].resize((size_t)np * s->n_lblocks);
+            HIPCHK(hipMemcpyAsync(sums[k].data(), s->d_b_sum, sums[k].size() * sizeof(double), hipMemcpyDeviceToHost,
+                                  s->stream));
+            HIPCHK(hipMemcpyAsync(codes[k].data(), s->d_b_code, codes[k].size() * sizeof(int64_t),
+                                  hipMemcpyDeviceToHost, s->stream));
+        }
+        for (Shard *s : f->shards) {
+            if (!s->n_cells) continue;
+            HIPCHK(hipSetDevice(s->device));
+            HIPCHK(hipStreamSynchronize(s->stream));
+        }
+        for (int64_t i = 0; i < np; ++i) {   // ggp_loglik_result, per point
+            std::vector<double> blocks((size_t)f->n_blocks, 0.0);
+            long long code = kNoNan;
+            for (size_t k = 0; k < ns; ++k) {
+                const Shard *s = f->shards[k];
+                for (int64_t j = 0; j < s->n_lblocks; ++j) {
+                    blocks[(size_t)s->blk_global[j]] = sums[k][(size_t)(i * s->n_lblocks + j)];
+                    code = std::min<long long>(code, codes[k][(size_t)(i * s->n_lblocks + j)]);
+                }
+            }
+            const double v = top_sum(std::move(blocks));
+            if (code != kNoNan) {
+                const int64_t rank = code >> 24, row = code & 0xffffff;
+                if (nan_cell) *nan_cell = f->dfs_order[rank];
+                if (nan_row) *nan_row = row == kRowStall ? -1 : row;
+                ll[p0 + i] = std::nan("");
+                if (row == kRowStall) {
+                    g_last_err = "evaluation stalled: a cell's wait for the cell it depends on timed out (a scheduling stall, not a NaN)";
+                    return GGP_ETIMEOUT;
+                }
+                return GGP_ENAN;
+            }
+            ll[p0 + i] = v;
+            if (std::isnan(v)) return GGP_ENAN;   // NaN from +inf + -inf across cells
+            *n_ok = (int32_t)(p0 + i + 1);
         }
     }
     return GGP_OK;

@@ -255,11 +255,10 @@ void log_iteration(const std::vector<double> &p, double tl, int iteration)
 }
 
 // +ll; throws std::domain_error("Likelihood is Nan") after the reference's side effects
-double total_likelihood(const std::vector<double> &params, Objective &o)
+// what total_likelihood does after an evaluation (likelihood.h:71-93, 137-158): the NaN log and
+// exception, the iteration count, the -m iteration log and the print-level line
+double account(const std::vector<double> &params, Objective &o, int rc, double ll, int64_t nc, int64_t nr)
 {
-    double ll = 0;
-    int64_t nc = -1, nr = -1;
-    const int rc = ggp_total_loglik(o.forest, params.data(), &ll, &nc, &nr);
     if (rc == GGP_ENAN) {
         if (g_save_ll) log_iteration(params, ll, g_iteration + 1);
         g_log << "\n(sc_likelihood) ERROR: Log likelihood is Nan\n";
@@ -281,6 +280,34 @@ double total_likelihood(const std::vector<double> &params, Objective &o)
         std::cout << g_iteration << ": ";
         for (double v : params) std::cout << std::setprecision(20) << v << ", ";
         std::cout << "ll=" << std::setprecision(30) << ll << std::setprecision(15) << "\n";
+    }
+    return ll;
+}
+
+double total_likelihood(const std::vector<double> &params, Objective &o)
+{
+    double ll = 0;
+    int64_t nc = -1, nr = -1;
+    const int rc = ggp_total_loglik(o.forest, params.data(), &ll, &nc, &nr);
+    return account(params, o, rc, ll, nc, nr);
+}
+
+// a known sequence of total_likelihood calls (each from the state the previous left) as one
+// ggp_total_loglik_chain call: the same values, log lines and exceptions, point by point
+std::vector<double> total_likelihood_chain(const std::vector<double> &pts, Objective &o)
+{
+    const int32_t n = (int32_t)(pts.size() / GGP_N_PARAMS);
+    std::vector<double> ll((size_t)n, 0.0);
+    int32_t n_ok = 0;
+    int64_t nc = -1, nr = -1;
+    const int rc = ggp_total_loglik_chain(o.forest, n, pts.data(), ll.data(), &n_ok, &nc, &nr);
+    auto point = [&](int32_t i) {
+        return std::vector<double>(pts.begin() + (size_t)i * GGP_N_PARAMS, pts.begin() + (size_t)(i + 1) * GGP_N_PARAMS);
+    };
+    for (int32_t i = 0; i < n_ok; ++i) account(point(i), o, GGP_OK, ll[(size_t)i], -1, -1);
+    if (rc != GGP_OK) {
+        if (n_ok < n) account(point(n_ok), o, rc, ll[(size_t)n_ok], nc, nr);   // throws
+        throw std::runtime_error(std::string("GPU likelihood failed: ") + ggp_strerror(rc));
     }
     return ll;
 }
@@ -364,11 +391,14 @@ double minimize(Objective &o, Params &P, double tolerance, bool log_space)
 // -hb (additive, opt-in): num_hessian_ll's 4 k^2 points (likelihood.h:211-258, same order, steps
 // and expression as ggp_num_hessian) in one ggp_total_loglik_batch call, each point from the
 // carried state left by the optimiser instead of chained from point to point
-void num_hessian_batched(Objective &o, const std::vector<double> &x, const std::vector<int> &idx, double epsilon,
-                         std::vector<double> &H)
+// num_hessian_ll's points (likelihood.h:211-258): for i, j of the free parameters, x +- h_i e_i
+// +- h_j e_j in the order ++, +-, -+, --, h = max(x epsilon, 1e-12) (the steps of ggp_num_hessian)
+void hessian_points(const std::vector<double> &x, const std::vector<int> &idx, double epsilon, std::vector<double> &h,
+                    std::vector<double> &pts)
 {
     const int k = (int)idx.size();
-    std::vector<double> h(k), pts;
+    h.assign((size_t)k, 0.0);
+    pts.clear();
     for (int a = 0; a < k; ++a) h[a] = std::max(x[idx[a]] * epsilon, 1e-12);
     for (int a = 0; a < k; ++a)
         for (int b = 0; b < k; ++b)
@@ -379,6 +409,14 @@ void num_hessian_batched(Objective &o, const std::vector<double> &x, const std::
                 xx[jj] = q % 2 == 0 ? xx[jj] + h[b] : xx[jj] - h[b];
                 pts.insert(pts.end(), xx.begin(), xx.end());
             }
+}
+
+void num_hessian_batched(Objective &o, const std::vector<double> &x, const std::vector<int> &idx, double epsilon,
+                         std::vector<double> &H)
+{
+    const int k = (int)idx.size();
+    std::vector<double> h, pts;
+    hessian_points(x, idx, epsilon, h, pts);
     const int n = 4 * k * k;
     std::vector<double> ll(n);
     std::vector<int32_t> st(n);
@@ -404,7 +442,6 @@ std::vector<double> ll_error_bars(Params &P, Objective &o, double epsilon)
     const std::vector<double> x = P.get_final();
     const std::vector<int> idx = P.non_fixed();
     const int k = (int)idx.size();
-    std::vector<int32_t> idx32(idx.begin(), idx.end());
     std::vector<double> H((size_t)k * k), Hi((size_t)k * k);
     if (g_batched_hessian) {
         num_hessian_batched(o, x, idx, epsilon, H);
@@ -413,14 +450,16 @@ std::vector<double> ll_error_bars(Params &P, Objective &o, double epsilon)
         for (int i = 0; i < k; ++i) err.push_back(-Hi[(size_t)i * k + i]);
         return err;
     }
-    struct Ctx { Objective *o; } ctx{&o};
-    auto cb = [](const double *xx, double *v, void *data) -> int {
-        auto *c = static_cast<Ctx *>(data);
-        *v = total_likelihood(std::vector<double>(xx, xx + GGP_N_PARAMS), *c->o);
-        return 0;
-    };
-    if (ggp_num_hessian(GGP_N_PARAMS, cb, &ctx, x.data(), idx32.data(), k, epsilon, H.data()) != GGP_OK)
-        throw std::runtime_error(ggp_host_last_error());
+    // num_hessian_ll's 4 k^2 calls, chained through the carried state as the reference makes them,
+    // in one ggp_total_loglik_chain call; H as ggp_num_hessian forms it
+    std::vector<double> h((size_t)k), pts;
+    hessian_points(x, idx, epsilon, h, pts);
+    const std::vector<double> ll = total_likelihood_chain(pts, o);
+    for (int a = 0; a < k; ++a)
+        for (int b = 0; b < k; ++b) {
+            const double *l = &ll[(size_t)4 * (a * k + b)];
+            H[(size_t)a * k + b] = (l[0] - l[1] - l[2] + l[3]) / (4 * h[a] * h[b]);
+        }
     ggp_inverse_pplu(k, H.data(), Hi.data());
     std::vector<double> err;
     for (int i = 0; i < k; ++i) err.push_back(-Hi[(size_t)i * k + i]);
@@ -503,10 +542,12 @@ void run_bound_1dscan(Objective &o, const Params &P, std::map<std::string, std::
             file << "log_likelihood" << "\n";
         }
         g_log << "Outfile: " << outfile << "\n";
+        std::vector<double> pts;   // the scan's calls, chained as the reference makes them
         for (double v : arange<double>(P.p.lower[i], P.p.upper[i], P.p.step[i])) {
             pv[i] = v;
-            total_likelihood(pv, o);
+            pts.insert(pts.end(), pv.begin(), pv.end());
         }
+        total_likelihood_chain(pts, o);
     }
     g_save_ll = false;
 }

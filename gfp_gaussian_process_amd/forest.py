@@ -504,6 +504,32 @@ class Forest:
                                                      st.ctypes.data_as(N.c_int32_p)))
         return ll, st == N.GGP_ENAN
 
+    def total_likelihood_chain(self, params_points) -> np.ndarray:
+        """+ll of every parameter point (rows of an [n, 11] array) in order, each from the carried
+        state the previous one left (ggp_total_loglik_chain): bitwise n successive
+        total_likelihood calls, run as one chained launch where the handle allows.  A failing
+        point raises what total_likelihood would (LikelihoodIsNan / EvaluationStalled), with
+        .point = its index and .ll = the values of the points before it."""
+        p = np.ascontiguousarray(np.atleast_2d(params_points), np.float64)
+        if p.ndim != 2 or p.shape[1] != N.N_PARAMS:
+            raise ValueError(f"expected [n, {N.N_PARAMS}] parameter points, got {p.shape}")
+        self._usable()
+        ll = np.zeros(p.shape[0])
+        n_ok, nc, nr = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        rc = self._lib.ggp_total_loglik_chain(self._h, p.shape[0], p.ctypes.data_as(N.c_double_p),
+                                              ll.ctypes.data_as(N.c_double_p), ctypes.byref(n_ok),
+                                              ctypes.byref(nc), ctypes.byref(nr))
+        if rc in (N.GGP_ENAN, N.GGP_ETIMEOUT):
+            try:
+                if rc == N.GGP_ENAN:
+                    raise self._nan(nc.value, nr.value)
+                self._stalled(rc)
+            except GGPError as e:
+                e.point, e.ll = int(n_ok.value), ll[:n_ok.value].copy()
+                raise
+        self._check(rc)
+        return ll
+
     def reset_state(self) -> None:
         self._check(self._lib.ggp_reset_state(self._h))
         self._poisoned = False

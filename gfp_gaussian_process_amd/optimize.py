@@ -90,7 +90,31 @@ def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, 
     return (np.exp(xb) if log else xb), -minf, rc
 
 
+def _chain_forest(objective):
+    """the Forest behind an objective that is a Forest or its bound total_likelihood (whose
+    known call sequences can run as one ggp_total_loglik_chain call), else None"""
+    if hasattr(objective, "total_likelihood_chain"):
+        return objective
+    owner = getattr(objective, "__self__", None)
+    if owner is not None and hasattr(owner, "total_likelihood_chain") and \
+            getattr(objective, "__name__", "") == "total_likelihood":
+        return owner
+    return None
+
+
 def num_hessian(objective, x, idx, epsilon: float) -> np.ndarray:
+    """num_hessian_ll (likelihood.h:211-258): H[i, j] = (l++ - l+- - l-+ + l--) / (4 h_i h_j) over
+    its 4 k^2 calls in its order, each from the carried state the previous left.  A Forest
+    objective runs them as one chained call (bitwise the call-by-call form, ggp_num_hessian)."""
+    forest = _chain_forest(objective)
+    if forest is not None:
+        pts, h = hessian_points(x, idx, epsilon)
+        q = forest.total_likelihood_chain(pts).reshape(len(h), len(h), 4)
+        out = np.zeros((len(h), len(h)))
+        for i in range(len(h)):
+            for j in range(len(h)):
+                out[i, j] = (q[i, j, 0] - q[i, j, 1] - q[i, j, 2] + q[i, j, 3]) / (4 * h[i] * h[j])
+        return out
     x = np.ascontiguousarray(x, np.float64)
     idx32 = np.ascontiguousarray(idx, np.int32)
     k = idx32.size
@@ -175,11 +199,18 @@ def bound_1dscan(objective, params: ParameterSet, final=None) -> dict:
     along arange(lower, upper, step) with the others at their final (else init) values.
     Returns {name: [(value, log_likelihood), ...]} in evaluation order."""
     base = np.asarray(params.init if final is None else final, np.float64)
+    forest = _chain_forest(objective)   # a Forest: each parameter's calls as one chained call
     out = {}
     for i in params.bound():
         pv = base.copy()
+        vals = arange(params.lower[i], params.upper[i], params.step[i])
+        if forest is not None:
+            pts = np.repeat(pv[None, :], len(vals), axis=0)
+            pts[:, i] = vals
+            out[params.names[i]] = list(zip(vals, forest.total_likelihood_chain(pts).tolist()))
+            continue
         rows = []
-        for v in arange(params.lower[i], params.upper[i], params.step[i]):
+        for v in vals:
             pv[i] = v
             rows.append((v, objective(pv.copy())))
         out[params.names[i]] = rows

@@ -10,6 +10,9 @@
  *                                total_likelihood_log_params         likelihood.h:161-167:
  *                                the caller negates / exponentiates)
  *                               incl. likelihood_recr / sc_likelihood likelihood.h:36-122
+ *   ggp_total_loglik_chain  a known sequence of total_likelihood calls, each from the state
+ *                               the previous left: num_hessian_ll's 4k^2  likelihood.h:211-258
+ *                               calls, the -s scan's                      main.cpp:80-114
  *   ggp_total_loglik_batch  the 4k^2 objective calls of num_hessian_ll   likelihood.h:211-258
  *                               (opt-in: points independent, not chained)
  *   ggp_joints        replaces  collect_joint_distributions (compute) correlation_tree.h:464-651
@@ -142,6 +145,18 @@ int ggp_total_loglik(ggp_forest *f, const double *params, double *ll, int64_t *n
  * GGP_EINVAL, GGP_ENOMEM or GGP_EDEV. */
 int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll,
                            int32_t *status);
+
+/* Chained objective: n_pts evaluations (params: n_pts*11 doubles) in order, each from the carried
+ * state the previous one left -- the results, the NaN location and the carried state afterwards
+ * are bitwise those of n_pts successive ggp_total_loglik calls.  ll[i] receives point i's +ll.
+ * Stops at the first point whose evaluation fails: returns its code (GGP_ENAN / GGP_ETIMEOUT,
+ * ll = NaN, nan_cell / nan_row as ggp_total_loglik reports them) with *n_ok = its index; else
+ * GGP_OK with *n_ok = n_pts.  Only a root's state crosses from one evaluation to the next
+ * (predictions.h:63-82), so on a path-launch handle (every level on the wave schedule) the points
+ * run in one launch per chunk, point i's root waiting for point i-1's and its trees overlapping
+ * with the later points'; other handles run the calls one by one (GGP_CHAIN_FUSED=0: always). */
+int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll,
+                           int32_t *n_ok, int64_t *nan_cell, int64_t *nan_row);
 
 /* Asynchronous form for drivers that pipeline: enqueue one evaluation on the handle's
  * stream; ggp_loglik_result() waits and returns what ggp_total_loglik would have. */

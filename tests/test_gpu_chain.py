@@ -1,0 +1,163 @@
+"""ggp_total_loglik_chain: a known sequence of objective calls, each from the carried state the
+previous one left (num_hessian_ll's 4k^2 calls, likelihood.h:211-258; the -s scan, main.cpp:80-114),
+in one chained launch.  The bar is bitwise: every value, the NaN location and the carried state
+afterwards equal those of the same calls made one by one through ggp_total_loglik (which the
+parity tests hold against the oracle at 1e-9); one oracle check on top.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("built")]
+
+PARAMS = json.load(open(os.path.join(GOLDEN, "oracle_example.json")))
+P0 = np.array([float.fromhex(x) for x in PARAMS["scaled/binomial/example"]["params"]])
+
+
+def _points(n, seed=5, scale=0.02):
+    rng = np.random.default_rng(seed)
+    return np.stack([P0 * (1.0 + scale * rng.standard_normal(P0.size)) for _ in range(n)])
+
+
+@pytest.fixture(scope="module")
+def example(example_paths):
+    import gfp_gaussian_process_amd as g
+    return g.HostForest.from_csv(example_paths["csv"], example_paths["config"])
+
+
+def _sequential(hf, pts, warm=1, **kw):
+    import gfp_gaussian_process_amd as g
+    f = g.Forest(hf, **kw)
+    for _ in range(warm):
+        f.total_likelihood(P0)
+    ll = np.array([f.total_likelihood(p) for p in pts])
+    return ll, f.state()
+
+
+def _chained(hf, pts, warm=1, **kw):
+    import gfp_gaussian_process_amd as g
+    f = g.Forest(hf, **kw)
+    for _ in range(warm):
+        f.total_likelihood(P0)
+    ll = f.total_likelihood_chain(pts)
+    return ll, f.state(), f
+
+
+def test_chain_bitwise_sequential_on_the_example(example):
+    """the reference's example (one tree, 77 cells, path launch): 40 points chained through the
+    root's carried state; values and the state afterwards bitwise the one-by-one calls, and the
+    handle continues the chain like a handle that made the calls itself"""
+    pts = _points(40)
+    want, st_want = _sequential(example, pts)
+    got, st_got, f = _chained(example, pts)
+    assert np.array_equal(got, want)
+    assert np.array_equal(st_got, st_want)
+    import gfp_gaussian_process_amd as g
+    h = g.Forest(example)
+    h.set_state(st_want)
+    assert f.total_likelihood(P0) == h.total_likelihood(P0)
+
+
+def test_chain_fresh_state_vs_oracle(example):
+    """from fresh cells (read_data's zero state), the chained values against the oracle's own
+    chained calls at 1e-9"""
+    from oracle import oracle as O
+    pts = _points(6, seed=9)
+    got, _, _ = _chained(example, pts, warm=0)
+    of = O.OracleForest(example.a)
+    for k, p in enumerate(pts):
+        vo, nc, _ = of.total_likelihood(p)
+        assert nc == -1
+        assert abs(got[k] - vo) / abs(vo) < 1e-9, k
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0, 0)])
+def test_chain_many_trees_and_shards(devices):
+    """a 48-tree forest (roots, first and second daughters: waits within a point and across
+    points), whole or in three logical shards: bitwise the sequential calls"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(48, 120)
+    pts = _points(25, seed=2)
+    want, st_want = _sequential(hf, pts, devices=list(devices))
+    got, st_got, _ = _chained(hf, pts, devices=list(devices))
+    assert np.array_equal(got, want)
+    assert np.array_equal(st_got, st_want)
+
+
+def test_chain_chunks(example, monkeypatch):
+    """points split over launches (GGP_BATCH_CHUNK=7: the carried state handed from one chunk's
+    last point to the next chunk's first) give the same bits"""
+    pts = _points(23, seed=4)
+    want, st_want = _sequential(example, pts)
+    monkeypatch.setenv("GGP_BATCH_CHUNK", "7")
+    got, st_got, _ = _chained(example, pts)
+    assert np.array_equal(got, want)
+    assert np.array_equal(st_got, st_want)
+
+
+def test_chain_level_launch_handles_run_one_by_one(example, monkeypatch):
+    """handles without the path launch (lane schedule; GGP_CHAIN_FUSED=0) take the call-by-call
+    form: the same values"""
+    pts = _points(5, seed=8)
+    want, _ = _sequential(example, pts, kernel="lane")
+    got, _, _ = _chained(example, pts, kernel="lane")
+    assert np.array_equal(got, want)
+    want_w, _ = _sequential(example, pts)
+    monkeypatch.setenv("GGP_CHAIN_FUSED", "0")
+    got_w, _, _ = _chained(example, pts)
+    assert np.array_equal(got_w, want_w)
+
+
+def test_chain_stops_at_the_first_nan_point(example):
+    """a NaN point (var_lambda < 0) raises LikelihoodIsNan with the sequential call's cell and
+    row; .point is its index and .ll the values before it, bitwise the sequential ones; the
+    handle then refuses to evaluate until its state is reset (include/ggp.h "Errors")"""
+    import gfp_gaussian_process_amd as g
+    pts = _points(9, seed=3)
+    pts[6, 2] = -1.0
+    f = g.Forest(example)
+    f.total_likelihood(P0)
+    seq = []
+    with pytest.raises(g.LikelihoodIsNan) as es:
+        for p in pts:
+            seq.append(f.total_likelihood(p))
+    c = g.Forest(example)
+    c.total_likelihood(P0)
+    with pytest.raises(g.LikelihoodIsNan) as ec:
+        c.total_likelihood_chain(pts)
+    assert ec.value.point == 6 and len(seq) == 6
+    assert np.array_equal(ec.value.ll, np.array(seq))
+    assert (ec.value.cell, ec.value.row) == (es.value.cell, es.value.row)
+    with pytest.raises(g.GGPError, match="unspecified"):
+        c.total_likelihood(P0)
+    c.reset_state()
+    assert math.isfinite(c.total_likelihood(P0))
+
+
+def test_chain_empty_and_bad_shapes(example):
+    import gfp_gaussian_process_amd as g
+    f = g.Forest(example)
+    assert f.total_likelihood_chain(np.zeros((0, 11))).shape == (0,)
+    with pytest.raises(ValueError):
+        f.total_likelihood_chain(np.zeros((2, 10)))
+
+
+def test_hessian_chained_equals_num_hessian(example):
+    """optimize.num_hessian on a Forest's objective (the chained call) is bitwise num_hessian_ll
+    over one-by-one calls (ggp_num_hessian with a callback), carried state included"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as opt
+    idx = [0, 1, 3, 7]
+    a = g.Forest(example)
+    a.total_likelihood(P0)
+    H_chain = opt.num_hessian(a.total_likelihood, P0, idx, 1e-2)
+    b = g.Forest(example)
+    b.total_likelihood(P0)
+    H_seq = opt.num_hessian(lambda p: b.total_likelihood(p), P0, idx, 1e-2)
+    assert np.array_equal(H_chain, H_seq)
+    assert np.array_equal(a.state(), b.state())
