@@ -823,7 +823,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
     const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed *__restrict__ red, const int64_t call_seq,
-    const unsigned spin_max, const double *__restrict__ ptab, const double *__restrict__ carry)
+    const unsigned spin_max, const double *__restrict__ ptab, const double *__restrict__ carry,
+    const int32_t *__restrict__ pt_pred)
 {
     namespace W = ggp::wave;
     [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // GGP_STAMPS builds only
@@ -834,9 +835,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     lds_fill<W::kTabRows * W::kTabRow>(lds + W::L_TAB, lane, [](const int k) { return W::tab_entry(k); });
     GGP_PSTAMP(1);
     const double *p = P.p;
-    // chained evaluations (ggp_total_loglik_chain): blockIdx.y = point; the point's parameter row
-    // and its state / ll / NaN / done slices of n cells each
+    // chained evaluations (ggp_total_loglik_chain / _tree): blockIdx.y = point; the point's
+    // parameter row and its state / ll / NaN / done slices of n cells each.  A point's roots start
+    // from the state point pred left (pt_pred[pt], or pt - 1; -1: the handle's carried state)
     const int pt = CHAIN ? (int)blockIdx.y : 0;
+    const int pred = CHAIN ? (pt_pred ? pt_pred[pt] : pt - 1) : -1;
     if constexpr (CHAIN) {
         p = ptab + 11 * pt;
         state += (size_t)20 * n * pt;
@@ -938,11 +941,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         bool carried_prev = false, publish = ch.y != 0;
         if constexpr (CHAIN) {
             const bool root = F.parent[c] < 0;
-            carried_prev = root && pt > 0;
-            publish = publish || (root && pt + 1 < (int)gridDim.y);
+            carried_prev = root && pred >= 0;
+            publish = publish || (root && (pt_pred != nullptr || pt + 1 < (int)gridDim.y));
             if (carried_prev) {
                 wc = c;
-                wdone = cell_done - n;
+                wdone = cell_done + (ptrdiff_t)n * (pred - pt);
             }
         }
         if (wc >= 0 && __hip_atomic_load(wdone + wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
@@ -979,7 +982,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         } else {
             double m[4], C[16];
             if (CHAIN && carried_prev) {   // a root: the previous point's final state of it (coherent loads)
-                const double *st = state - (size_t)20 * n + (size_t)20 * c;
+                const double *st = state + (ptrdiff_t)20 * n * (pred - pt) + (size_t)20 * c;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) C[k] = ld_agent(st + 4 + k);
                 root_init(F, p, m, C);
@@ -2186,7 +2189,8 @@ struct Shard {
     double *d_b_ptab = nullptr, *d_b_state = nullptr, *d_b_ll = nullptr, *d_b_sum = nullptr;
     int32_t *d_b_nan = nullptr;
     int64_t *d_b_code = nullptr;
-    unsigned *d_b_done = nullptr;   // ggp_total_loglik_chain: per point, the cells' done flags
+    unsigned *d_b_done = nullptr;   // ggp_total_loglik_chain / _tree: per point, the cells' done flags
+    int32_t *d_b_pred = nullptr;    // ggp_total_loglik_tree: each point's predecessor
     int64_t b_cap = 0;   // points the workspace holds
     // -j: the smoother and the per-row joint tables, kept for the parameters they were made with
     // (the CLI asks for many start-row ranges with the same parameters)
@@ -2249,6 +2253,7 @@ struct ggp_forest {
     std::vector<int32_t> dfs_order;    // global DFS position -> global cell
     std::vector<int64_t> row_off;      // global row_offset
     Comm *comm = nullptr;              // multi-process mode (ggp_comm_attach)
+    int32_t tree_pts = 0;              // points of the last ggp_total_loglik_tree (ggp_keep_point_state)
 };
 
 namespace {
@@ -2295,7 +2300,7 @@ int launch_levels(Shard *f, const ggp_params &P)
         hipLaunchKernelGGL(k_loglik_wave<false>, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
                            f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
                            f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max,
-                           (const double *)nullptr, (const double *)nullptr);
+                           (const double *)nullptr, (const double *)nullptr, (const int32_t *)nullptr);
         HIPCHK(hipGetLastError());
         f->kernel_used = GGP_KERNEL_WAVE;
         f->last_code = GGP_KERNEL_WAVE << 8 | 64;
@@ -2313,7 +2318,7 @@ int launch_levels(Shard *f, const ggp_params &P)
             hipLaunchKernelGGL(k_loglik_wave<false>, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
                                f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
                                (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max,
-                               (const double *)nullptr, (const double *)nullptr);
+                               (const double *)nullptr, (const double *)nullptr, (const int32_t *)nullptr);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
         } else if (kind == GGP_KERNEL_PAIR) {
@@ -2472,12 +2477,13 @@ void shard_free_joints(Shard *f)
 void batch_free(Shard *f)
 {
     for (void *p : {(void *)f->d_b_ptab, (void *)f->d_b_state, (void *)f->d_b_ll, (void *)f->d_b_sum,
-                    (void *)f->d_b_nan, (void *)f->d_b_code, (void *)f->d_b_done})
+                    (void *)f->d_b_nan, (void *)f->d_b_code, (void *)f->d_b_done, (void *)f->d_b_pred})
         if (p) (void)hipFree(p);
     f->d_b_ptab = f->d_b_state = f->d_b_ll = f->d_b_sum = nullptr;
     f->d_b_nan = nullptr;
     f->d_b_code = nullptr;
     f->d_b_done = nullptr;
+    f->d_b_pred = nullptr;
     f->b_cap = 0;
 }
 
@@ -3570,6 +3576,7 @@ static int64_t batch_reserve(ggp_forest *f, int32_t n_pts)
         check(dev_upload<double>(&s->d_b_sum, nullptr, (size_t)chunk * s->n_lblocks));
         check(dev_upload<int64_t>(&s->d_b_code, nullptr, (size_t)chunk * s->n_lblocks));
         check(dev_upload<unsigned>(&s->d_b_done, nullptr, (size_t)chunk * nc));
+        check(dev_upload<int32_t>(&s->d_b_pred, nullptr, (size_t)chunk));
         if (rc == GGP_OK && hipMemset(s->d_b_done, 0, (size_t)chunk * nc * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
         if (rc != GGP_OK) { batch_free(s); return -rc; }
         s->b_cap = chunk;
@@ -3589,6 +3596,7 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
         for (int32_t i = 0; i < n_pts; ++i) { ll[i] = 0.0; status[i] = GGP_OK; }
         return GGP_OK;
     }
+    f->tree_pts = 0;
     const int64_t chunk = batch_reserve(f, n_pts);
     if (chunk <= 0) return (int)-chunk;
     const size_t ns = f->shards.size();
@@ -3663,6 +3671,93 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
 // other cell only for its parent within its point, and the points' trees overlap on the device.
 // Per point: k_reduce_blocks' sums (bitwise the in-launch reduction) and the host's top_sum.
 // Other handles (level launches, a communicator) run the calls one by one.
+// chained points on the path-launch shards: np points of params, point i's roots from the state
+// point pred[i] left (pred NULL: i - 1; -1: the carried state); per shard its block sums and
+// first-NaN codes per point, on the host once the shards are synchronised
+static bool chain_fusable(const ggp_forest *f)
+{
+    bool fused = f->comm == nullptr;
+    if (const char *e = std::getenv("GGP_CHAIN_FUSED")) fused = fused && std::atoi(e) != 0;
+    for (const Shard *s : f->shards)
+        if (s->n_cells && s->n_paths == 0) fused = false;
+    return fused;
+}
+
+static int run_points(ggp_forest *f, int64_t np, const double *params, const int32_t *pred, bool carry_last,
+                      std::vector<std::vector<double>> &sums, std::vector<std::vector<int64_t>> &codes)
+{
+    const size_t ns = f->shards.size();
+    sums.assign(ns, {});
+    codes.assign(ns, {});
+    ggp_params P0{};
+    for (size_t k = 0; k < ns; ++k) {   // enqueue every shard
+        Shard *s = f->shards[k];
+        if (!s->n_cells) continue;
+        const int64_t nc = s->n_cells;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipMemcpyAsync(s->d_b_ptab, params, (size_t)np * 11 * sizeof(double), hipMemcpyHostToDevice, s->stream));
+        if (pred)
+            HIPCHK(hipMemcpyAsync(s->d_b_pred, pred, (size_t)np * sizeof(int32_t), hipMemcpyHostToDevice, s->stream));
+        ++s->epoch;
+        hipLaunchKernelGGL(k_loglik_wave<true>, dim3((unsigned)s->n_paths, (unsigned)np), dim3(64), 0, s->stream, s->F, P0,
+                           s->d_path_cells, (int)nc, s->d_b_state, s->d_b_ll, s->d_b_nan, s->d_chain, s->d_b_done, s->epoch,
+                           s->d_path_seq, (const ChainRed *)nullptr, (int64_t)0, s->spin_max, (const double *)s->d_b_ptab,
+                           (const double *)s->d_state, pred ? (const int32_t *)s->d_b_pred : (const int32_t *)nullptr);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,
+                           s->stream, nc, s->d_b_ll, s->d_b_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt,
+                           s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
+                           (int64_t *)nullptr, (int64_t)0, (double *)nullptr, (int64_t *)nullptr);
+        HIPCHK(hipGetLastError());
+        if (carry_last)   // the carried state: the last point's (every cell, as its sequential call leaves it)
+            HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)(np - 1) * nc * 20, (size_t)nc * 20 * sizeof(double),
+                                  hipMemcpyDeviceToDevice, s->stream));
+        sums[k].resize((size_t)np * s->n_lblocks);
+        codes[k].resize((size_t)np * s->n_lblocks);
+        HIPCHK(hipMemcpyAsync(sums[k].data(), s->d_b_sum, sums[k].size() * sizeof(double), hipMemcpyDeviceToHost,
+                              s->stream));
+        HIPCHK(hipMemcpyAsync(codes[k].data(), s->d_b_code, codes[k].size() * sizeof(int64_t), hipMemcpyDeviceToHost,
+                              s->stream));
+    }
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    return GGP_OK;
+}
+
+// point i's result as ggp_loglik_result forms it: the code, the value, the NaN location
+static int point_result(const ggp_forest *f, const std::vector<std::vector<double>> &sums,
+                        const std::vector<std::vector<int64_t>> &codes, int64_t i, double *ll, int64_t *nan_cell,
+                        int64_t *nan_row)
+{
+    std::vector<double> blocks((size_t)f->n_blocks, 0.0);
+    long long code = kNoNan;
+    for (size_t k = 0; k < f->shards.size(); ++k) {
+        const Shard *s = f->shards[k];
+        for (int64_t j = 0; j < s->n_lblocks; ++j) {
+            blocks[(size_t)s->blk_global[j]] = sums[k][(size_t)(i * s->n_lblocks + j)];
+            code = std::min<long long>(code, codes[k][(size_t)(i * s->n_lblocks + j)]);
+        }
+    }
+    const double v = top_sum(std::move(blocks));
+    if (nan_cell) *nan_cell = -1;
+    if (nan_row) *nan_row = -1;
+    *ll = v;
+    if (code != kNoNan) {
+        const int64_t rank = code >> 24, row = code & 0xffffff;
+        if (nan_cell) *nan_cell = f->dfs_order[rank];
+        if (nan_row) *nan_row = row == kRowStall ? -1 : row;
+        *ll = std::nan("");
+        return row == kRowStall ? GGP_ETIMEOUT : GGP_ENAN;
+    }
+    return std::isnan(v) ? GGP_ENAN : GGP_OK;   // NaN from +inf + -inf across cells
+}
+
+static const char *kStallMsg =
+    "evaluation stalled: a cell's wait for the cell it depends on timed out (a scheduling stall, not a NaN)";
+
 int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *n_ok,
                            int64_t *nan_cell, int64_t *nan_row)
 {
@@ -3674,11 +3769,8 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
     *n_ok = 0;
     if (nan_cell) *nan_cell = -1;
     if (nan_row) *nan_row = -1;
-    bool fused = f->comm == nullptr;
-    if (const char *e = std::getenv("GGP_CHAIN_FUSED")) fused = fused && std::atoi(e) != 0;
-    for (Shard *s : f->shards)
-        if (s->n_cells && s->n_paths == 0) fused = false;
-    if (!fused || f->n_cells == 0) {
+    f->tree_pts = 0;
+    if (!chain_fusable(f) || f->n_cells == 0) {
         for (int32_t i = 0; i < n_pts; ++i) {
             const int rc = ggp_total_loglik(f, params + (size_t)11 * i, ll + i, nan_cell, nan_row);
             if (rc != GGP_OK) return rc;
@@ -3689,71 +3781,83 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
     if (n_pts == 0) return GGP_OK;
     const int64_t chunk = batch_reserve(f, n_pts);
     if (chunk <= 0) return (int)-chunk;
-    const size_t ns = f->shards.size();
-    std::vector<std::vector<double>> sums(ns);
-    std::vector<std::vector<int64_t>> codes(ns);
-    ggp_params P0{};
+    std::vector<std::vector<double>> sums;
+    std::vector<std::vector<int64_t>> codes;
     for (int64_t p0 = 0; p0 < n_pts; p0 += chunk) {
         const int64_t np = std::min<int64_t>(chunk, n_pts - p0);
-        for (size_t k = 0; k < ns; ++k) {   // enqueue every shard
-            Shard *s = f->shards[k];
-            if (!s->n_cells) continue;
-            const int64_t nc = s->n_cells;
-            HIPCHK(hipSetDevice(s->device));
-            HIPCHK(hipMemcpyAsync(s->d_b_ptab, params + 11 * p0, (size_t)np * 11 * sizeof(double),
-                                  hipMemcpyHostToDevice, s->stream));
-            ++s->epoch;
-            hipLaunchKernelGGL(k_loglik_wave<true>, dim3((unsigned)s->n_paths, (unsigned)np), dim3(64), 0, s->stream, s->F,
-                               P0, s->d_path_cells, (int)nc, s->d_b_state, s->d_b_ll, s->d_b_nan, s->d_chain, s->d_b_done,
-                               s->epoch, s->d_path_seq, (const ChainRed *)nullptr, (int64_t)0, s->spin_max,
-                               (const double *)s->d_b_ptab, (const double *)s->d_state);
-            HIPCHK(hipGetLastError());
-            hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,
-                               s->stream, nc, s->d_b_ll, s->d_b_nan, s->d_tree_dfs, s->d_blk_t0, s->d_blk_nt,
-                               s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
-                               (int64_t *)nullptr, (int64_t)0, (double *)nullptr, (int64_t *)nullptr);
-            HIPCHK(hipGetLastError());
-            // the carried state: the chunk's last point (every cell, as its sequential call leaves it)
-            HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)(np - 1) * nc * 20, (size_t)nc * 20 * sizeof(double),
-                                  hipMemcpyDeviceToDevice, s->stream));
-            sums[k].resize((size_t)np * s->n_lblocks);
-            codes[k].resize((size_t)np * s->n_lblocks);
-            HIPCHK(hipMemcpyAsync(sums[k].data(), s->d_b_sum, sums[k].size() * sizeof(double), hipMemcpyDeviceToHost,
-                                  s->stream));
-            HIPCHK(hipMemcpyAsync(codes[k].data(), s->d_b_code, codes[k].size() * sizeof(int64_t),
-                                  hipMemcpyDeviceToHost, s->stream));
-        }
-        for (Shard *s : f->shards) {
-            if (!s->n_cells) continue;
-            HIPCHK(hipSetDevice(s->device));
-            HIPCHK(hipStreamSynchronize(s->stream));
-        }
-        for (int64_t i = 0; i < np; ++i) {   // ggp_loglik_result, per point
-            std::vector<double> blocks((size_t)f->n_blocks, 0.0);
-            long long code = kNoNan;
-            for (size_t k = 0; k < ns; ++k) {
-                const Shard *s = f->shards[k];
-                for (int64_t j = 0; j < s->n_lblocks; ++j) {
-                    blocks[(size_t)s->blk_global[j]] = sums[k][(size_t)(i * s->n_lblocks + j)];
-                    code = std::min<long long>(code, codes[k][(size_t)(i * s->n_lblocks + j)]);
-                }
-            }
-            const double v = top_sum(std::move(blocks));
-            if (code != kNoNan) {
-                const int64_t rank = code >> 24, row = code & 0xffffff;
-                if (nan_cell) *nan_cell = f->dfs_order[rank];
-                if (nan_row) *nan_row = row == kRowStall ? -1 : row;
-                ll[p0 + i] = std::nan("");
-                if (row == kRowStall) {
-                    g_last_err = "evaluation stalled: a cell's wait for the cell it depends on timed out (a scheduling stall, not a NaN)";
-                    return GGP_ETIMEOUT;
-                }
-                return GGP_ENAN;
-            }
-            ll[p0 + i] = v;
-            if (std::isnan(v)) return GGP_ENAN;   // NaN from +inf + -inf across cells
+        const int rc = run_points(f, np, params + 11 * p0, nullptr, true, sums, codes);
+        if (rc != GGP_OK) return rc;
+        for (int64_t i = 0; i < np; ++i) {
+            const int r = point_result(f, sums, codes, i, ll + p0 + i, nan_cell, nan_row);
+            if (r == GGP_ETIMEOUT) g_last_err = kStallMsg;
+            if (r != GGP_OK) return r;
             *n_ok = (int32_t)(p0 + i + 1);
         }
+    }
+    return GGP_OK;
+}
+
+// Speculative evaluation (the -m optimiser's next calls): points whose roots start from the state
+// another point of the call left, all in one launch; the carried state is left unchanged until
+// ggp_keep_point_state picks the point whose state the caller's sequence of calls would have left.
+int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, const int32_t *pred, double *ll,
+                          int32_t *status, int64_t *nan_cell, int64_t *nan_row)
+{
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
+    if (!f || n_pts < 0 || (n_pts > 0 && (!params || !pred || !ll || !status))) {
+        g_last_err = "ggp_total_loglik_tree: bad arguments";
+        return GGP_EINVAL;
+    }
+    for (int32_t i = 0; i < n_pts; ++i)
+        if (pred[i] < -1 || pred[i] >= i) {
+            g_last_err = "ggp_total_loglik_tree: pred[i] must lie in [-1, i)";
+            return GGP_EINVAL;
+        }
+    f->tree_pts = 0;
+    if (!chain_fusable(f)) {
+        g_last_err = "ggp_total_loglik_tree: the handle has no path launch (or is attached to a communicator)";
+        return GGP_EINVAL;
+    }
+    if (n_pts == 0) return GGP_OK;
+    if (f->n_cells == 0) {
+        for (int32_t i = 0; i < n_pts; ++i) {
+            ll[i] = 0.0;
+            status[i] = GGP_OK;
+            if (nan_cell) nan_cell[i] = -1;
+            if (nan_row) nan_row[i] = -1;
+        }
+        f->tree_pts = n_pts;
+        return GGP_OK;
+    }
+    const int64_t chunk = batch_reserve(f, n_pts);
+    if (chunk <= 0) return (int)-chunk;
+    if (chunk < n_pts) {
+        g_last_err = "ggp_total_loglik_tree: more points than one launch holds";
+        return GGP_EINVAL;
+    }
+    std::vector<std::vector<double>> sums;
+    std::vector<std::vector<int64_t>> codes;
+    const int rc = run_points(f, n_pts, params, pred, false, sums, codes);
+    if (rc != GGP_OK) return rc;
+    for (int32_t i = 0; i < n_pts; ++i)
+        status[i] = point_result(f, sums, codes, i, ll + i, nan_cell ? nan_cell + i : nullptr, nan_row ? nan_row + i : nullptr);
+    f->tree_pts = n_pts;
+    return GGP_OK;
+}
+
+int ggp_keep_point_state(ggp_forest *f, int32_t point)
+{
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
+    if (!f || point < 0 || point >= f->tree_pts) {
+        g_last_err = "ggp_keep_point_state: no such point of the last ggp_total_loglik_tree call";
+        return GGP_EINVAL;
+    }
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        const int64_t nc = s->n_cells;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)point * nc * 20, (size_t)nc * 20 * sizeof(double),
+                              hipMemcpyDeviceToDevice, s->stream));
     }
     return GGP_OK;
 }

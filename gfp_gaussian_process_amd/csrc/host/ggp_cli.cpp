@@ -245,6 +245,16 @@ struct Objective {
     ggp_forest *forest = nullptr;
     ggp_host_forest *host = nullptr;
     const ggp_forest_desc *desc = nullptr;
+    // -m lookahead (ggp_nm::Lookahead): the announced call and the candidates for the call after
+    // it, evaluated ahead in one ggp_total_loglik_tree call; consumed by total_likelihood when the
+    // calls come (a call that matches none is evaluated as usual)
+    struct Ahead {
+        bool active = false, first_done = false, off = false;
+        int n = 0;
+        std::vector<double> pts, ll;
+        std::vector<int32_t> st;
+        std::vector<int64_t> nc, nr;
+    } ahead;
 };
 
 void log_iteration(const std::vector<double> &p, double tl, int iteration)
@@ -284,8 +294,62 @@ double account(const std::vector<double> &params, Objective &o, int rc, double l
     return ll;
 }
 
+// evaluate ahead: `first` (the next call) and `next` (one of which may be the call after it, from
+// the state `first` leaves) in one speculative launch; nothing changes until the calls come
+void look_ahead(Objective &o, const std::vector<const double *> &pts)
+{
+    Objective::Ahead &a = o.ahead;
+    a.active = false;
+    if (a.off) return;
+    a.n = (int)pts.size();
+    a.pts.resize((size_t)a.n * GGP_N_PARAMS);
+    for (int k = 0; k < a.n; ++k) std::memcpy(&a.pts[(size_t)k * GGP_N_PARAMS], pts[k], GGP_N_PARAMS * sizeof(double));
+    std::vector<int32_t> pred((size_t)a.n, 0);
+    pred[0] = -1;
+    a.ll.assign((size_t)a.n, 0.0);
+    a.st.assign((size_t)a.n, 0);
+    a.nc.assign((size_t)a.n, -1);
+    a.nr.assign((size_t)a.n, -1);
+    const int rc = ggp_total_loglik_tree(o.forest, a.n, a.pts.data(), pred.data(), a.ll.data(), a.st.data(), a.nc.data(),
+                                         a.nr.data());
+    if (rc == GGP_EINVAL) {   // no path launch on this handle: no lookahead
+        a.off = true;
+        return;
+    }
+    if (rc != GGP_OK) throw std::runtime_error(std::string("GPU likelihood failed: ") + ggp_strerror(rc));
+    a.active = true;
+    a.first_done = false;
+}
+
+// a call the lookahead evaluated: point k's result, its state made the carried state
+bool ahead_take(const std::vector<double> &params, Objective &o, int k_lo, int k_hi, double &out)
+{
+    Objective::Ahead &a = o.ahead;
+    for (int k = k_lo; k < k_hi; ++k) {
+        if (std::memcmp(params.data(), &a.pts[(size_t)k * GGP_N_PARAMS], GGP_N_PARAMS * sizeof(double)) != 0) continue;
+        const int rc = ggp_keep_point_state(o.forest, k);
+        if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_keep_point_state: ") + ggp_strerror(rc));
+        out = account(params, o, a.st[(size_t)k], a.ll[(size_t)k], a.nc[(size_t)k], a.nr[(size_t)k]);
+        return true;
+    }
+    return false;
+}
+
 double total_likelihood(const std::vector<double> &params, Objective &o)
 {
+    Objective::Ahead &a = o.ahead;
+    if (a.active) {
+        double v = 0;
+        if (!a.first_done) {
+            a.first_done = true;
+            a.active = ahead_take(params, o, 0, 1, v);   // then the candidates stay announced
+            if (a.active) return v;
+        } else {
+            a.active = false;
+            if (ahead_take(params, o, 1, a.n, v)) return v;
+            // not a candidate: the carried state is the announced call's, as its call left it
+        }
+    }
     double ll = 0;
     int64_t nc = -1, nr = -1;
     const int rc = ggp_total_loglik(o.forest, params.data(), &ll, &nc, &nr);
@@ -297,6 +361,7 @@ double total_likelihood(const std::vector<double> &params, Objective &o)
 std::vector<double> total_likelihood_chain(const std::vector<double> &pts, Objective &o)
 {
     const int32_t n = (int32_t)(pts.size() / GGP_N_PARAMS);
+    o.ahead.active = false;
     std::vector<double> ll((size_t)n, 0.0);
     int32_t n_ok = 0;
     int64_t nc = -1, nr = -1;
@@ -368,12 +433,30 @@ double minimize(Objective &o, Params &P, double tolerance, bool log_space)
         *v = -total_likelihood(pv, o);   // throws on NaN, unwinding the optimiser
         return true;
     };
+    // the lookahead: the reflected point and its possible successors, in parameter space
+    std::vector<std::vector<double>> la(4, std::vector<double>(n));
+    const ggp_nm::Lookahead look = [&](const double *first, const double *const *next, int n_next) {
+        std::vector<const double *> pts;
+        for (int k = 0; k <= n_next; ++k) {
+            const double *src = k == 0 ? first : next[k - 1];
+            if (!src) continue;
+            std::vector<double> &d = la[pts.size()];
+            for (int i = 0; i < n; ++i) d[i] = log_space ? std::exp(src[i]) : src[i];
+            pts.push_back(d.data());
+        }
+        look_ahead(o, pts);
+    };
+    const char *lk = std::getenv("GGP_NM_LOOKAHEAD");
+    const bool use_look = !(lk && std::atoi(lk) == 0);
     double minf = 0;
     ggp_nm::Stats st;
     ggp_nm::Result r;
     try {
-        r = ggp_nm::minimize(n, f, lb.data(), ub.data(), x.data(), step.data(), tolerance, 0, &minf, st);
+        r = ggp_nm::minimize(n, f, lb.data(), ub.data(), x.data(), step.data(), tolerance, 0, &minf, st,
+                             use_look ? &look : nullptr);
+        o.ahead.active = false;
     } catch (std::exception &e) {
+        o.ahead.active = false;
         g_log << "(minimize_wrapper) ERROR: Log likelihood optimization failed (" << e.what() << ")" << std::endl;
         throw;
     }

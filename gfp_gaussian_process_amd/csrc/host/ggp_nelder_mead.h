@@ -35,6 +35,13 @@ enum Result {   // nlopt_result values
 // f(x, &value) -> false to force a stop (the reference's objective throws on a NaN)
 using Objective = std::function<bool(const double *x, double *value)>;
 
+// Optional lookahead, called before each reflected point's call with that point and the points
+// one of which the next call of the iteration may be -- expansion, outside contraction, inside
+// contraction (NULL where that step would end the run instead).  An objective whose calls carry
+// state can evaluate them ahead, each from the state the reflected point leaves; the sequence of
+// calls, and so the trajectory, is unchanged.
+using Lookahead = std::function<void(const double *first, const double *const *next, int n_next)>;
+
 inline bool close_pt(double a, double b) { return std::fabs(a - b) <= 1e-13 * (std::fabs(a) + std::fabs(b)); }
 
 // xnew = c + scale (c - xold), pinned to the bounds; false if xnew coincides with c or xold
@@ -59,7 +66,7 @@ struct Stats {
 
 // nldrmd_minimize_ on the reduced problem (all lb < ub)
 inline Result nldrmd(int n, const Objective &f, const double *lb, const double *ub, double *x, double *minf,
-                     const double *xstep, double ftol_abs, long maxeval, Stats &st)
+                     const double *xstep, double ftol_abs, long maxeval, Stats &st, const Lookahead *look = nullptr)
 {
     const double alpha = 1, beta = 0.5, gamm = 2, delta = 0.5;
     const int w = n + 1;                                // row: f, x[0..n-1]
@@ -137,6 +144,14 @@ inline Result nldrmd(int n, const Objective &f, const double *lb, const double *
         // (nldrmd's x-tolerance test never fires with xtol_rel = xtol_abs = 0)
 
         if (!reflectpt(n, xcur.data(), c.data(), alpha, xh, lb, ub)) return XTOL_REACHED;
+        if (look && *look) {   // the points the branches below would call next (same expressions)
+            std::vector<double> xe(n), xo(n), xi(n);
+            const bool ve = reflectpt(n, xe.data(), c.data(), gamm, xh, lb, ub);
+            const bool vo = reflectpt(n, xo.data(), c.data(), beta, xh, lb, ub);
+            const bool vi = reflectpt(n, xi.data(), c.data(), -beta, xh, lb, ub);
+            const double *next[3] = {ve ? xe.data() : nullptr, vo ? xo.data() : nullptr, vi ? xi.data() : nullptr};
+            (*look)(xcur.data(), next, 3);
+        }
         double fr;
         if ((ret = eval(xcur.data(), &fr)) != SUCCESS) return ret;
 
@@ -174,7 +189,7 @@ inline Result nldrmd(int n, const Objective &f, const double *lb, const double *
 
 // nlopt_optimize for LN_NELDERMEAD: bound check, elimdim, first evaluation, nldrmd
 inline Result minimize(int n, const Objective &f, const double *lb, const double *ub, double *x, const double *dx,
-                       double ftol_abs, long maxeval, double *minf, Stats &st)
+                       double ftol_abs, long maxeval, double *minf, Stats &st, const Lookahead *look = nullptr)
 {
     for (int i = 0; i < n; ++i)
         if (lb[i] > ub[i] || x[i] < lb[i] || x[i] > ub[i]) return INVALID_ARGS;
@@ -198,6 +213,18 @@ inline Result minimize(int n, const Objective &f, const double *lb, const double
         for (int j = 0; j < nd; ++j) buf[free_dims[j]] = xd[j];
         return f(buf.data(), v);
     };
+    // the lookahead in full coordinates (the eliminated dimensions re-inserted)
+    std::vector<std::vector<double>> lbuf(4, full);
+    const Lookahead lr = [&](const double *first, const double *const *next, int n_next) {
+        const double *fl[3] = {nullptr, nullptr, nullptr};
+        for (int k = 0; k <= n_next && k < 4; ++k) {
+            const double *src = k == 0 ? first : next[k - 1];
+            if (!src) continue;
+            for (int j = 0; j < nd; ++j) lbuf[k][free_dims[j]] = src[j];
+            if (k > 0) fl[k - 1] = lbuf[k].data();
+        }
+        (*look)(lbuf[0].data(), fl, n_next < 3 ? n_next : 3);
+    };
     // nldrmd_minimize: the starting point is evaluated first
     if (!fr(xr.data(), minf)) return FORCED_STOP;
     ++st.nevals;
@@ -205,7 +232,8 @@ inline Result minimize(int n, const Objective &f, const double *lb, const double
     if (maxeval > 0 && st.nevals >= maxeval) {
         ret = MAXEVAL_REACHED;
     } else if (nd > 0) {
-        ret = nldrmd(nd, fr, lbr.data(), ubr.data(), xr.data(), minf, dxr.data(), ftol_abs, maxeval, st);
+        ret = nldrmd(nd, fr, lbr.data(), ubr.data(), xr.data(), minf, dxr.data(), ftol_abs, maxeval, st,
+                     look && *look ? &lr : nullptr);
     }
     for (int j = 0; j < nd; ++j) full[free_dims[j]] = xr[j];
     std::memcpy(x, full.data(), sizeof(double) * n);

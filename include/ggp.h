@@ -158,6 +158,18 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
 int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll,
                            int32_t *n_ok, int64_t *nan_cell, int64_t *nan_row);
 
+/* Speculative evaluation (the -m optimiser's lookahead): n_pts points in one launch,
+ * point i's roots starting from the state point pred[i] left (pred[i] in [-1, i); -1 = the
+ * carried state), every other cell from its parent within its point.  ll[i] / status[i] (GGP_OK,
+ * GGP_ENAN, GGP_ETIMEOUT) and, if not NULL, nan_cell[i] / nan_row[i] are what a ggp_total_loglik
+ * call of point i after the calls of its pred chain would return.  The carried state is left
+ * unchanged; ggp_keep_point_state(i) then makes it the state point i left (valid until the next
+ * tree, chain or batch call).  Needs a path-launch handle without a communicator (else
+ * GGP_EINVAL) and at most one launch's points (the batch workspace; else GGP_EINVAL). */
+int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, const int32_t *pred,
+                          double *ll, int32_t *status, int64_t *nan_cell, int64_t *nan_row);
+int ggp_keep_point_state(ggp_forest *f, int32_t point);
+
 /* Asynchronous form for drivers that pipeline: enqueue one evaluation on the handle's
  * stream; ggp_loglik_result() waits and returns what ggp_total_loglik would have. */
 int ggp_total_loglik_async(ggp_forest *f, const double *params);

@@ -386,3 +386,26 @@ def test_cli_two_segments_matches_oracle(tmp_path, example_paths):
     em = np.max(np.abs(got[:, :4] - ref_m) / (np.abs(ref_m) + sd))
     ec = np.max(np.abs(got[:, 4:] - ref_c[:, iu[0], iu[1]]) / (sd[:, iu[0]] * sd[:, iu[1]]))
     assert em < 1e-4 and ec < 1e-4, (em, ec)
+
+
+def test_cli_lookahead_and_chain_give_the_sequential_files(tmp_path, example_paths):
+    """-m with the optimiser's lookahead (each reflected point and its three possible successors
+    in one speculative launch) and the chained Hessian / scan calls: every output file byte for
+    byte that of the call-by-call run (GGP_NM_LOOKAHEAD=0, GGP_CHAIN_FUSED=0) -- the same
+    trajectory, iteration log, error bars (carried state included) and final values"""
+    pf = _param_file(tmp_path / "p.txt", {0: "2.31E-03, 2.31E-04", 7: "3.35E-04, 3.35E-05", 8: "8.26E-01, 8.26E-02",
+                                           6: "4.95E-04, 1.0E-04, 1.0E-04, 9.0E-04"})
+    outs = {}
+    for tag, env in (("seq", {"GGP_NM_LOOKAHEAD": "0", "GGP_CHAIN_FUSED": "0"}), ("fast", {})):
+        e = dict(os.environ, **env)
+        r = subprocess.run([CLI, "-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-m", "-s",
+                            "-t", "1e-3", "-o", str(tmp_path / tag)], capture_output=True, text=True, timeout=600,
+                           cwd=tmp_path, env=e)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[tag] = {n: open(tmp_path / tag / n, "rb").read() for n in sorted(os.listdir(tmp_path / tag))
+                     if n.endswith(".csv") or n.endswith(".txt")}
+    assert sorted(outs["seq"]) == sorted(outs["fast"]) and len(outs["seq"]) >= 4, sorted(outs["seq"])
+    for n in outs["seq"]:
+        assert outs["seq"][n] == outs["fast"][n], n
+    it = [n for n in outs["fast"] if n.endswith("_iterations.csv")]
+    assert len(it) == 1 and len(_ll_table(str(tmp_path / "fast" / it[0]))) > 40, it
