@@ -245,14 +245,14 @@ struct Objective {
     ggp_forest *forest = nullptr;
     ggp_host_forest *host = nullptr;
     const ggp_forest_desc *desc = nullptr;
-    // -m lookahead (ggp_nm::Lookahead): the announced call and the candidates for the call after
-    // it, evaluated ahead in one ggp_total_loglik_tree call; consumed by total_likelihood when the
-    // calls come (a call that matches none is evaluated as usual)
+    // -m lookahead (ggp_nm::Lookahead): a tree of the run's possible next calls (node k from the
+    // state node pred[k] leaves; -1: the carried state), evaluated in one ggp_total_loglik_tree
+    // call; total_likelihood serves a call from the children of the last node served
     struct Ahead {
-        bool active = false, first_done = false, off = false;
-        int n = 0;
+        bool active = false, off = false;
+        int n = 0, cur = -1;
         std::vector<double> pts, ll;
-        std::vector<int32_t> st;
+        std::vector<int32_t> pred, st;
         std::vector<int64_t> nc, nr;
     } ahead;
 };
@@ -294,61 +294,55 @@ double account(const std::vector<double> &params, Objective &o, int rc, double l
     return ll;
 }
 
-// evaluate ahead: `first` (the next call) and `next` (one of which may be the call after it, from
-// the state `first` leaves) in one speculative launch; nothing changes until the calls come
-void look_ahead(Objective &o, const std::vector<const double *> &pts)
+// evaluate a tree of calls ahead in one speculative launch; nothing changes until the calls come
+void look_ahead(Objective &o, const std::vector<std::vector<double>> &pts, const std::vector<int> &pred)
 {
     Objective::Ahead &a = o.ahead;
     a.active = false;
-    if (a.off) return;
+    if (a.off || pts.empty()) return;
     a.n = (int)pts.size();
+    a.cur = -1;
     a.pts.resize((size_t)a.n * GGP_N_PARAMS);
-    for (int k = 0; k < a.n; ++k) std::memcpy(&a.pts[(size_t)k * GGP_N_PARAMS], pts[k], GGP_N_PARAMS * sizeof(double));
-    std::vector<int32_t> pred((size_t)a.n, 0);
-    pred[0] = -1;
+    for (int k = 0; k < a.n; ++k) std::memcpy(&a.pts[(size_t)k * GGP_N_PARAMS], pts[k].data(), GGP_N_PARAMS * sizeof(double));
+    a.pred.assign(pred.begin(), pred.end());
     a.ll.assign((size_t)a.n, 0.0);
     a.st.assign((size_t)a.n, 0);
     a.nc.assign((size_t)a.n, -1);
     a.nr.assign((size_t)a.n, -1);
-    const int rc = ggp_total_loglik_tree(o.forest, a.n, a.pts.data(), pred.data(), a.ll.data(), a.st.data(), a.nc.data(),
-                                         a.nr.data());
-    if (rc == GGP_EINVAL) {   // no path launch on this handle: no lookahead
+    const int rc = ggp_total_loglik_tree(o.forest, a.n, a.pts.data(), a.pred.data(), a.ll.data(), a.st.data(),
+                                         a.nc.data(), a.nr.data());
+    if (rc == GGP_EINVAL) {   // no path launch on this handle (or too many points): no lookahead
         a.off = true;
         return;
     }
     if (rc != GGP_OK) throw std::runtime_error(std::string("GPU likelihood failed: ") + ggp_strerror(rc));
     a.active = true;
-    a.first_done = false;
 }
 
-// a call the lookahead evaluated: point k's result, its state made the carried state
-bool ahead_take(const std::vector<double> &params, Objective &o, int k_lo, int k_hi, double &out)
+// the node that serves the call `params` next: a child of the last node served, else -1
+int ahead_node(const Objective &o, const double *params)
 {
-    Objective::Ahead &a = o.ahead;
-    for (int k = k_lo; k < k_hi; ++k) {
-        if (std::memcmp(params.data(), &a.pts[(size_t)k * GGP_N_PARAMS], GGP_N_PARAMS * sizeof(double)) != 0) continue;
-        const int rc = ggp_keep_point_state(o.forest, k);
-        if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_keep_point_state: ") + ggp_strerror(rc));
-        out = account(params, o, a.st[(size_t)k], a.ll[(size_t)k], a.nc[(size_t)k], a.nr[(size_t)k]);
-        return true;
-    }
-    return false;
+    const Objective::Ahead &a = o.ahead;
+    if (!a.active) return -1;
+    for (int k = 0; k < a.n; ++k)
+        if (a.pred[(size_t)k] == a.cur &&
+            std::memcmp(params, &a.pts[(size_t)k * GGP_N_PARAMS], GGP_N_PARAMS * sizeof(double)) == 0)
+            return k;
+    return -1;
 }
 
 double total_likelihood(const std::vector<double> &params, Objective &o)
 {
     Objective::Ahead &a = o.ahead;
     if (a.active) {
-        double v = 0;
-        if (!a.first_done) {
-            a.first_done = true;
-            a.active = ahead_take(params, o, 0, 1, v);   // then the candidates stay announced
-            if (a.active) return v;
-        } else {
-            a.active = false;
-            if (ahead_take(params, o, 1, a.n, v)) return v;
-            // not a candidate: the carried state is the announced call's, as its call left it
+        const int k = ahead_node(o, params.data());
+        if (k >= 0) {   // evaluated ahead: its state becomes the carried state, its value the call's
+            a.cur = k;
+            const int rc = ggp_keep_point_state(o.forest, k);
+            if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_keep_point_state: ") + ggp_strerror(rc));
+            return account(params, o, a.st[(size_t)k], a.ll[(size_t)k], a.nc[(size_t)k], a.nr[(size_t)k]);
         }
+        a.active = false;   // not foreseen: the carried state is the last served node's
     }
     double ll = 0;
     int64_t nc = -1, nr = -1;
@@ -433,19 +427,21 @@ double minimize(Objective &o, Params &P, double tolerance, bool log_space)
         *v = -total_likelihood(pv, o);   // throws on NaN, unwinding the optimiser
         return true;
     };
-    // the lookahead: the reflected point and its possible successors, in parameter space
-    std::vector<std::vector<double>> la(4, std::vector<double>(n));
-    const ggp_nm::Lookahead look = [&](const double *first, const double *const *next, int n_next) {
-        std::vector<const double *> pts;
-        for (int k = 0; k <= n_next; ++k) {
-            const double *src = k == 0 ? first : next[k - 1];
-            if (!src) continue;
-            std::vector<double> &d = la[pts.size()];
-            for (int i = 0; i < n; ++i) d[i] = log_space ? std::exp(src[i]) : src[i];
-            pts.push_back(d.data());
-        }
-        look_ahead(o, pts);
+    // the lookahead, in parameter space (log_space: the exponentials the objective takes)
+    auto to_params = [&](const double *src) {
+        std::vector<double> v((size_t)n);
+        for (int i = 0; i < n; ++i) v[i] = log_space ? std::exp(src[i]) : src[i];
+        return v;
     };
+    ggp_nm::Lookahead look;
+    look.need = [&](const double *xx) { return ahead_node(o, to_params(xx).data()) < 0; };
+    look.tree = [&](const std::vector<std::vector<double>> &xs, const std::vector<int> &pred) {
+        std::vector<std::vector<double>> ps;
+        for (const auto &xx : xs) ps.push_back(to_params(xx.data()));
+        look_ahead(o, ps, pred);
+    };
+    if (const char *e = std::getenv("GGP_NM_AHEAD_DEPTH")) look.depth = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("GGP_NM_AHEAD_NODES")) look.max_nodes = std::max(1, std::atoi(e));
     const char *lk = std::getenv("GGP_NM_LOOKAHEAD");
     const bool use_look = !(lk && std::atoi(lk) == 0);
     double minf = 0;
@@ -455,6 +451,10 @@ double minimize(Objective &o, Params &P, double tolerance, bool log_space)
         r = ggp_nm::minimize(n, f, lb.data(), ub.data(), x.data(), step.data(), tolerance, 0, &minf, st,
                              use_look ? &look : nullptr);
         o.ahead.active = false;
+        if (g_clock.on)
+            std::fprintf(stderr, "[ggp timing] -m: %ld calls, %ld iterations (%ld expansions, %ld accepts, %ld contractions, %ld shrinks)\n",
+                         st.nevals, st.iterations, st.expansions, st.accepts, st.contractions, st.shrinks);
+        g_clock.mark("-m: minimised");
     } catch (std::exception &e) {
         o.ahead.active = false;
         g_log << "(minimize_wrapper) ERROR: Log likelihood optimization failed (" << e.what() << ")" << std::endl;
@@ -585,6 +585,7 @@ void run_minimization(Objective &o, Params &P, std::map<std::string, std::string
             for (double v : error) file << "," << v;
             file << "\n";
         }
+        g_clock.mark("-m: error bars (Hessians)");
     }
     {   // save_final_likelihood (likelihood.h:316-339)
         std::ofstream file(outfile_estim, std::ios_base::app);

@@ -25,7 +25,11 @@ def main():
     with gzip.open(os.path.join(GOLD, "example_input.csv.gz"), "rb") as a, open(csv, "wb") as b:
         shutil.copyfileobj(a, b)
     res, files = {}, {}
-    for tag, env in (("call_by_call", {"GGP_NM_LOOKAHEAD": "0", "GGP_CHAIN_FUSED": "0"}), ("default", {})):
+    runs = [("call_by_call", {"GGP_NM_LOOKAHEAD": "0", "GGP_CHAIN_FUSED": "0"}), ("default", {"GGP_TIMING": "1"})]
+    for spec in filter(None, os.environ.get("EXMP_EXTRA", "").split(";")):   # name:K=V,K=V
+        name, kv = spec.split(":")
+        runs.append((name, dict([e.split("=") for e in kv.split(",")], GGP_TIMING="1")))
+    for tag, env in runs:
         out = os.path.join(d, tag)
         t0 = time.perf_counter()
         r = subprocess.run([CLI, "-i", csv, "-b", os.path.join(GOLD, "example_parameter_file.txt"), "-c",
@@ -38,9 +42,12 @@ def main():
                       if not n.endswith(".log")}
         its = [n for n in files[tag] if n.endswith("_iterations.csv")]
         res[tag] = {"wall_s": wall, "nelder_mead_calls": files[tag][its[0]].count(b"\n") - 1 if its else None}
+        timing = [ln for ln in r.stderr.splitlines() if ln.startswith("[ggp timing]")]
+        if timing:
+            res[tag]["phases"] = timing
         print(tag, res[tag], file=sys.stderr, flush=True)
-    res["identical_files"] = sorted(files["default"]) == sorted(files["call_by_call"]) and all(
-        files["default"][n] == files["call_by_call"][n] for n in files["default"])
+    res["identical_files"] = all(sorted(files[t]) == sorted(files["call_by_call"]) and all(
+        files[t][n] == files["call_by_call"][n] for n in files[t]) for t in files)
     res["files"] = sorted(files["default"])
     res["speedup"] = res["call_by_call"]["wall_s"] / res["default"]["wall_s"]
     shutil.rmtree(d, ignore_errors=True)
