@@ -166,8 +166,10 @@ def example_mp(tmp: str, cpu_budget: float):
             "cpu_ms_per_eval_1core": cpu_ms, "cpu_estimate_s": n_eval * cpu_ms / 1e3,
             "reference_published": "around 5min (example_data_set/README.txt:1-3, hardware not stated)",
             "note": "lib/ggp -i input.csv -b parameter_file.txt -c csv_config.txt -m -p -g 1 (the reference's "
-                    "command), wall time of the whole CLI run incl. ingest, -p and output files; ms_per_eval = "
-                    "wall / evaluations (an upper bound per evaluation)"}
+                    "command), wall time of the whole CLI run incl. ingest, -p and output files; the optimiser "
+                    "evaluates its possible next calls ahead and the Hessians run chained (every output file "
+                    "byte-identical to the call-by-call run: tools/example_mp_time.py); ms_per_eval = wall / "
+                    "evaluations"}
 
 
 def inprocess_child(argv) -> int:
@@ -386,9 +388,24 @@ def main() -> int:
             fg.total_likelihood_batch(pts)
         barrier()
         hel = (time.perf_counter() - t1) / reps
+        # the same points with the reference's semantics (each from the state the previous left),
+        # as the CLI's error bars make them: one ggp_total_loglik_chain call, bitwise the calls
+        st0 = fg.state()
+        fg.total_likelihood_chain(pts[:8])
+        cel = 0.0
+        for _ in range(reps):
+            fg.set_state(st0)
+            barrier()
+            t1 = time.perf_counter()
+            fg.total_likelihood_chain(pts)
+            barrier()
+            cel += (time.perf_counter() - t1) / reps
         hess = {"points": len(pts), "rows_per_point": rows_rank, "ms_per_batch": 1e3 * hel,
                 "updates_per_s_per_gpu": len(pts) * rows_rank / hel,
                 "sequential_ms_estimate": len(pts) * 1e3 * el / args.steps,
+                "chained": {"ms_per_chain": 1e3 * cel, "updates_per_s_per_gpu": len(pts) * rows_rank / cel,
+                            "note": "the same points chained through the carried state as the reference "
+                                    "calls them (ggp_total_loglik_chain: bitwise the one-by-one calls)"},
                 "note": "batched objective (opt-in, points independent) on the C2 forest; not the headline value"}
 
     # ---- the -p smoother on a per-GPU shard of BASELINE configs[4] (C5: 1M trees x 500 tp over
