@@ -174,3 +174,23 @@ def test_hessian_points_match_num_hessian_visits():
     assert np.array_equal(np.array(seen), pts)
     assert np.array_equal(O.num_hessian_batched(Batch(), x, idx, 1e-2), H)
     assert h[3] == 1e-12
+
+
+@pytest.mark.parametrize("n,fixed", [(10, -1), (4, 1), (2, -1)])
+def test_lookahead_serves_the_same_calls(tmp_path, n, fixed):
+    """the -m lookahead (ggp_nelder_mead.h Machine + speculate): the run makes the same calls with
+    the same values as without it, and every call after the first is served from a speculated
+    tree (parents listed before children, at most Lookahead::max_nodes points per tree)"""
+    import shutil
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "nm_ahead_check")
+    subprocess.run([cxx, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "gfp_gaussian_process_amd", "csrc", "host"),
+                    "-o", exe, os.path.join(ROOT, "tests", "nm_ahead_check.cpp")], check=True)
+    out = subprocess.run([exe, str(n), str(fixed)], capture_output=True, text=True, check=True).stdout.split()
+    assert out[0] == "same", out
+    calls, served, launches, max_nodes = map(int, out[1:])
+    assert calls > 50 and served == calls - 1, out
+    assert launches * 2 < calls and max_nodes <= 40, out
