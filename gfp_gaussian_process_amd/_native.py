@@ -23,6 +23,9 @@ c_int32_p = ctypes.POINTER(ctypes.c_int32)
 c_double_p = ctypes.POINTER(ctypes.c_double)
 # int (*)(const double *x, double *value, void *data)   (ggp_objective_fn, include/ggp_host.h)
 OBJECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_double_p, c_double_p, ctypes.c_void_p)
+AHEAD_NEED_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p)
+AHEAD_TREE_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                 ctypes.c_void_p)
 
 
 class ForestDesc(ctypes.Structure):
@@ -120,6 +123,10 @@ HOST_SYMBOLS = {
     "ggp_nldrmd_minimize": (ctypes.c_int, [ctypes.c_int32, OBJECTIVE_FN, ctypes.c_void_p, c_double_p, c_double_p,
                                            c_double_p, c_double_p, ctypes.c_double, ctypes.c_int64, c_double_p,
                                            c_int64_p]),
+    "ggp_nldrmd_minimize_ahead": (ctypes.c_int, [ctypes.c_int32, OBJECTIVE_FN, AHEAD_NEED_FN, AHEAD_TREE_FN,
+                                                 ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                                 ctypes.c_double, ctypes.c_int64, c_double_p, c_int64_p,
+                                                 ctypes.c_int32, ctypes.c_int32]),
     "ggp_num_hessian": (ctypes.c_int, [ctypes.c_int32, OBJECTIVE_FN, ctypes.c_void_p, c_double_p, c_int32_p,
                                        ctypes.c_int32, ctypes.c_double, c_double_p]),
     "ggp_inverse_pplu": (ctypes.c_int, [ctypes.c_int32, c_double_p, c_double_p]),

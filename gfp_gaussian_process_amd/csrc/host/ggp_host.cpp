@@ -897,6 +897,29 @@ extern "C" int ggp_nldrmd_minimize(int32_t n, ggp_objective_fn f, void *data, co
     return r;
 }
 
+extern "C" int ggp_nldrmd_minimize_ahead(int32_t n, ggp_objective_fn f, ggp_ahead_need_fn need, ggp_ahead_tree_fn tree,
+                                         void *data, const double *lb, const double *ub, double *x, const double *dx,
+                                         double ftol_abs, int64_t maxeval, double *minf, int64_t *nevals, int32_t depth,
+                                         int32_t max_nodes)
+{
+    if (n < 0 || !f || !need || !tree || !lb || !ub || !x || !dx || !minf) return ggp_nm::INVALID_ARGS;
+    ggp_nm::Stats st;
+    const ggp_nm::Objective obj = [&](const double *xx, double *v) { return f(xx, v, data) == 0; };
+    ggp_nm::Lookahead look;
+    if (depth > 0) look.depth = depth;
+    if (max_nodes > 0) look.max_nodes = max_nodes;
+    look.need = [&](const double *xx) { return need(xx, data) != 0; };
+    look.tree = [&](const std::vector<std::vector<double>> &xs, const std::vector<int> &pred) {
+        std::vector<double> flat;
+        for (const auto &v : xs) flat.insert(flat.end(), v.begin(), v.end());
+        const std::vector<int32_t> p32(pred.begin(), pred.end());
+        tree(flat.data(), p32.data(), (int32_t)xs.size(), data);
+    };
+    const ggp_nm::Result r = ggp_nm::minimize(n, obj, lb, ub, x, dx, ftol_abs, (long)maxeval, minf, st, &look);
+    if (nevals) *nevals = st.nevals;
+    return r;
+}
+
 extern "C" int ggp_num_hessian(int32_t n, ggp_objective_fn f, void *data, const double *x, const int32_t *idx,
                                int32_t k, double epsilon, double *out)
 {

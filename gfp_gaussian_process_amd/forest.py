@@ -530,6 +530,32 @@ class Forest:
         self._check(rc)
         return ll
 
+    def total_likelihood_tree(self, params_points, pred):
+        """speculative evaluation (ggp_total_loglik_tree): point i (a row of an [n, 11] array) from
+        the state point pred[i] leaves (-1: the carried state), in one launch; the carried state
+        is unchanged until keep_point_state(i).  Returns (ll, status, nan_cell, nan_row) arrays
+        (status: GGP_OK / GGP_ENAN / GGP_ETIMEOUT per point); None if the handle has no path
+        launch (nothing was evaluated)."""
+        p = np.ascontiguousarray(np.atleast_2d(params_points), np.float64)
+        pr = np.ascontiguousarray(pred, np.int32)
+        if p.ndim != 2 or p.shape[1] != N.N_PARAMS or pr.shape != (p.shape[0],):
+            raise ValueError("expected [n, 11] points and n predecessors")
+        self._usable()
+        n = p.shape[0]
+        ll, st = np.zeros(n), np.zeros(n, np.int32)
+        nc, nr = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        rc = self._lib.ggp_total_loglik_tree(self._h, n, p.ctypes.data_as(N.c_double_p), pr.ctypes.data_as(N.c_int32_p),
+                                             ll.ctypes.data_as(N.c_double_p), st.ctypes.data_as(N.c_int32_p),
+                                             nc.ctypes.data_as(N.c_int64_p), nr.ctypes.data_as(N.c_int64_p))
+        if rc == N.GGP_EINVAL:
+            return None
+        self._check(rc)
+        return ll, st, nc, nr
+
+    def keep_point_state(self, point: int) -> None:
+        """make the state point `point` of the last total_likelihood_tree left the carried state"""
+        self._check(self._lib.ggp_keep_point_state(self._h, int(point)))
+
     def reset_state(self) -> None:
         self._check(self._lib.ggp_reset_state(self._h))
         self._poisoned = False

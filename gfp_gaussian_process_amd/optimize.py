@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -42,10 +43,11 @@ def _callback(f, n, errors: list):
     return N.OBJECTIVE_FN(cb)
 
 
-def nldrmd_minimize(f, x0, lb, ub, dx, ftol_abs: float, maxeval: int = 0):
+def nldrmd_minimize(f, x0, lb, ub, dx, ftol_abs: float, maxeval: int = 0, ahead=None):
     """minimise f over the box [lb, ub] (lb == ub: a fixed dimension); returns
     (x_best, f_best, result_code, n_evaluations).  An exception raised by f stops the run
-    and propagates (the reference's NaN path)."""
+    and propagates (the reference's NaN path).  ahead: an _Ahead (the lookahead of a stateful
+    objective, ggp_nldrmd_minimize_ahead) -- the same calls and result."""
     x = np.ascontiguousarray(x0, np.float64).copy()
     n = x.size
     lb, ub, dx = (np.ascontiguousarray(v, np.float64) for v in (lb, ub, dx))
@@ -54,11 +56,80 @@ def nldrmd_minimize(f, x0, lb, ub, dx, ftol_abs: float, maxeval: int = 0):
     minf = ctypes.c_double()
     nev = ctypes.c_int64()
     dp = lambda a: a.ctypes.data_as(N.c_double_p)  # noqa: E731
-    rc = N.host().ggp_nldrmd_minimize(n, cb, None, dp(lb), dp(ub), dp(x), dp(dx), ftol_abs, maxeval,
-                                      ctypes.byref(minf), ctypes.byref(nev))
+    if ahead is None:
+        rc = N.host().ggp_nldrmd_minimize(n, cb, None, dp(lb), dp(ub), dp(x), dp(dx), ftol_abs, maxeval,
+                                          ctypes.byref(minf), ctypes.byref(nev))
+    else:
+        need, tree = ahead.callbacks(n, errors)
+        rc = N.host().ggp_nldrmd_minimize_ahead(n, cb, need, tree, None, dp(lb), dp(ub), dp(x), dp(dx), ftol_abs,
+                                                maxeval, ctypes.byref(minf), ctypes.byref(nev), 0, 0)
     if errors:
         raise errors[0]
     return x, minf.value, rc, nev.value
+
+
+class _Ahead:
+    """The optimiser's lookahead for a Forest objective (include/ggp_host.h
+    ggp_nldrmd_minimize_ahead): the run's possible next calls evaluated in one
+    ggp_total_loglik_tree launch, each from the state its parent call leaves; call() serves the
+    real calls from them while they match (bitwise parameters, from the node last served), else
+    evaluates as usual.  to_params: the optimiser's point -> the objective's parameters."""
+
+    def __init__(self, forest, to_params):
+        self.f, self.to_params = forest, to_params
+        self.active, self.off, self.cur = False, False, -1
+        self.keys, self.pred, self.res = [], [], None
+
+    def node(self, p) -> int:
+        if not self.active:
+            return -1
+        key = np.ascontiguousarray(p, np.float64).tobytes()
+        for k, (kk, pk) in enumerate(zip(self.keys, self.pred)):
+            if pk == self.cur and kk == key:
+                return k
+        return -1
+
+    def callbacks(self, n, errors):
+        def need(xp, _data):
+            try:
+                return int(self.node(self.to_params(np.ctypeslib.as_array(xp, shape=(n,)).copy())) < 0)
+            except BaseException as e:
+                errors.append(e)
+                return 1
+
+        def tree(xp, predp, n_pts, _data):
+            try:
+                self.active = False
+                if self.off:
+                    return
+                xs = np.ctypeslib.as_array(xp, shape=(n_pts, n))
+                pts = np.stack([self.to_params(xs[k].copy()) for k in range(n_pts)])
+                pred = np.ctypeslib.as_array(predp, shape=(n_pts,)).copy()
+                r = self.f.total_likelihood_tree(pts, pred)
+                if r is None:   # no path launch on this handle: call by call
+                    self.off = True
+                    return
+                self.keys = [np.ascontiguousarray(p).tobytes() for p in pts]
+                self.pred, self.res, self.cur, self.active = list(pred), r, -1, True
+            except BaseException as e:
+                errors.append(e)
+                self.off = True
+        self._cbs = (N.AHEAD_NEED_FN(need), N.AHEAD_TREE_FN(tree))   # kept alive for the run
+        return self._cbs
+
+    def call(self, params) -> float:
+        k = self.node(params)
+        if k < 0:
+            self.active = False
+            return self.f.total_likelihood(params)
+        self.cur = k
+        self.f.keep_point_state(k)
+        ll, st, nc, nr = (a[k] for a in self.res)
+        if st == N.GGP_ENAN:
+            raise self.f._nan(int(nc), int(nr))
+        self.f._stalled(int(st))
+        self.f._check(int(st))
+        return float(ll)
 
 
 def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, search_space: str = "log",
@@ -81,8 +152,14 @@ def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, 
                 dx[i] = math.log(1.0 + params.step[i] / init[i]) if log else params.step[i]
                 lb[i] = ln(params.lower[i])
                 ub[i] = ln(params.upper[i])
-    f = (lambda v: -objective(np.exp(v))) if log else (lambda v: -objective(v))
-    xb, minf, rc, _ = nldrmd_minimize(f, x, lb, ub, dx, tolerance, maxeval)
+    to_params = (lambda v: np.exp(v)) if log else (lambda v: v)
+    forest = _chain_forest(objective)
+    ahead = None
+    if forest is not None and os.environ.get("GGP_NM_LOOKAHEAD", "1") != "0":
+        ahead = _Ahead(forest, to_params)   # a Forest: the lookahead (the same calls)
+        objective = ahead.call
+    f = lambda v: -objective(to_params(v))  # noqa: E731
+    xb, minf, rc, _ = nldrmd_minimize(f, x, lb, ub, dx, tolerance, maxeval, ahead)
     if rc == INVALID_ARGS:
         raise ValueError("nlopt invalid argument")
     if rc == FAILURE:

@@ -114,6 +114,20 @@ int ggp_nldrmd_minimize(int32_t n, ggp_objective_fn f, void *data, const double 
                         double *x, const double *dx, double ftol_abs, int64_t maxeval, double *minf,
                         int64_t *nevals);
 
+/* ggp_nldrmd_minimize with the lookahead (csrc/host/ggp_nelder_mead.h Lookahead), for an
+ * objective whose calls carry state: need(x, data) returns non-zero when the objective cannot
+ * serve the call x from what it evaluated ahead; tree(x, pred, n_pts, data) then receives the
+ * run's possible next calls (n_pts points, n doubles each; pred[i] = the point whose state point i
+ * starts from, -1 = the next call) to evaluate ahead, e.g. with ggp_total_loglik_tree.  depth /
+ * max_nodes bound the tree (<= 0: 2 / 40).  The calls made, and the result, are those of
+ * ggp_nldrmd_minimize. */
+typedef int (*ggp_ahead_need_fn)(const double *x, void *data);
+typedef void (*ggp_ahead_tree_fn)(const double *x, const int32_t *pred, int32_t n_pts, void *data);
+int ggp_nldrmd_minimize_ahead(int32_t n, ggp_objective_fn f, ggp_ahead_need_fn need, ggp_ahead_tree_fn tree,
+                              void *data, const double *lb, const double *ub, double *x, const double *dx,
+                              double ftol_abs, int64_t maxeval, double *minf, int64_t *nevals, int32_t depth,
+                              int32_t max_nodes);
+
 /* num_hessian_ll (likelihood.h:211-258): central 4-point differences over the parameters
  * idx[0..k-1] of x, h_i = max(x_i * epsilon, 1e-12), evaluated in the reference's order
  * (i, j, then ++ +- -+ --).  out: k*k row-major.  Returns 0, or the callback's stop. */

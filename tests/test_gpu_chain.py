@@ -161,3 +161,37 @@ def test_hessian_chained_equals_num_hessian(example):
     H_seq = opt.num_hessian(lambda p: b.total_likelihood(p), P0, idx, 1e-2)
     assert np.array_equal(H_chain, H_seq)
     assert np.array_equal(a.state(), b.state())
+
+
+def test_python_minimize_lookahead_is_the_same_run(example, tmp_path, monkeypatch):
+    """optimize.minimize_wrapper on a Forest objective takes the lookahead
+    (ggp_nldrmd_minimize_ahead + ggp_total_loglik_tree): the same result, evaluation count and
+    carried state as the call-by-call run (GGP_NM_LOOKAHEAD=0)"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as opt
+    names = ["mean_lambda", "gamma_lambda", "var_lambda", "mean_q", "gamma_q", "var_q", "beta",
+             "var_x", "var_g", "var_dx", "var_dg"]
+    free = {0: "2.31E-03, 2.31E-04", 7: "3.35E-04, 3.35E-05", 8: "8.26E-01, 8.26E-02"}
+    pf = tmp_path / "p.txt"
+    pf.write_text("".join(f"{n} = {free.get(i, repr(float(P0[i])))}\n" for i, n in enumerate(names)))
+    P = g.ParameterSet.load(str(pf))
+    runs = {}
+    for tag in ("seq", "ahead"):
+        if tag == "seq":
+            monkeypatch.setenv("GGP_NM_LOOKAHEAD", "0")
+        else:
+            monkeypatch.delenv("GGP_NM_LOOKAHEAD", raising=False)
+        f = g.Forest(example)
+        calls = []
+        orig = f.total_likelihood
+
+        def counted(p, orig=orig, calls=calls):   # the calls the run makes (not the speculated ones)
+            calls.append(np.array(p, copy=True))
+            return orig(p)
+        x, ll, rc = opt.minimize_wrapper(f.total_likelihood if tag == "ahead" else counted, P, tolerance=1e-3,
+                                         search_space="log", maxeval=400)
+        runs[tag] = (x, ll, rc, f.state(), len(calls))
+    a, b = runs["seq"], runs["ahead"]
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2]
+    assert np.array_equal(a[3], b[3])
+    assert a[4] > 50
