@@ -409,3 +409,22 @@ def test_cli_lookahead_and_chain_give_the_sequential_files(tmp_path, example_pat
         assert outs["seq"][n] == outs["fast"][n], n
     it = [n for n in outs["fast"] if n.endswith("_iterations.csv")]
     assert len(it) == 1 and len(_ll_table(str(tmp_path / "fast" / it[0]))) > 40, it
+
+
+def test_cli_lookahead_nan_run_fails_like_the_sequential_one(tmp_path, example_paths):
+    """-m in linear space with var_x free below zero: the run meets a NaN likelihood and quits
+    (likelihood.h:71-93).  With the lookahead (a speculated call may be NaN without being made) the
+    iteration log and the error log are byte for byte the call-by-call run's"""
+    pf = _param_file(tmp_path / "p.txt", {7: "3.35E-04, 5.0E-04, -1.0E-03, 1.0E-03", 8: "8.26E-01, 8.26E-02"})
+    outs = {}
+    for tag, env in (("seq", {"GGP_NM_LOOKAHEAD": "0", "GGP_CHAIN_FUSED": "0"}), ("fast", {})):
+        r = subprocess.run([CLI, "-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-m",
+                            "-space", "linear", "-t", "1e-6", "-o", str(tmp_path / tag)], capture_output=True, text=True,
+                           timeout=600, cwd=tmp_path, env=dict(os.environ, **env))
+        assert r.returncode != 0 and "Likelihood is Nan" in r.stdout, r.stdout[-800:]
+        outs[tag] = {n: open(tmp_path / tag / n, "rb").read().replace(str(tmp_path / tag).encode(), b"OUT")
+                     for n in sorted(os.listdir(tmp_path / tag))}   # the logs name the output directory
+    assert sorted(outs["seq"]) == sorted(outs["fast"])
+    assert any(n.endswith("_error.log") for n in outs["seq"])
+    for n in outs["seq"]:
+        assert outs["seq"][n] == outs["fast"][n], n
