@@ -34,6 +34,8 @@ class _Stop(Exception):
 
 def _callback(f, n, errors: list):
     def cb(xp, vp, _data):
+        if errors:   # a lookahead callback failed: stop the run there (re-raised by the caller)
+            return 1
         try:
             vp[0] = float(f(np.ctypeslib.as_array(xp, shape=(n,)).copy()))
             return 0
