@@ -195,3 +195,21 @@ def test_python_minimize_lookahead_is_the_same_run(example, tmp_path, monkeypatc
     assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2]
     assert np.array_equal(a[3], b[3])
     assert a[4] > 50
+
+
+def test_python_scan_chained_equals_calls(example, tmp_path):
+    """optimize.bound_1dscan on a Forest objective (one chained call per parameter) gives the
+    call-by-call values bitwise, and leaves the same carried state"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as opt
+    names = ["mean_lambda", "gamma_lambda", "var_lambda", "mean_q", "gamma_q", "var_q", "beta",
+             "var_x", "var_g", "var_dx", "var_dg"]
+    bound = {8: "8.26E-01, 1.0E-01, 4.0E-01, 1.3E+00", 7: "3.35E-04, 1.0E-04, 1.0E-04, 9.0E-04"}
+    pf = tmp_path / "p.txt"
+    pf.write_text("".join(f"{n} = {bound.get(i, repr(float(P0[i])))}\n" for i, n in enumerate(names)))
+    P = g.ParameterSet.load(str(pf))
+    a, b = g.Forest(example), g.Forest(example)
+    ra = opt.bound_1dscan(a.total_likelihood, P)
+    rb = opt.bound_1dscan(lambda p: b.total_likelihood(p), P)
+    assert ra == rb and sum(len(v) for v in ra.values()) > 10
+    assert np.array_equal(a.state(), b.state())
