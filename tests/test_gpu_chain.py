@@ -213,3 +213,30 @@ def test_python_scan_chained_equals_calls(example, tmp_path):
     rb = opt.bound_1dscan(lambda p: b.total_likelihood(p), P)
     assert ra == rb and sum(len(v) for v in ra.values()) > 10
     assert np.array_equal(a.state(), b.state())
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0, 0)])
+def test_tree_points_bitwise_their_call_sequences(devices):
+    """ggp_total_loglik_tree: every point's value is bitwise a ggp_total_loglik call made after
+    the calls of its predecessor chain (emulated with state snapshots), the carried state is left
+    alone, and keep_point_state(i) adopts exactly the state point i's call leaves -- on one shard
+    and on three logical shards of a 48-tree forest"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(48, 120)
+    pts = _points(7, seed=12)
+    pred = np.array([-1, 0, 0, 1, 1, 2, 4], np.int32)
+    f = g.Forest(hf, devices=list(devices))
+    f.total_likelihood(P0)
+    st0 = f.state()
+    ll, status, nc, nr = f.total_likelihood_tree(pts, pred)
+    assert (status == 0).all() and (nc == -1).all()
+    assert np.array_equal(f.state(), st0)                      # nothing adopted yet
+    e = g.Forest(hf, devices=list(devices))
+    after = {}
+    for i in range(len(pts)):
+        e.set_state(st0 if pred[i] < 0 else after[pred[i]])
+        assert e.total_likelihood(pts[i]) == ll[i], i
+        after[i] = e.state()
+    for i in (6, 3, 0):
+        f.keep_point_state(i)
+        assert np.array_equal(f.state(), after[i]), i
