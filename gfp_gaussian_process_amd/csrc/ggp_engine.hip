@@ -459,6 +459,41 @@ __global__ __launch_bounds__(256) void k_replicate(const double *__restrict__ sr
 // the G lanes through LDS (ggp_prop.h tasks), cutting the per-step latency that bounds
 // small forests.  Bitwise identical to the lane schedule.
 // ------------------------------------------------------------------------------------------
+// Optional launch timeline (tools/timeline.hip builds this file with GGP_TIMELINE; the shipped
+// library never does): lane 0 of each path block writes the constant 100 MHz clock at the
+// phases of its launch, g_tl[block][phase], so the fixed cost of a launch can be attributed.
+#ifdef GGP_TIMELINE
+__device__ unsigned long long g_tl[8192 * 8];
+#define GGP_TL(k)                                                                              \
+    do {                                                                                       \
+        __builtin_amdgcn_s_waitcnt(0);                                                         \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8192)                          \
+            g_tl[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+// per-launch event counts (g_cnt): steady steps, steps whose stage B took a rare branch (some
+// lane), dt-cache refreshes, row-chunk loads
+__device__ unsigned long long g_cnt[4];
+#define GGP_TL_CNT_DECL unsigned tl_cnt[4] = {0, 0, 0, 0}
+#define GGP_TL_CNT(k, cond) tl_cnt[k] += (cond) ? 1u : 0u
+#define GGP_TL_CNT_FLUSH()                                                                     \
+    do {                                                                                       \
+        if (threadIdx.x == 0)                                                                  \
+            for (int k_ = 0; k_ < 4; ++k_) atomicAdd(&g_cnt[k_], (unsigned long long)tl_cnt[k_]); \
+    } while (0)
+// where the block runs: HW_ID (wave, SIMD, CU, SH, SE) in the low word, XCC_ID in the high word
+#define GGP_TL_HWID()                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8192)                          \
+            g_tl[blockIdx.x * 8 + 7] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |  \
+                                       ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32); \
+    } while (0)
+#else
+#define GGP_TL(k)
+#define GGP_TL_HWID()
+#define GGP_TL_CNT_DECL
+#define GGP_TL_CNT(k, cond)
+#define GGP_TL_CNT_FLUSH()
+#endif
 // Optional per-stage cycle stamps (tools/stamp_group.hip builds this file with GGP_STAMPS;
 // the shipped library never does).
 #ifdef GGP_STAMPS
@@ -728,6 +763,10 @@ constexpr unsigned kChainQuietPerRow = 1100;    // s_memtime units (~0.5 us) of 
 // the block result straight to its mapped host slots and counts the block; the last block
 // publishes the call's sequence number.  Counters are agent-scope atomics with few arrivals
 // (a block: its paths; done: the blocks); the last arrival resets its counter for the next call.
+// The ChainRed travels as a kernel argument (no pointer to chase at the end of the launch), and
+// each path's block, its path count and tree bounds are loaded at the launch's start
+// (RedPre): the reduction's only round trips are the block count, the cells' results (all
+// lanes at once), the host slots and the done count.
 struct ChainRed {
     const int32_t *path_blk;      // local block of each path
     const int32_t *blk_npaths;    // paths per local block
@@ -737,7 +776,7 @@ struct ChainRed {
     int64_t *out_seq;
     double *host_sum;
     long long *host_nan;
-    int n_lblocks;
+    int n_lblocks;                // 0: no in-launch reduction
 };
 constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
 
@@ -758,46 +797,122 @@ GGP_DEV T ld_agent_i(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED,
 template <class T>
 GGP_DEV void st_agent_i(T *p, const T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-GGP_DEV void chain_reduce(const ChainRed &R, const int64_t seq, const int b, const int lane, const double *cell_ll,
-                          const int32_t *cell_nan)
+// what the reduction of path b needs, loaded at the launch's start and parked in LDS (red[0..63]:
+// lane k <= nb the DFS start of the block's tree k, k = nb its end; red[64..66]: the block j, its
+// path count, nb), so no register holds it through the steps
+struct RedPre {
+    int j, npaths, nb;
+    int64_t tb;
+};
+GGP_DEV RedPre red_load(const ChainRed &R, const int b, const int lane)
 {
-    if (lane != 0) return;
+    RedPre q{0, 0, 0, 0};
+    if (R.n_lblocks <= 0) return q;
+    q.j = R.path_blk[b];
+    q.npaths = R.blk_npaths[q.j];
+    q.nb = R.blk_nt[q.j];
+    const int t0 = R.blk_t0[q.j];
+    q.tb = lane <= q.nb ? R.tree_dfs[t0 + lane] : 0;
+    return q;
+}
+GGP_DEV void red_park(const RedPre &q, double *red, const int lane)
+{
+    red[lane] = __longlong_as_double((long long)q.tb);
+    if (lane == 0) {
+        red[64] = (double)q.j;
+        red[65] = (double)q.npaths;
+        red[66] = (double)q.nb;
+    }
+}
+GGP_DEV RedPre red_unpark(const double *red, const int lane)
+{
+    RedPre q;
+    q.tb = (int64_t)__double_as_longlong(red[lane]);
+    q.j = __builtin_amdgcn_readfirstlane((int)red[64]);
+    q.npaths = __builtin_amdgcn_readfirstlane((int)red[65]);
+    q.nb = __builtin_amdgcn_readfirstlane((int)red[66]);
+    return q;
+}
+
+// every lane of the path's wave calls it after the path's last cell results are stored; scr:
+// 192 doubles of the wave's LDS that nothing reads any more
+GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq, const int lane, const double *cell_ll,
+                          const int32_t *cell_nan, double *scr)
+{
     __builtin_amdgcn_s_waitcnt(0);   // this path's cell results are at the coherence point
-    const int j = R.path_blk[b];
-    if (add_agent(R.cnt_blk + j) + 1 != (unsigned)R.blk_npaths[j]) return;
-    zero_agent(R.cnt_blk + j);
-    const int t0 = R.blk_t0[j], nb = R.blk_nt[j];
+    int last = 0;
+    if (lane == 0) last = add_agent(R.cnt_blk + q.j) + 1 == (unsigned)q.npaths;
+    if (__builtin_amdgcn_readfirstlane(last) == 0) return;
+    if (lane == 0) zero_agent(R.cnt_blk + q.j);
+    // the block's cells [c_lo, c_hi) in DFS order, 64 at a time: every lane loads one cell's
+    // result, lane 0 adds them tree by tree in DFS order (k_reduce_blocks' per-thread loop)
+    const int nb = q.nb;
+    double *s_ll = scr, *s_end = scr + 128;
+    int32_t *s_nan = reinterpret_cast<int32_t *>(scr + 64);
+    s_end[lane] = __longlong_as_double((long long)q.tb);
+    const int64_t c_lo = (int64_t)__shfl((long long)q.tb, 0, 64);
+    const int64_t c_hi = (int64_t)__shfl((long long)q.tb, nb, 64);
     double sv[8];
     long long sn[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {   // tree sums, each in DFS order (k_reduce_blocks' per-thread loop)
-        double v = 0.0;
-        long long code = kChainNoNan;
-        if (k < nb)
-            for (int64_t i = R.tree_dfs[t0 + k]; i < R.tree_dfs[t0 + k + 1]; ++i) {
-                v += ld_agent(cell_ll + i);
-                const int nr = ld_agent_i(cell_nan + i);
-                if (nr != kNanNone && code == kChainNoNan) code = ((long long)R.gdfs[i] << 24) | (long long)nr;
-            }
-        sv[k] = v;
-        sn[k] = code;
+    for (int k = 0; k < 8; ++k) {
+        sv[k] = 0.0;
+        sn[k] = kChainNoNan;
     }
+    int k = 0;
+    int64_t k_end = 0;
+    for (int64_t base = c_lo; base < c_hi; base += 64) {
+        const int64_t i = base + lane;
+        double x = 0.0;
+        int nr = kNanNone;
+        if (i < c_hi) {
+            x = ld_agent(cell_ll + i);
+            nr = ld_agent_i(cell_nan + i);
+        }
+        s_ll[lane] = x;
+        s_nan[lane] = nr;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            const int64_t top = base + 64 < c_hi ? base + 64 : c_hi;
+            if (base == c_lo) k_end = (int64_t)__double_as_longlong(s_end[1]);
+            for (int64_t c = base; c < top; ++c) {
+                while (c >= k_end && k + 1 < nb) {
+                    ++k;
+                    k_end = (int64_t)__double_as_longlong(s_end[k + 1]);
+                }
+                const double v = s_ll[c - base];
+                const int r = s_nan[c - base];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u == k) {
+                        sv[u] += v;
+                        if (r != kNanNone && sn[u] == kChainNoNan) sn[u] = ((long long)R.gdfs[c] << 24) | (long long)r;
+                    }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane != 0) return;
 #pragma unroll
     for (int w = 32; w >= 1; w >>= 1)   // k_reduce_blocks' tree over 64 slots; slots >= 8 hold 0
 #pragma unroll
-        for (int k = 0; k < 8 && k < w; ++k) {
-            sv[k] = sv[k] + (k + w < 8 ? sv[(k + w) & 7] : 0.0);
-            sn[k] = min(sn[k], k + w < 8 ? sn[(k + w) & 7] : kChainNoNan);
+        for (int u = 0; u < 8 && u < w; ++u) {
+            sv[u] = sv[u] + (u + w < 8 ? sv[(u + w) & 7] : 0.0);
+            sn[u] = min(sn[u], u + w < 8 ? sn[(u + w) & 7] : kChainNoNan);
         }
     // the block result to its mapped host slots (system-coherent stores), complete before the count
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(R.host_sum + j), (unsigned long long)__double_as_longlong(sv[0]),
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(R.host_sum + q.j), (unsigned long long)__double_as_longlong(sv[0]),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(R.host_nan + j, sn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(R.host_nan + q.j, sn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_s_waitcnt(0);
     if (add_agent(R.done) + 1 != (unsigned)R.n_lblocks) return;
     zero_agent(R.done);
-    // every block's slots were written before its count: the sequence number last (the host polls it)
-    __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // every block's slots reached host memory before its count (each block waited for its stores
+    // before adding): the sequence number last, a plain system-scope store (a release here would
+    // also write back this XCD's L2, which holds nothing the host reads)
+    __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -822,7 +937,7 @@ template <bool CHAIN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
-    const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed *__restrict__ red, const int64_t call_seq,
+    const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed red, const int64_t call_seq,
     const unsigned spin_max, const double *__restrict__ ptab, const double *__restrict__ carry,
     const int32_t *__restrict__ pt_pred)
 {
@@ -832,8 +947,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int lane = threadIdx.x;
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
-    lds_fill<W::kTabRows * W::kTabRow>(lds + W::L_TAB, lane, [](const int k) { return W::tab_entry(k); });
-    GGP_PSTAMP(1);
+    GGP_TL(0);
+    GGP_TL_HWID();
+    GGP_TL_CNT_DECL;
+    // every global load of the launch's setup is issued before the first wait: the reduction's
+    // block tables, the Dawson/exp table, this lane's row of the lane constants and the first
+    // cell's first 64 rows; make_ou runs while they are in flight
+    const RedPre rq0 = red_load(red, blockIdx.x, lane);
+    constexpr int kTabN = W::kTabRows * W::kTabRow, kTabR = (kTabN + 63) / 64;
+    double tab_v[kTabR];
+#pragma unroll
+    for (int j = 0; j < kTabR; ++j) tab_v[j] = W::tab_entry(min(lane + 64 * j, kTabN - 1));
+    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
+    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
+    double pre_l = 0.0, pre_f = 0.0, pre_t = 0.0, pre_t64 = 0.0;   // the first cell's chunk [r0, r0 + 64)
+    {
+        const int c = cells[i_lo];
+        const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1], rr = r0 + lane;
+        if (rr < r1) {
+            pre_l = F.logl[rr];
+            pre_f = F.fp[rr];
+            pre_t = F.time[rr];
+        }
+        if (lane == 0 && r0 + 64 < r1) pre_t64 = F.time[r0 + 64];
+    }
     const double *p = P.p;
     // chained evaluations (ggp_total_loglik_chain / _tree): blockIdx.y = point; the point's
     // parameter row and its state / ll / NaN / done slices of n cells each.  A point's roots start
@@ -851,7 +988,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     W::Lane L;
     {
         const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
-        lds[W::L_MONO + lane] = W::lane_kappa(lane, ou);   // the 33 kappas, one per lane (MONO is free here)
+        const double kap = W::lane_kappa(lane, ou);
+#pragma unroll
+        for (int j = 0; j < kTabR; ++j)
+            if (lane + 64 * j < kTabN) lds[W::L_TAB + lane + 64 * j] = tab_v[j];
+        if (red.n_lblocks > 0) red_park(rq0, lds + W::L_RED, lane);
+        lds[W::L_ROWL + lane] = pre_l;   // the first cell's chunk (its loop iteration loads no rows)
+        lds[W::L_ROWF + lane] = pre_f;
+        lds[W::L_ROWT + lane] = pre_t;
+        if (lane == 0) lds[W::L_ROWT + 64] = pre_t64;
+        GGP_PSTAMP(1);
+        GGP_TL(1);
+        lds[W::L_MONO + lane] = kap;   // the 33 kappas, one per lane (MONO is free here)
         wave_sync();
         L = W::lane_from(lane, LC, ou, lds + W::L_MONO);
         wave_sync();
@@ -866,12 +1014,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         lds[W::L_ZERO] = 0.0;
     }
     GGP_PSTAMP(2);
+    GGP_TL(2);
     // exp(s t) and the exp-derived basis depend on the parameters and dt only; dt compared by its
     // bits (a NaN pattern no time difference produces: nothing cached yet)
     unsigned long long dt_cached = 0x7ff4dead0000beefULL;
+    // the dt cache's keys start as that pattern too; way dt_victim is replaced next
+    if (lane < W::kDtWays) lds[W::L_DTK + lane] = __longlong_as_double((long long)dt_cached);
+    int dt_victim = 0;
+    const int dt_my_slot = W::dt_slot(lane < W::kDtVals ? lane : 0);
     GGP_STAMP_DECL;
-    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
-    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
     int64_t prev_last = -1;
     // the cell's first state into POST (lanes' entries) and V (stage D's variables), from registers
     // holding the same values in every lane (once per cell)
@@ -890,13 +1041,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const long long db = __double_as_longlong(dt);
         const unsigned long long dbits = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(db >> 32)) << 32) |
                                          (unsigned)__builtin_amdgcn_readfirstlane((int)(db & 0xffffffff));
+        GGP_TL_CNT(2, dbits != dt_cached);
         if (dbits != dt_cached) {   // lane constants and kernel arguments only: no OU values live in the loop
-            if (lane < 7) lds[lane < 6 ? W::L_X + ggp::XS_bt + lane : W::L_XPGQ] = exp(L.c_sv * dt);
-            wave_sync();
-            if (lane < ggp::kNDerived)
-                lds[W::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W::L_X, p[1], dt);
-            if (lane == 0) lds[W::L_V + ggp::V_T] = dt;
-            wave_sync();
+            // a cached way of this dt (lane w compares key w): its values to the working slots;
+            // else computed, then saved into way dt_victim (bitwise the same values either way)
+            const unsigned long long key = (unsigned long long)__double_as_longlong(lds[W::L_DTK + (lane & (W::kDtWays - 1))]);
+            const unsigned long long hit = __ballot(lane < W::kDtWays && key == dbits);
+            if (hit != 0ull) {
+                const int way = __builtin_ctzll(hit);
+                if (lane < W::kDtVals) lds[dt_my_slot] = lds[W::L_DTC + W::kDtVals * way + lane];
+                if (lane == 0) lds[W::L_V + ggp::V_T] = dt;
+                wave_sync();
+            } else {
+                if (lane < 7) lds[lane < 6 ? W::L_X + ggp::XS_bt + lane : W::L_XPGQ] = exp(L.c_sv * dt);
+                wave_sync();
+                if (lane < ggp::kNDerived)
+                    lds[W::L_BV + ggp::BV_R_EBT + lane] = ggp::derived_generic(ggp::kDerived[lane], lds + W::L_X, p[1], dt);
+                if (lane == 0) lds[W::L_V + ggp::V_T] = dt;
+                wave_sync();
+                if (lane < W::kDtVals) lds[W::L_DTC + W::kDtVals * dt_victim + lane] = lds[dt_my_slot];
+                if (lane == 0) lds[W::L_DTK + dt_victim] = __longlong_as_double((long long)dbits);
+                dt_victim = (dt_victim + 1) & (W::kDtWays - 1);
+            }
             dt_cached = dbits;
         }
         const double *po = lds + W::L_POST;
@@ -906,6 +1072,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         {   // stage B: one exponential or Dawson value per lane
             const W::BOut o = W::stageB(S, L, lds);
             double v = o.v;
+            GGP_TL_CNT(1, __builtin_amdgcn_readfirstlane(__ballot(o.rare) != 0 ? 1 : 0));
             if (o.rare) v = W::stageB_rare(L.b_isD, o.arg, o.z, o.v);   // skipped (execz) when no lane needs it
             lds[L.b_dst] = v;
         }
@@ -996,6 +1163,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         double t_cur = F.time[r0];
         prev_last = r1 - 1;
         GGP_PSTAMP(3);
+        if (i == i_lo) GGP_TL(3);
         // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane)
         auto load_chunk = [&](const int64_t base) {
             const int64_t rr = base + lane;
@@ -1010,7 +1178,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             lds[W::L_ROWT + lane] = t;
             if (lane == 0) lds[W::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
         };
-        load_chunk(r0);
+        if (i != i_lo) load_chunk(r0);   // the first cell's chunk is in LDS since the launch's start
         wave_sync();
         double cl = 0.0;
         int nan_row = kNanNone;
@@ -1068,6 +1236,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) return false;
                 slot = 0;
                 if (live) load_chunk(r0 + done);
+                GGP_TL_CNT(3, live);
             }
             GGP_STAMP(10);
             wave_sync();   // the LDS slots are rewritten by the next step
@@ -1114,6 +1283,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         GGP_PSTAMP(5);
         while (live) {   // steady steps: the state distributed over lanes 0-19
             GGP_STAMP_STEP();
+            GGP_TL_CNT(0, true);
             const double t_next = left > 1 ? lds[W::L_ROWT + slot + 1] : 0.0;
             propagate(dt);
             {
@@ -1147,6 +1317,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (!end_step()) break;
         }
         GGP_PSTAMP(6);
+        GGP_TL(4);
         wave_sync();
         // the cell's results; its state from lanes 0-19 (one coalesced store), agent-coherent with
         // the flag after it when a second daughter waits for it
@@ -1166,11 +1337,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (lane == 0) __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         GGP_PSTAMP(7);
+        GGP_TL(5);
         wave_sync();   // the LDS rows and ring are the next cell's
     }
     GGP_STAMP_FLUSH();
     GGP_PSTAMP_FLUSH();
-    if (red) chain_reduce(*red, call_seq, blockIdx.x, lane, cell_ll, cell_nan);
+    if (red.n_lblocks > 0) chain_reduce(red, red_unpark(lds + W::L_RED, lane), call_seq, lane, cell_ll, cell_nan, lds + W::L_RX0);
+    GGP_TL(6);
+    GGP_TL_CNT_FLUSH();
 }
 
 
@@ -2144,7 +2318,7 @@ struct Shard {
     // arrival counters
     int32_t *d_path_blk = nullptr, *d_blk_npaths = nullptr;
     unsigned *d_cnt_blk = nullptr;
-    void *d_red = nullptr;             // the ChainRed of the path launch (device copy)
+    ChainRed red{};                    // the path launch's in-launch reduction (a kernel argument)
     std::vector<int32_t> level_kind;   // GGP_KERNEL_* each level runs
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
     int64_t n_trees = 0, n_lblocks = 0;
@@ -2299,7 +2473,7 @@ int launch_levels(Shard *f, const ggp_params &P)
         HIPCHK(prof_begin());
         hipLaunchKernelGGL(k_loglik_wave<false>, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
                            f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
-                           f->d_cell_done, f->epoch, f->d_path_seq, (const ChainRed *)f->d_red, f->seq, f->spin_max,
+                           f->d_cell_done, f->epoch, f->d_path_seq, f->red, f->seq, f->spin_max,
                            (const double *)nullptr, (const double *)nullptr, (const int32_t *)nullptr);
         HIPCHK(hipGetLastError());
         f->kernel_used = GGP_KERNEL_WAVE;
@@ -2317,7 +2491,7 @@ int launch_levels(Shard *f, const ggp_params &P)
         if (kind == GGP_KERNEL_WAVE) {
             hipLaunchKernelGGL(k_loglik_wave<false>, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
                                f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
-                               (const int32_t *)nullptr, (const ChainRed *)nullptr, (int64_t)0, f->spin_max,
+                               (const int32_t *)nullptr, ChainRed{}, (int64_t)0, f->spin_max,
                                (const double *)nullptr, (const double *)nullptr, (const int32_t *)nullptr);
             f->kernel_used = GGP_KERNEL_WAVE;
             f->last_code = GGP_KERNEL_WAVE << 8 | 64;
@@ -2499,7 +2673,7 @@ void shard_destroy(Shard *f)
                     (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
                     (void *)f->d_blk_sum, (void *)f->d_blk_nan, (void *)f->d_chain, (void *)f->d_cell_done,
                     (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_blk,
-                    (void *)f->d_blk_npaths, (void *)f->d_cnt_blk, f->d_red,
+                    (void *)f->d_blk_npaths, (void *)f->d_cnt_blk,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -2806,9 +2980,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
                 R.host_sum = f->m_sum;
                 R.host_nan = (long long *)f->m_nan;
                 R.n_lblocks = (int)f->n_lblocks;
-                ChainRed *dr = nullptr;
-                check(dev_upload(&dr, &R, 1));
-                f->d_red = dr;
+                f->red = R;
             }
         }
         check(dev_upload(&f->d_chain, ch.data(), nc));
@@ -3701,7 +3873,7 @@ static int run_points(ggp_forest *f, int64_t np, const double *params, const int
         ++s->epoch;
         hipLaunchKernelGGL(k_loglik_wave<true>, dim3((unsigned)s->n_paths, (unsigned)np), dim3(64), 0, s->stream, s->F, P0,
                            s->d_path_cells, (int)nc, s->d_b_state, s->d_b_ll, s->d_b_nan, s->d_chain, s->d_b_done, s->epoch,
-                           s->d_path_seq, (const ChainRed *)nullptr, (int64_t)0, s->spin_max, (const double *)s->d_b_ptab,
+                           s->d_path_seq, ChainRed{}, (int64_t)0, s->spin_max, (const double *)s->d_b_ptab,
                            (const double *)s->d_state, pred ? (const int32_t *)s->d_b_pred : (const int32_t *)nullptr);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,

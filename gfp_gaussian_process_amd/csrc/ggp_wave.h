@@ -295,8 +295,19 @@ enum {
     L_ROWF = L_ROWL + 64,
     L_ROWT = L_ROWF + 64,
     L_DUMMY = L_ROWT + 66,                        // one slot per lane for stores without a task
-    kLds = L_DUMMY + 64
+    L_RED = L_DUMMY + 64,                         // the in-launch reduction's prefetched tables
+    L_DTK = L_RED + 68,                           // the dt cache: kDtWays keys (dt's bits), then
+    L_DTC = L_DTK + 8,                            // per way the kDtVals values that depend on dt only
+    kLds = L_DTC + 8 * 25
 };
+// the dt cache: the values a step reads that depend on the parameters and dt only (the six
+// exp(s t), exp(+gq t) and the 18 exp-derived basis values), kept for the last kDtWays distinct
+// dt of the block (a cell's times are floats: the example's dt = 1 comes in 13 bit patterns,
+// alternating, so one entry missed 36% of its steps)
+constexpr int kDtWays = 8, kDtVals = 7 + kNDerived;
+static_assert(kDtVals == 25, "the cache way layout holds 25 values");
+// the working slot of cached value v (lane v copies it)
+constexpr int dt_slot(const int v) { return v < 6 ? L_X + XS_bt + v : v == 6 ? L_XPGQ : L_BV + BV_R_EBT + (v - 7); }
 static_assert(L_X % 2 == 0 && L_TAB == 0, "128-bit table rows");
 static_assert(L_RT % 2 == 0, "128-bit ll-term reads");
 

@@ -197,3 +197,58 @@ def test_path_launch_bitwise_equal_to_level_launches(monkeypatch):
             f.total_likelihood(bad)
         got.append((e.value.cell, e.value.row))
     assert got[0] == got[1]
+
+
+def _shards_of(lib, h):
+    import ctypes
+    n = ctypes.c_int32()
+    assert lib.ggp_forest_shards(h, ctypes.byref(n), None, None, None, 0) == 0
+    dv = (ctypes.c_int32 * max(1, n.value))()
+    rows = (ctypes.c_int64 * max(1, n.value))()
+    cells = (ctypes.c_int64 * max(1, n.value))()
+    assert lib.ggp_forest_shards(h, ctypes.byref(n), dv, rows, cells, n.value) == 0
+    return [(dv[k], rows[k], cells[k]) for k in range(n.value)]
+
+
+def test_descriptor_device_sets():
+    """The device-set values INTEGRATION.md's binding documents, through the raw C-ABI: a
+    zero-filled descriptor's n_devices = 0 is device 0 only (one shard); GGP_ALL_DEVICES (-1) is
+    one shard per visible device (ggp_device_count); n > 0 with devices = NULL is ordinals
+    0..n-1.  Every form gives the same total (include/ggp.h "Sharding")."""
+    import ctypes
+    from gfp_gaussian_process_amd import _native as N
+    lib = N.engine()
+    hf = _forest(64, 40)
+    nd = ctypes.c_int32()
+    assert lib.ggp_device_count(ctypes.byref(nd)) == 0 and nd.value >= 1
+    P = np.asarray(INIT, np.float64)
+    cases = {"zero": (0, [(0, hf.n_rows, hf.n_cells)]),
+             "all": (N.GGP_ALL_DEVICES, None),
+             "one": (1, [(0, hf.n_rows, hf.n_cells)])}
+    lls = {}
+    for name, (n_dev, want) in cases.items():
+        d = hf.desc()
+        d.n_devices, d.devices = n_dev, None
+        h = ctypes.c_void_p()
+        rc = lib.ggp_forest_create(ctypes.byref(d), ctypes.byref(h))
+        assert rc == 0, (name, rc)
+        try:
+            sh = _shards_of(lib, h)
+            if want is not None:
+                assert sh == want, (name, sh)
+            else:   # every visible device once, the forest split by whole trees
+                assert sorted(s[0] for s in sh) == list(range(nd.value)), sh
+                assert sum(s[1] for s in sh) == hf.n_rows and sum(s[2] for s in sh) == hf.n_cells
+            ll, nc, nr = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+            assert lib.ggp_total_loglik(h, P.ctypes.data_as(N.c_double_p), ctypes.byref(ll), ctypes.byref(nc),
+                                        ctypes.byref(nr)) == 0
+            lls[name] = ll.value
+        finally:
+            lib.ggp_forest_destroy(h)
+    assert lls["zero"] == lls["all"] == lls["one"], lls
+    # a descriptor naming a device that does not exist is refused, not silently remapped
+    d = hf.desc()
+    bad = np.asarray([nd.value], np.int32)
+    d.n_devices, d.devices = 1, bad.ctypes.data_as(N.c_int32_p)
+    h = ctypes.c_void_p()
+    assert lib.ggp_forest_create(ctypes.byref(d), ctypes.byref(h)) != 0

@@ -3,7 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include \
 //     -I gfp_gaussian_process_amd/csrc -o tools/stamp_group tools/stamp_group.hip \
 //     -L gfp_gaussian_process_amd/lib -lggp_host -Wl,-rpath,$PWD/gfp_gaussian_process_amd/lib
-//   tools/stamp_group TREES [KERNEL=2]
+//   tools/stamp_group TREES [KERNEL=2] [ROWS_PER_TREE=200]
 #define GGP_STAMPS
 #include "ggp_engine.hip"
 #include "ggp_host.h"
@@ -15,8 +15,9 @@ int main(int argc, char **argv)
 {
     const int64_t trees = argc > 1 ? atoll(argv[1]) : 1000;
     const int kernel = argc > 2 ? atoi(argv[2]) : GGP_KERNEL_GROUP;
+    const int64_t rows = argc > 3 ? atoll(argv[3]) : 200;   // rows per tree (SURVEY 8(d) shape)
     ggp_host_forest *hf = nullptr;
-    if (ggp_synthetic_forest(trees, 200, 20261015ULL, 0, 1, 1, &hf) != 0) { fprintf(stderr, "synthetic failed\n"); return 1; }
+    if (ggp_synthetic_forest(trees, rows, 20261015ULL, 0, 1, 1, &hf) != 0) { fprintf(stderr, "synthetic failed\n"); return 1; }
     ggp_forest_desc d;
     ggp_host_forest_desc(hf, &d);
     d.kernel = kernel;
