@@ -237,6 +237,10 @@ def main() -> int:
     ap.add_argument("--predict-rows", type=int, default=500, help="rows per tree of the -p forest")
     ap.add_argument("--example-mp", type=int, default=1,
                     help="also time the reference's published workload: the CLI's -m -p on the example (N=1; 0 = skip)")
+    ap.add_argument("--c3-evals", type=int, default=400,
+                    help="also time BASELINE configs[2]: -m on 10k trees x 200 tp, this many evaluations (N=1; 0 = skip)")
+    ap.add_argument("--joints-trees", type=int, default=20,
+                    help="also time -j over every start row of this many C5-shaped trees (N=1; 0 = skip)")
     ap.add_argument("--inprocess", type=int, default=1,
                     help="N > 1: also time the CLI's in-process device-list path (one process, every rank's trees "
                          "sharded over devices 0..N-1, include/ggp.h) on rank 0 while the others wait (0 = skip)")
@@ -478,6 +482,69 @@ def main() -> int:
         else:
             store.wait(["ggp_inprocess_done"])
         barrier()
+    # ---- BASELINE configs[2] (C3): the -m loop on the 10k trees x 200 tp forest, all 11 parameters
+    # free (the example's file with beta = 4.95E-04, 4.95E-05), log space, LN_NELDERMEAD at
+    # tol 1e-10 through optimize.minimize_wrapper (the product's optimiser and objective), bounded
+    # at a fixed evaluation count ----
+    c3 = None
+    if world == 1 and args.c3_evals > 0:
+        from gfp_gaussian_process_amd import optimize as opt
+        P3 = g.ParameterSet.load(os.path.join(ROOT, "tests", "golden", "example_parameter_file.txt"))
+        P3.kind[6], P3.step[6] = "free", 4.95e-05
+        h3 = g.HostForest.synthetic(10000, 200, seed=SEED, first_tree=10 ** 6)
+        f3 = g.Forest(h3, device=local, kernel=args.kernel)
+        calls = [0]
+
+        def obj3(p):
+            calls[0] += 1
+            return f3.total_likelihood(p)
+        obj3(P3.init)                               # warm-up (workspaces), not counted below
+        f3.reset_state()
+        calls[0] = 0
+        barrier()
+        t1 = time.perf_counter()
+        x3, ll3, rc3 = opt.minimize_wrapper(obj3, P3, tolerance=1e-10, search_space="log", maxeval=args.c3_evals)
+        barrier()
+        c3el = time.perf_counter() - t1
+        c3 = {"config": "C3: synthetic 10000 trees x 200 tp, -m log-space Nelder-Mead (minimize_wrapper), "
+                        "11 free parameters, tol 1e-10, bounded at maxeval",
+              "rows": h3.n_rows, "evaluations": calls[0], "seconds": c3el, "ms_per_eval": 1e3 * c3el / calls[0],
+              "evals_per_s": calls[0] / c3el, "updates_per_s": calls[0] * h3.n_rows / c3el,
+              "ll_best": ll3, "nlopt_result": rc3, "levels": f3.info()["levels"],
+              "note": "BASELINE configs[2]; the optimiser's calls are sequential (carried state), each one "
+                      "GPU evaluation with the optimiser's host step between; not the headline value"}
+        f3.close()
+
+    # ---- BASELINE configs[4]'s -j half on C5-shaped trees (the <= 10k-row subset): 20
+    # trees x 500 tp (250 + 125 + 125 rows), ggp_joints over every start row in ranges of 2,048
+    # as the CLI streams them, the joints copied to the host ----
+    jc5 = None
+    if world == 1 and args.joints_trees > 0:
+        hj = g.HostForest.synthetic(args.joints_trees, args.predict_rows, seed=SEED, first_tree=2 * 10 ** 6)
+        fj = g.Forest(hj, device=local)
+        nrj = hj.n_rows
+        fj.joints(P_EXAMPLE, 1e-10, 0, min(nrj, 256), cap=1 << 20)   # warm-up: smoother tables cached
+        barrier()
+        t1 = time.perf_counter()
+        nj, cap, lo = 0, 1 << 21, 0
+        while lo < nrj:
+            hi = min(nrj, lo + 2048)
+            try:
+                idx_j, _ = fj.joints(P_EXAMPLE, 1e-10, lo, hi, cap=cap)
+            except g.GGPError:
+                cap *= 2
+                continue
+            nj += len(idx_j)
+            lo = hi
+        barrier()
+        jel = time.perf_counter() - t1
+        jc5 = {"config": f"-j on {args.joints_trees} C5-shaped trees x {args.predict_rows} tp ({nrj} rows), "
+                         "tol 1e-10, every start row, ranges of 2,048 start rows",
+               "rows": nrj, "joints": nj, "seconds": jel, "joints_per_s": nj / jel, "start_rows_per_s": nrj / jel,
+               "note": "BASELINE configs[4]'s -j leg on its tree shape (SURVEY 8(d) subset); joints computed on "
+                       "the GPU and copied to the host (72 doubles each), parameter tables cached per parameters"}
+        fj.close()
+
     exmp = None
     if world == 1 and args.example_mp:
         exmp = example_mp(os.path.join("/tmp", f"ggp_example_mp_{os.getpid()}"), 3.0 if not args.no_cpu else 0.5)
@@ -530,6 +597,10 @@ def main() -> int:
             result["hessian_batch"] = hess
         if exmp is not None:
             result["example_mp"] = exmp
+        if c3 is not None:
+            result["c3_minimize"] = c3
+        if jc5 is not None:
+            result["joints_c5_subset"] = jc5
         if inproc is not None:
             result["inprocess"] = inproc
         if world == 1 and not args.no_cpu:

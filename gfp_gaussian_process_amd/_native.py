@@ -64,6 +64,7 @@ ENGINE_SYMBOLS = {
     "ggp_total_loglik_tree": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, c_double_p, c_int32_p, c_double_p,
                                              c_int32_p, c_int64_p, c_int64_p]),
     "ggp_keep_point_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "ggp_chain_fallbacks": (ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     "ggp_total_loglik_async": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "ggp_loglik_result": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_int64_p, c_int64_p]),
     "ggp_predict": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, c_double_p,

@@ -747,13 +747,25 @@ GGP_DEV double dpp_f64(const double v)
 // once per block.  A path's first cell, if a second daughter, waits for its parent's done flag
 // (this evaluation's epoch: relaxed agent-scope polls); a cell with a second daughter publishes
 // its state (lanes 0-19, agent-scope stores), waits for the stores (s_waitcnt vmcnt(0)), then
-// its flag.  Paths are ordered by the depth of their first cell, so a parent's path has a lower
-// block index; progress relies on the waiting block and its parent's block being resident
-// together (the path launch holds at most as many blocks as the device keeps resident, sized by
-// the occupancy query), and a wait that exceeds spin_max polls ends as a stall (GGP_ETIMEOUT),
-// never as a hang or a model NaN.  chain[c] = {parent to wait for or -1, 1 if a second daughter
-// waits for c}.
+// its flag.  Paths are ordered by the depth of their first cell, so a waiting block's parent
+// has a lower block index.  What progress relies on:
+//   - the single-call path launch (grid = n_paths <= the blocks the device holds resident, from
+//     the occupancy query at creation): every block is resident at once, so every wait ends;
+//   - chained and tree launches (k_loglik_wave<true>, grid n_paths x points, blockIdx.y = point,
+//     a point's roots waiting for its predecessor point's roots): the grid may exceed residency,
+//     and then progress relies on the dispatcher starting a lower linear block index no later
+//     than a higher one (a waiting block only ever waits on a lower index), which the hardware
+//     does but the programming guide does not promise.  Each chained launch is capped so its
+//     chain of roots stays within kChainRowsPerLaunch rows (ggp_total_loglik_chain), well inside
+//     one wait's budget.
+// A wait that exceeds spin_max polls ends as a stall (GGP_ETIMEOUT), never as a hang or a model
+// NaN; ggp_total_loglik_chain then finishes the remaining points call by call from the last
+// completed point's state, and the -m lookahead evaluates a stalled node's call normally.
+// chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c}.
 constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling (GGP_CHAIN_SPIN_MAX)
+// rows of chained roots one chained launch may hold (~1 us per row: a few seconds, against the
+// ~20 s a wait may take before it counts as a stall)
+constexpr int64_t kChainRowsPerLaunch = int64_t(1) << 22;
 constexpr unsigned kChainQuietPerRow = 1100;    // s_memtime units (~0.5 us) of unpolled sleep per parent row
 
 // In-launch reduction of a path launch (replaces k_reduce_blocks there, with the same sums):
@@ -1097,10 +1109,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         GGP_STAMP(7);
         wave_sync();
     };
+    bool next_pre = false;   // the previous cell's last flush loaded this cell's first chunk
     for (int i = i_lo; i < i_hi; ++i) {
         const int c = cells[i];
         const int2 ch = chain[c];
         bool chain_broken = false;
+        // the path's next cell: its first chunk is loaded during this cell's last flush
+        const int c_nx = i + 1 < i_hi ? cells[i + 1] : -1;
+        const int64_t r0n = c_nx >= 0 ? F.row_off[c_nx] : 0, r1n = c_nx >= 0 ? F.row_off[c_nx + 1] : 0;
         // the cell to wait for: a second daughter's parent; in a chain also a root's own state at
         // the end of the previous point (its carried state)
         int wc = ch.x;
@@ -1132,6 +1148,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 __builtin_amdgcn_s_sleep(8);
             }
         }
+        // a root whose predecessor point's root stalled stalls too (its state would be that
+        // root's unfinished one): the tree's dependent points report GGP_ETIMEOUT, not a value
+        if (CHAIN && carried_prev && !chain_broken &&
+            ld_agent_i(cell_nan + (wdone - cell_done) + F.dfs_rank[c]) == kRowStall)
+            chain_broken = true;
         const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
         double dt = 0.0;
         bool pending;
@@ -1178,7 +1199,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             lds[W::L_ROWT + lane] = t;
             if (lane == 0) lds[W::L_ROWT + 64] = base + 64 < r1 ? F.time[base + 64] : 0.0;
         };
-        if (i != i_lo) load_chunk(r0);   // the first cell's chunk is in LDS since the launch's start
+        // the first cell's chunk is in LDS since the launch's start, a later one's since its
+        // predecessor's last flush (unless that stopped at a NaN)
+        if (i != i_lo && !next_pre) load_chunk(r0);
+        next_pre = false;
         wave_sync();
         double cl = 0.0;
         int nan_row = kNanNone;
@@ -1199,6 +1223,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (slot == 64 || !live) {
                 const int done = nrows - left;
                 const int64_t base = done - slot;
+                // the next chunk (this cell's, or the path's next cell's first) is loaded while the
+                // flush runs, and goes to LDS after the flush has read this chunk's rows
+                const bool nx = live || c_nx >= 0;
+                const int64_t nb0 = live ? r0 + done : r0n, ne = live ? r1 : r1n;
+                double na = 0.0, nf = 0.0, nt = 0.0, nt64 = 0.0;
+                if (nx) {
+                    const int64_t rr = nb0 + lane;
+                    if (rr < ne) {
+                        na = F.logl[rr];
+                        nf = F.fp[rr];
+                        nt = F.time[rr];
+                    }
+                    if (lane == 0 && nb0 + 64 < ne) nt64 = F.time[nb0 + 64];
+                }
                 wave_sync();
                 if (lane < slot) {
                     const double s00 = lds[W::L_RS0 + lane], s01 = lds[W::L_RS1 + lane], s11 = lds[W::L_RS2 + lane];
@@ -1235,8 +1273,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 }
                 if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) return false;
                 slot = 0;
-                if (live) load_chunk(r0 + done);
-                GGP_TL_CNT(3, live);
+                if (nx) {
+                    wave_sync();   // every lane has read this chunk's rows (lane 0's sum: the ll terms only)
+                    lds[W::L_ROWL + lane] = na;
+                    lds[W::L_ROWF + lane] = nf;
+                    lds[W::L_ROWT + lane] = nt;
+                    if (lane == 0) lds[W::L_ROWT + 64] = nt64;
+                }
+                next_pre = !live && c_nx >= 0;
+                GGP_TL_CNT(3, nx);
             }
             GGP_STAMP(10);
             wave_sync();   // the LDS slots are rewritten by the next step
@@ -2428,6 +2473,8 @@ struct ggp_forest {
     std::vector<int64_t> row_off;      // global row_offset
     Comm *comm = nullptr;              // multi-process mode (ggp_comm_attach)
     int32_t tree_pts = 0;              // points of the last ggp_total_loglik_tree (ggp_keep_point_state)
+    int64_t max_root_rows = 1;         // rows of the longest root cell (the chained launch's cap)
+    int64_t chain_fallbacks = 0;       // chained calls finished call by call after a stall
 };
 
 namespace {
@@ -3398,6 +3445,8 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     f->n_cells = nc;
     f->n_rows = nr;
     f->n_trees = (int64_t)tree_start.size() - 1;
+    for (int64_t c = 0; c < nc; ++c)
+        if (d->parent[c] < 0) f->max_root_rows = std::max<int64_t>(f->max_root_rows, d->row_offset[c + 1] - d->row_offset[c]);
     f->dfs_order = dfs;
     f->row_off.assign(d->row_offset ? d->row_offset : nullptr, d->row_offset ? d->row_offset + nc + 1 : nullptr);
     if (nc == 0) f->row_off.assign(1, 0);
@@ -3855,7 +3904,7 @@ static bool chain_fusable(const ggp_forest *f)
     return fused;
 }
 
-static int run_points(ggp_forest *f, int64_t np, const double *params, const int32_t *pred, bool carry_last,
+static int run_points(ggp_forest *f, int64_t np, const double *params, const int32_t *pred,
                       std::vector<std::vector<double>> &sums, std::vector<std::vector<int64_t>> &codes)
 {
     const size_t ns = f->shards.size();
@@ -3881,9 +3930,6 @@ static int run_points(ggp_forest *f, int64_t np, const double *params, const int
                            s->d_gdfs, (int)s->n_lblocks, s->d_b_sum, s->d_b_code, (unsigned *)nullptr,
                            (int64_t *)nullptr, (int64_t)0, (double *)nullptr, (int64_t *)nullptr);
         HIPCHK(hipGetLastError());
-        if (carry_last)   // the carried state: the last point's (every cell, as its sequential call leaves it)
-            HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)(np - 1) * nc * 20, (size_t)nc * 20 * sizeof(double),
-                                  hipMemcpyDeviceToDevice, s->stream));
         sums[k].resize((size_t)np * s->n_lblocks);
         codes[k].resize((size_t)np * s->n_lblocks);
         HIPCHK(hipMemcpyAsync(sums[k].data(), s->d_b_sum, sums[k].size() * sizeof(double), hipMemcpyDeviceToHost,
@@ -3930,6 +3976,20 @@ static int point_result(const ggp_forest *f, const std::vector<std::vector<doubl
 static const char *kStallMsg =
     "evaluation stalled: a cell's wait for the cell it depends on timed out (a scheduling stall, not a NaN)";
 
+// the carried state becomes the state point `point` of the last run_points left (every cell, as
+// its sequential call leaves it); the copies are enqueued on each shard's stream
+static int adopt_point_state(ggp_forest *f, int64_t point)
+{
+    for (Shard *s : f->shards) {
+        if (!s->n_cells) continue;
+        const int64_t nc = s->n_cells;
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipMemcpyAsync(s->d_state, s->d_b_state + (size_t)point * nc * 20, (size_t)nc * 20 * sizeof(double),
+                              hipMemcpyDeviceToDevice, s->stream));
+    }
+    return GGP_OK;
+}
+
 int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *n_ok,
                            int64_t *nan_cell, int64_t *nan_row)
 {
@@ -3951,21 +4011,54 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
         return GGP_OK;
     }
     if (n_pts == 0) return GGP_OK;
-    const int64_t chunk = batch_reserve(f, n_pts);
+    int64_t chunk = batch_reserve(f, n_pts);
     if (chunk <= 0) return (int)-chunk;
+    // a launch's chain of roots (point i's roots wait for point i - 1's) stays within
+    // kChainRowsPerLaunch rows, so no wait in it comes near the stall budget
+    int64_t rows_cap = kChainRowsPerLaunch;
+    if (const char *e = std::getenv("GGP_CHAIN_ROWS_PER_LAUNCH"))   // tests: the cap's chunk boundaries
+        if (std::atoll(e) > 0) rows_cap = std::atoll(e);
+    chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, rows_cap / f->max_root_rows));
     std::vector<std::vector<double>> sums;
     std::vector<std::vector<int64_t>> codes;
     for (int64_t p0 = 0; p0 < n_pts; p0 += chunk) {
         const int64_t np = std::min<int64_t>(chunk, n_pts - p0);
-        const int rc = run_points(f, np, params + 11 * p0, nullptr, true, sums, codes);
+        int rc = run_points(f, np, params + 11 * p0, nullptr, sums, codes);
         if (rc != GGP_OK) return rc;
-        for (int64_t i = 0; i < np; ++i) {
-            const int r = point_result(f, sums, codes, i, ll + p0 + i, nan_cell, nan_row);
-            if (r == GGP_ETIMEOUT) g_last_err = kStallMsg;
-            if (r != GGP_OK) return r;
+        int64_t i = 0;
+        int r = GGP_OK;
+        for (; i < np; ++i) {
+            r = point_result(f, sums, codes, i, ll + p0 + i, nan_cell, nan_row);
+            if (r != GGP_OK) break;
             *n_ok = (int32_t)(p0 + i + 1);
         }
+        if (r == GGP_OK || r == GGP_ENAN) {   // after a NaN the carried state is unspecified (as one by one)
+            if ((rc = adopt_point_state(f, r == GGP_OK ? np - 1 : i)) != GGP_OK) return rc;
+            if (r != GGP_OK) return r;
+            continue;
+        }
+        // a stall (GGP_ETIMEOUT) is the chained schedule's, not the calls': the carried state
+        // becomes the last completed point's (or stays the one before this launch), and the
+        // remaining points run one by one -- the same calls, so the same values
+        if (i > 0 && (rc = adopt_point_state(f, i - 1)) != GGP_OK) return rc;
+        ++f->chain_fallbacks;
+        for (int64_t q = p0 + i; q < n_pts; ++q) {
+            const int rq = ggp_total_loglik(f, params + (size_t)11 * q, ll + q, nan_cell, nan_row);
+            if (rq != GGP_OK) return rq;
+            *n_ok = (int32_t)(q + 1);
+        }
+        return GGP_OK;
     }
+    return GGP_OK;
+}
+
+int ggp_chain_fallbacks(const ggp_forest *f, int64_t *n)
+{
+    if (!f || !n) {
+        g_last_err = "ggp_chain_fallbacks: bad arguments";
+        return GGP_EINVAL;
+    }
+    *n = f->chain_fallbacks;
     return GGP_OK;
 }
 
@@ -4009,7 +4102,7 @@ int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, co
     }
     std::vector<std::vector<double>> sums;
     std::vector<std::vector<int64_t>> codes;
-    const int rc = run_points(f, n_pts, params, pred, false, sums, codes);
+    const int rc = run_points(f, n_pts, params, pred, sums, codes);
     if (rc != GGP_OK) return rc;
     for (int32_t i = 0; i < n_pts; ++i)
         status[i] = point_result(f, sums, codes, i, ll + i, nan_cell ? nan_cell + i : nullptr, nan_row ? nan_row + i : nullptr);

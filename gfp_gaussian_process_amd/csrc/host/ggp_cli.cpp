@@ -335,7 +335,10 @@ double total_likelihood(const std::vector<double> &params, Objective &o)
 {
     Objective::Ahead &a = o.ahead;
     if (a.active) {
-        const int k = ahead_node(o, params.data());
+        int k = ahead_node(o, params.data());
+        // a node whose speculative launch stalled (GGP_ETIMEOUT: the lookahead's schedule, not the
+        // call) is not served: the call runs below from the carried state, the last node served
+        if (k >= 0 && a.st[(size_t)k] == GGP_ETIMEOUT) k = -1;
         if (k >= 0) {   // evaluated ahead: its state becomes the carried state, its value the call's
             a.cur = k;
             const int rc = ggp_keep_point_state(o.forest, k);

@@ -552,6 +552,13 @@ class Forest:
         self._check(rc)
         return ll, st, nc, nr
 
+    def chain_fallbacks(self) -> int:
+        """chained calls (total_likelihood_chain) of this handle that finished one by one after a
+        stall of the chained schedule (ggp_chain_fallbacks)"""
+        n = ctypes.c_int64()
+        self._check(self._lib.ggp_chain_fallbacks(self._h, ctypes.byref(n)))
+        return n.value
+
     def keep_point_state(self, point: int) -> None:
         """make the state point `point` of the last total_likelihood_tree left the carried state"""
         self._check(self._lib.ggp_keep_point_state(self._h, int(point)))

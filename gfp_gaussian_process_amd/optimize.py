@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 from . import _native as N
-from .forest import ParameterSet
+from .forest import Forest, ParameterSet
 
 # nlopt_result
 FAILURE, INVALID_ARGS, FORCED_STOP = -1, -2, -5
@@ -121,6 +121,10 @@ class _Ahead:
 
     def call(self, params) -> float:
         k = self.node(params)
+        # a node whose speculative launch stalled (GGP_ETIMEOUT: the lookahead's schedule, not the
+        # call) is not served: the call runs as usual from the carried state, the last node served
+        if k >= 0 and int(self.res[1][k]) == N.GGP_ETIMEOUT:
+            k = -1
         if k < 0:
             self.active = False
             return self.f.total_likelihood(params)
@@ -171,12 +175,13 @@ def minimize_wrapper(objective, params: ParameterSet, tolerance: float = 1e-10, 
 
 def _chain_forest(objective):
     """the Forest behind an objective that is a Forest or its bound total_likelihood (whose
-    known call sequences can run as one ggp_total_loglik_chain call), else None"""
-    if hasattr(objective, "total_likelihood_chain"):
-        return objective
+    known call sequences can run as one ggp_total_loglik_chain call), else None.  Only the
+    Forest's own total_likelihood qualifies: a subclass that overrides it (a prior, a logging
+    wrapper) is called one call at a time, so every call goes through the override."""
+    if isinstance(objective, Forest):
+        return objective if type(objective).total_likelihood is Forest.total_likelihood else None
     owner = getattr(objective, "__self__", None)
-    if owner is not None and hasattr(owner, "total_likelihood_chain") and \
-            getattr(objective, "__name__", "") == "total_likelihood":
+    if isinstance(owner, Forest) and getattr(objective, "__func__", None) is Forest.total_likelihood:
         return owner
     return None
 

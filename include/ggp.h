@@ -154,9 +154,15 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
  * GGP_OK with *n_ok = n_pts.  Only a root's state crosses from one evaluation to the next
  * (predictions.h:63-82), so on a path-launch handle (every level on the wave schedule) the points
  * run in one launch per chunk, point i's root waiting for point i-1's and its trees overlapping
- * with the later points'; other handles run the calls one by one (GGP_CHAIN_FUSED=0: always). */
+ * with the later points'; other handles run the calls one by one (GGP_CHAIN_FUSED=0: always).
+ * A chunk holds at most 2^22 rows of chained roots.  A wait of the chained schedule that times
+ * out is not the calls' failure: the carried state becomes the last completed point's and the
+ * remaining points run one by one (the same values; ggp_chain_fallbacks counts such chains), so
+ * GGP_ETIMEOUT comes back only when a one-by-one call stalls too. */
 int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, double *ll,
                            int32_t *n_ok, int64_t *nan_cell, int64_t *nan_row);
+/* chained calls of this handle that finished one by one after a stall of the chained schedule */
+int ggp_chain_fallbacks(const ggp_forest *f, int64_t *n);
 
 /* Speculative evaluation (the -m optimiser's lookahead): n_pts points in one launch,
  * point i's roots starting from the state point pred[i] left (pred[i] in [-1, i); -1 = the

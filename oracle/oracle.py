@@ -146,11 +146,16 @@ class OracleForest:
     def joints(self, params_per_segment, tol=1e-10, r_lo=0, r_hi=None, cap=1 << 20):
         """-j for start rows [r_lo, r_hi): (idx [k, 2] = (start, target), val [k, 72])"""
         p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
-        fwd, bwd, _ = self.predict(p)
+        key = p.tobytes()
+        if getattr(self, "_joint_smooth_key", None) != key:   # the smoother once per parameters
+            fwd, bwd, _ = self.predict(p)
+            self._joint_smooth = (fwd, bwd, self.after_predict.copy())
+            self._joint_smooth_key = key
+        fwd, bwd, after = self._joint_smooth
         r_hi = self.f.n_rows if r_hi is None else r_hi
         idx = np.zeros((cap, 2), np.int64)
         val = np.zeros((cap, 72))
-        n = self._L().ora_joints(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(fwd), _dp(bwd), _dp(self.after_predict),
+        n = self._L().ora_joints(ctypes.byref(self.f), _dp(p), p.shape[0], _dp(fwd), _dp(bwd), _dp(after),
                              tol, r_lo, r_hi, cap, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _dp(val))
         if n > cap:
             raise ValueError(f"{n} joints > cap {cap}")

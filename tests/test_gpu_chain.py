@@ -240,3 +240,123 @@ def test_tree_points_bitwise_their_call_sequences(devices):
     for i in (6, 3, 0):
         f.keep_point_state(i)
         assert np.array_equal(f.state(), after[i]), i
+
+
+# ---- stalls of the chained and speculative schedules (include/ggp.h ggp_total_loglik_chain) ----
+# GGP_CHAIN_SPIN_MAX=0 (read when a handle is created) makes every wait that finds its cell not
+# done time out at once: a point's roots waiting for the previous point's, a second daughter for
+# its parent.  A forest of roots only has no wait inside a point, so its one-by-one calls never
+# stall there while its chained and tree launches do.
+
+def _roots_only(hf):
+    import gfp_gaussian_process_amd as g
+    a = hf.a
+    ro = a["row_offset"]
+    roots = np.nonzero(a["parent"] == -1)[0]
+    rows = np.concatenate([np.arange(ro[c], ro[c + 1]) for c in roots])
+    b = dict(a)
+    b["row_offset"] = np.concatenate([[0], np.cumsum(ro[roots + 1] - ro[roots])]).astype(np.int64)
+    for k in ("parent", "daughter1", "daughter2"):
+        b[k] = np.full(len(roots), -1, np.int32)
+    for k in ("segment", "time", "log_length", "fp"):
+        b[k] = np.ascontiguousarray(a[k][rows])
+    return g.HostForest(b)
+
+
+def _stalling(hf, monkeypatch, **kw):
+    import gfp_gaussian_process_amd as g
+    monkeypatch.setenv("GGP_CHAIN_SPIN_MAX", "0")
+    f = g.Forest(hf, kernel="wave", **kw)
+    monkeypatch.delenv("GGP_CHAIN_SPIN_MAX")
+    return f
+
+
+def test_chain_stall_finishes_call_by_call(monkeypatch):
+    """a chained launch whose waits time out (point 1's roots find point 0's still running) is
+    the schedule's failure, not the calls': the chain adopts the last completed point's state and
+    runs the rest one by one -- values and carried state bitwise the sequential calls', no
+    EvaluationStalled, one fallback counted"""
+    import gfp_gaussian_process_amd as g
+    hf = _roots_only(g.HostForest.synthetic(48, 400))   # 48 roots of 200 rows: point 0 is still running
+    pts = _points(12)
+    want, st_want = _sequential(hf, pts, kernel="wave")
+    f = _stalling(hf, monkeypatch)
+    f.total_likelihood(P0)
+    got = f.total_likelihood_chain(pts)
+    assert np.array_equal(got, want)
+    assert np.array_equal(f.state(), st_want)
+    assert f.chain_fallbacks() == 1
+    more = _points(3, seed=9)   # the handle goes on like one that made the calls itself
+    w2 = g.Forest(hf, kernel="wave")
+    w2.set_state(st_want)
+    assert np.array_equal(f.total_likelihood_chain(more), np.array([w2.total_likelihood(p) for p in more]))
+
+
+def test_chain_stall_raises_when_the_calls_stall_too(monkeypatch):
+    """with second daughters the one-by-one calls wait too: the chain ends as EvaluationStalled
+    (GGP_ETIMEOUT), never LikelihoodIsNan, at point 0 with no values"""
+    import ctypes
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import _native as N
+    f = _stalling(g.HostForest.synthetic(64, 200), monkeypatch)
+    with pytest.raises(g.EvaluationStalled) as ei:
+        f.total_likelihood_chain(_points(5))
+    assert not isinstance(ei.value, g.LikelihoodIsNan)
+    assert ei.value.point == 0 and ei.value.ll.size == 0
+    f2 = _stalling(g.HostForest.synthetic(64, 200), monkeypatch)
+    pts = np.ascontiguousarray(_points(5), np.float64)
+    ll = np.zeros(5)
+    n_ok, nc, nr = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+    rc = N.engine().ggp_total_loglik_chain(f2._h, 5, pts.ctypes.data_as(N.c_double_p), ll.ctypes.data_as(N.c_double_p),
+                                           ctypes.byref(n_ok), ctypes.byref(nc), ctypes.byref(nr))
+    assert rc == N.GGP_ETIMEOUT and n_ok.value == 0 and nr.value == -1
+
+
+def test_tree_stall_statuses(monkeypatch):
+    """ggp_total_loglik_tree under stalls: points from the carried state (pred -1) complete,
+    bitwise the one-by-one call; points that wait on another point report GGP_ETIMEOUT, never
+    GGP_ENAN"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import _native as N
+    hf = _roots_only(g.HostForest.synthetic(48, 400))
+    pts = _points(6, seed=3)
+    pred = np.array([-1, 0, 0, 1, -1, 4], np.int32)
+    f = _stalling(hf, monkeypatch)
+    f.total_likelihood(P0)
+    ll, st, nc, nr = f.total_likelihood_tree(pts, pred)
+    assert st[0] == N.GGP_OK and st[4] == N.GGP_OK
+    assert all(int(v) in (N.GGP_OK, N.GGP_ETIMEOUT) for v in st)
+    assert st[1] == N.GGP_ETIMEOUT and st[5] == N.GGP_ETIMEOUT
+    ref = g.Forest(hf, kernel="wave")
+    ref.total_likelihood(P0)
+    st0 = ref.state()
+    assert ll[0] == ref.total_likelihood(pts[0])
+    ref.set_state(st0)
+    assert ll[4] == ref.total_likelihood(pts[4])
+
+
+def test_minimize_lookahead_with_stalls_matches_call_by_call(monkeypatch):
+    """-m's lookahead on a handle whose speculative launches stall: a stalled node is not served,
+    its call runs as usual from the last served node's state -- the optimiser's result and the
+    carried state are those of the call-by-call run"""
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import optimize as opt
+    hf = _roots_only(g.HostForest.synthetic(16, 80))
+    P = g.ParameterSet.load(os.path.join(GOLDEN, "example_parameter_file.txt"))
+    a = _stalling(hf, monkeypatch)
+    xa, lla, rca = opt.minimize_wrapper(a.total_likelihood, P, tolerance=1e-6, maxeval=120)
+    monkeypatch.setenv("GGP_NM_LOOKAHEAD", "0")
+    b = g.Forest(hf, kernel="wave")
+    xb, llb, rcb = opt.minimize_wrapper(b.total_likelihood, P, tolerance=1e-6, maxeval=120)
+    assert rca == rcb and lla == llb and np.array_equal(xa, xb)
+    assert np.array_equal(a.state(), b.state())
+
+
+def test_chain_rows_cap_chunks_bitwise(monkeypatch, example):
+    """the cap on chained root rows per launch (2^22; here 1000 rows: four of the example's
+    243-row root per launch) splits a chain into launches with the same values and state"""
+    pts = _points(11, seed=8)
+    want, st_want = _sequential(example, pts)
+    monkeypatch.setenv("GGP_CHAIN_ROWS_PER_LAUNCH", "1000")
+    got, st_got, _ = _chained(example, pts)
+    assert np.array_equal(got, want) and np.array_equal(st_got, st_want)

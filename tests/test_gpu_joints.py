@@ -226,3 +226,66 @@ def test_joints_example_full_size(example_paths):
     print(f"example full: {len(sample)} sampled start rows, {n} pairs compared, max err {err:.2e}, "
           f"median {med:.2e}, worst event {worst:.1f} tol")
     assert med < 1e-6, med
+
+
+def test_joints_c5_shape_subset_cli_and_oracle(tmp_path):
+    """BASELINE configs[4]'s -j leg on its own tree shape, the <= 10k-row subset SURVEY 8(d)
+    prescribes: 20 C5-shaped trees x 500 tp (root 250 + daughters 125 + 125 rows, 10k rows;
+    collect_joint_distributions walks the deeper subtrees of correlation_tree.h:588-648 here).
+      * the CLI's -js over every start row of the forest (the reference's CSV surface, written by
+        ggp_dataset_write_csv), whose line count is the engine's joint count over all start rows;
+      * the first and last start row of every cell (120 walks, divisions included) against the
+        oracle with test_joints_synthetic_vs_oracle's bar (threshold events at MARGIN x tol,
+        values at 1e-6 of the oracle's standard deviations);
+      * those start rows' lines in the file are the engine's joints formatted as the reference
+        prints them (ostream <<, 6 significant digits)."""
+    import glob
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    from test_gpu_cli import _param_file, _run
+    hs = g.HostForest.synthetic(20, 500, with_ids=True)
+    csv, cfg = str(tmp_path / "c5sub.csv"), str(tmp_path / "c5sub_config.txt")
+    g.Dataset.from_forest(hs).write_csv(csv, cfg)
+    pf = _param_file(tmp_path / "p.txt", {})
+    _run(["-i", csv, "-b", pf, "-c", cfg, "-js", "-o", str(tmp_path / "o")], tmp_path)
+    sp = glob.glob(str(tmp_path / "o" / "*_joints_sparse.csv"))
+    assert len(sp) == 1
+    hf = g.HostForest.from_csv(csv, cfg, -1, "scaled", "binomial")   # the forest the CLI read
+    nr, ro = hf.n_rows, hf.a["row_offset"]
+    assert nr == 10000 and hf.n_cells == 60
+    fg, of = g.Forest(hf), O.OracleForest(hf.a)
+    total = 0
+    for lo in range(0, nr, 2048):
+        ig, _ = fg.joints(P, 1e-10, lo, min(nr, lo + 2048), cap=1 << 21)
+        total += len(ig)
+    sample = sorted({int(ro[c]) for c in range(hf.n_cells)} | {int(ro[c + 1]) - 1 for c in range(hf.n_cells)})
+    G = [fg.joints(P, 1e-10, s, s + 1, cap=1 << 16) for s in sample]
+    Ov = [of.joints(P, 1e-10, s, s + 1, cap=1 << 16) for s in sample]
+
+    def cat(parts):
+        return np.concatenate([q[0] for q in parts]), np.concatenate([q[1] for q in parts])
+    (ig, vg), (io, vo) = cat(G), cat(Ov)
+    err, med, n, worst = _compare(ig, vg, io, vo)
+    print(f"C5-shaped subset: {total} joints over {nr} start rows; {len(sample)} sampled walks, {n} pairs "
+          f"compared, max err {err:.2e}, median {med:.2e}, worst event {worst:.2f} tol")
+    assert err < 1e-6, err
+    # the file: one line per joint (unique (cell_id, time) per row), and the sampled start rows'
+    # lines are the engine's values printed as the reference prints them
+    want = {}
+    for s, (a, v) in zip(sample, G):
+        want[s] = [f"{s},{t}," + ",".join("%g" % x for x in list(vv[:8]) +
+                                          [vv[8 + 8 * i + j] for i in range(8) for j in range(i, 8)])
+                   for (_, t), vv in zip(a.tolist(), v)]
+    got, lines, body = {s: [] for s in sample}, 0, False
+    with open(sp[0]) as fh:
+        for line in fh:
+            if body:
+                lines += 1
+                s = int(line[:line.index(",")])
+                if s in got:
+                    got[s].append(line.rstrip("\n"))
+            elif line.startswith("start_row,column,"):
+                body = True
+    assert lines == total, (lines, total)
+    for s in sample:
+        assert got[s] == want[s], (s, got[s][:2], want[s][:2])

@@ -626,15 +626,18 @@ P = PARAMS
 hf = g.HostForest.synthetic(1000, 200)
 same, nan_ok, t, mode = True, True, {}, {}
 b = g.Forest(hf)
+keep = []   # comm-attached handles kept to the teardown below (the loop destroys the rest as it goes)
 for name, ec in (("engine", True), ("torch", False)):   # RCCL inside the engine; torch's all_gather
     a = g.Forest(hf)
     obj = ShardedObjective(a, always_gather=True, engine_comm=ec)
+    if ec: keep.append(a)
     mode[name] = obj.engine
     b.reset_state()
     same = same and all(obj.total_likelihood(P) == b.total_likelihood(P) for _ in range(3))
     for _ in range(5):   # fresh objectives: their first collective is ordered after the engine
         a2, b2 = g.Forest(hf), g.Forest(hf)
         same = same and ShardedObjective(a2, always_gather=True, engine_comm=ec).total_likelihood(P) == b2.total_likelihood(P)
+        if ec and len(keep) < 3: keep.append(a2)
     bad = list(P); bad[2] = -1.0
     try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
         ShardedObjective(g.Forest(hf), always_gather=True, engine_comm=ec).total_likelihood(bad); nan_ok = False
@@ -645,17 +648,31 @@ for name, ec in (("engine", True), ("torch", False)):   # RCCL inside the engine
         t0 = time.perf_counter()
         for _ in range(200): fn(P)
         t[nm] = 1e3 * (time.perf_counter() - t0) / 200
-dist.destroy_process_group()
-print(json.dumps({"same": same, "nan_ok": nan_ok, "ms": t, "engine_mode": mode}))
+# teardown of comm-attached handles in a defined order (ORDER): each engine communicator is
+# destroyed by its handle (ggp_forest_destroy: the shard's stream synchronised, ncclCommDestroy,
+# then the streams), before or after torch's process group
+attached = [o for o in keep if getattr(o, "_comm_rank", None) is not None]
+if ORDER == "close_first":
+    for o in attached: o.close()
+    dist.destroy_process_group()
+elif ORDER == "group_first":
+    dist.destroy_process_group()
+    for o in attached: o.close()
+else:   # "exit": the group destroyed, the handles left to the interpreter's teardown
+    dist.destroy_process_group()
+print(json.dumps({"same": same, "nan_ok": nan_ok, "ms": t, "engine_mode": mode, "attached": len(attached)}), flush=True)
 '''
 
 
-def test_sharded_objective_collective_path_on_rccl():
+@pytest.mark.parametrize("order", ["close_first", "group_first", "exit"])
+def test_sharded_objective_collective_path_on_rccl(order):
     """ShardedObjective's two RCCL paths on a 1-rank nccl group in a child process -- the
     engine's own (ggp_comm_attach: partial, all-gather and rank-order sum on the engine's stream)
     and torch's (pinned staging, all_gather_into_tensor, combine_partials): bitwise the direct
     objective over a carried-state chain, NaN raised with this rank's cell; prints the per-call
-    cost of each"""
+    cost of each.  Then every comm-attached handle is destroyed explicitly before torch's process
+    group, after it, or left to the interpreter's exit: the child exits 0 in every order (DESIGN
+    §5: the round-3 SIGSEGV came from torch using an engine stream its owner had destroyed)."""
     import socket
     import subprocess
     import sys
@@ -664,13 +681,13 @@ def test_sharded_objective_collective_path_on_rccl():
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    code = f"ROOT={ROOT!r}\nPARAMS={list(CONFIGS[0][2])!r}\n" + _GATHER_CHILD
+    code = f"ROOT={ROOT!r}\nPARAMS={list(CONFIGS[0][2])!r}\nORDER={order!r}\n" + _GATHER_CHILD
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     out = json.loads(r.stdout.strip().splitlines()[-1])
     print("collective path ms/call:", out["ms"])
     assert out["engine_mode"] == {"engine": True, "torch": False}
-    assert out["same"] and out["nan_ok"]
+    assert out["same"] and out["nan_ok"] and out["attached"] >= 1
 
 
 def test_chain_stall_is_a_timeout_not_a_nan(monkeypatch):

@@ -194,3 +194,24 @@ def test_lookahead_serves_the_same_calls(tmp_path, n, fixed):
     calls, served, launches, max_nodes = map(int, out[1:])
     assert calls > 50 and served == calls - 1, out
     assert launches * 2 < calls and max_nodes <= 40, out
+
+
+def test_chain_dispatch_only_for_the_forest_objective():
+    """num_hessian / bound_1dscan / minimize_wrapper take the chained and lookahead engine calls
+    only for a Forest or its own bound total_likelihood; a subclass overriding total_likelihood
+    (a prior, a logging wrapper) or any other callable is called one call at a time"""
+    from gfp_gaussian_process_amd import Forest
+    from gfp_gaussian_process_amd.optimize import _chain_forest
+
+    class WithPrior(Forest):
+        def total_likelihood(self, params):
+            return super().total_likelihood(params) - 1.0
+
+    f = Forest.__new__(Forest)       # no device handle: only the dispatch is under test
+    w = WithPrior.__new__(WithPrior)
+    assert _chain_forest(f) is f
+    assert _chain_forest(f.total_likelihood) is f
+    assert _chain_forest(w) is None
+    assert _chain_forest(w.total_likelihood) is None
+    assert _chain_forest(lambda p: f.total_likelihood(p)) is None
+    assert _chain_forest(f.state) is None
