@@ -153,8 +153,34 @@ def _load(name: str, table: dict):
     return lib
 
 
+def _one_hip_runtime() -> None:
+    """One HIP runtime per process.  libggp.so needs libamdhip64.so.7; PyTorch-ROCm ships its own
+    copy (same SONAME, another file) and its libraries ask for it by another name, so when the
+    engine loads first the process would map two HIP runtimes, and torch's then sees no GPU
+    (measured: "No HIP GPUs are available", tools/two_runtimes.py).  When torch is installed, its
+    runtime is mapped first (RTLD_GLOBAL, without importing torch): the engine binds to it by
+    SONAME and a later `import torch` finds the same file already loaded.  GGP_HIP_RUNTIME=rocm
+    keeps /opt/rocm's (for processes that never import torch)."""
+    if os.environ.get("GGP_HIP_RUNTIME", "") == "rocm":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        hip = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def engine():
     """libggp.so (HIP, gfx950)."""
+    if "libggp.so" not in _cache:
+        _one_hip_runtime()
     return _load("libggp.so", ENGINE_SYMBOLS)
 
 
