@@ -215,3 +215,20 @@ def test_chain_dispatch_only_for_the_forest_objective():
     assert _chain_forest(w.total_likelihood) is None
     assert _chain_forest(lambda p: f.total_likelihood(p)) is None
     assert _chain_forest(f.state) is None
+
+
+@pytest.mark.parametrize("name", ["fixed_dimension", "bound_pinned", "rugged_shrinks"])
+def test_nelder_mead_call_sequences_are_pinned(name):
+    """every objective call of three recorded runs of the restatement (a fixed dimension, a bound
+    the optimum lies on, a rugged function whose simplex shrinks 3 times), bit for bit, and each
+    run's result: tests/golden/make_nm_sequences.py froze the machine the GPU CLI's -m trajectory
+    is checked against, so an edit of the machine or its lookahead cannot move it unnoticed"""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_nm_sequences as M
+    want = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "nm_call_sequences.json")))[name]
+    got = M.run(name)
+    assert len(got["calls"]) == len(want["calls"])
+    assert got["calls"] == want["calls"]
+    assert (got["x"], got["minf"], got["rc"], got["nevals"]) == (want["x"], want["minf"], want["rc"], want["nevals"])
