@@ -227,10 +227,9 @@ constexpr int kOSlots = 10;
 constexpr int kParts[2][4] = {{1 | 2, 4 | 8, 0, 0}, {1, 2, 4, 8}};
 
 template <int OFF, size_t... J>
-GGP_DEV void exps(const ggp::Step &S, double *X, std::index_sequence<J...>)
+GGP_DEV void exps(const ggp::Step &S, double *X, std::index_sequence<J...> seq)
 {
-    ((X[OFF + J] = ggp::exp_body(S, ggp::XTask{ggp::kXT[OFF + J].kind, ggp::kXT[OFF + J].iB, ggp::kXT[OFF + J].ic,
-                                               ggp::kXT[OFF + J].it})), ...);
+    ggp::lane_exps_flagged<OFF>(S, X, seq);   // the lane schedule's exponentials (ggp_prop.h), tasks OFF + J
 }
 template <int OFF, size_t... J>
 GGP_DEV void dawsons(const ggp::Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
@@ -4044,6 +4043,7 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
         ++f->chain_fallbacks;
         for (int64_t q = p0 + i; q < n_pts; ++q) {
             const int rq = ggp_total_loglik(f, params + (size_t)11 * q, ll + q, nan_cell, nan_row);
+            if (rq == GGP_ETIMEOUT) g_last_err = kStallMsg;
             if (rq != GGP_OK) return rq;
             *n_ok = (int32_t)(q + 1);
         }

@@ -68,6 +68,31 @@ GGP_DEV double exp_ocml(const double x)
 
 constexpr double kExpFastMax = 0x1p50;   // exp_ocml is ocml's exp for |x| below this
 
+// exp(x) for the lane schedules: exp_ocml's sequence with the compiler's own operand choice (SGPR
+// coefficients, no inline asm) and without ocml's per-call range checks (two compares and four
+// selects); the check becomes one compare folded into the lane's flag `big`.  A lane whose flag is
+// set recomputes its exponentials with ocml's exp (lane_exps' cold path), so every value is ocml's
+// bitwise: exp_ocml's for |x| < kExpFastMax, ocml's own beyond
+GGP_DEV double exp_lane(const double x, bool &big)
+{
+    big = big | !(__builtin_fabs(x) < kExpFastMax);
+    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
+    double t = __builtin_fma(-dn, 0x1.62e42fefa39efp-1, x);
+    t = __builtin_fma(-dn, 0x1.abc9e3b39803fp-56, t);
+    double p = __builtin_fma(t, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+    p = __builtin_fma(t, p, 0x1.71dee623fde64p-19);
+    p = __builtin_fma(t, p, 0x1.a01997c89e6b0p-16);
+    p = __builtin_fma(t, p, 0x1.a01a014761f6ep-13);
+    p = __builtin_fma(t, p, 0x1.6c16c1852b7b0p-10);
+    p = __builtin_fma(t, p, 0x1.1111111122322p-7);
+    p = __builtin_fma(t, p, 0x1.55555555502a1p-5);
+    p = __builtin_fma(t, p, 0x1.5555555555511p-3);
+    p = __builtin_fma(t, p, 0x1.000000000000bp-1);
+    p = __builtin_fma(t, p, 1.0);
+    p = __builtin_fma(t, p, 1.0);
+    return __builtin_ldexp(p, (int)dn);
+}
+
 // 1/d for finite nonzero d as v_rcp_f64 and two Newton steps (5 instructions against the ~11 of
 // the IEEE sequence).  Used where the value only seeds rdiv, whose residual correction makes
 // the quotient independent of an ulp in the seed.  d = 0 or inf gives NaN (IEEE: inf, 0);
@@ -712,6 +737,18 @@ template <size_t... J>
 GGP_DEV void lane_exps(const Step &S, double *X, std::index_sequence<J...>)
 {
     ((X[J] = exp_body(S, XTask{kXT[J].kind, kXT[J].iB, kXT[J].ic, kXT[J].it})), ...);
+}
+// the same values with exp_lane (one compare per exponential instead of ocml's checks): faster
+// where registers allow (the lane-pair schedule's share of the tasks: C4 shard 0.81 -> 0.79 ms),
+// slower in the one-wave lane and smoother kernels, which keep lane_exps (tools/lane_ab.py)
+template <size_t OFF, size_t... J>
+GGP_DEV void lane_exps_flagged(const Step &S, double *X, std::index_sequence<J...>)
+{
+    bool big = false;
+    ((X[OFF + J] = exp_lane(exp_arg_body(S, XTask{kXT[OFF + J].kind, kXT[OFF + J].iB, kXT[OFF + J].ic, kXT[OFF + J].it}),
+                            big)), ...);
+    if (big)   // an argument beyond kExpFastMax (inf / NaN states): ocml's exp for this lane's set
+        ((X[OFF + J] = exp_body(S, XTask{kXT[OFF + J].kind, kXT[OFF + J].iB, kXT[OFF + J].ic, kXT[OFF + J].it})), ...);
 }
 template <size_t... J>
 GGP_DEV void lane_dawsons(const Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
