@@ -64,12 +64,22 @@ def main():
     res["ll_ms"] = 1e3 * min(times)
     res["ll_updates_per_s"] = n / min(times)
     log(f"total log-likelihood {ll!r}: {res['ll_ms']:.1f} ms ({res['ll_updates_per_s']:.3g} updates/s)")
+    # the split an 8-GPU run uses: each chunk is one GPU's whole-tree shard (LPT over reduction
+    # blocks); per chunk its rows, cells and the device time of its launches in one evaluation
+    res["shard_split"] = [{"device": d, "rows": r, "cells": c} for d, r, c in f.shards()]
+    f.enable_profile()
+    f.reset_state()
+    f.total_likelihood(P)
+    ms, lrows, kern = f.launch_profile()
+    res["ll_launches"] = [{"ms": a, "rows": b, "kernel": k} for a, b, k in zip(ms, lrows, kern)]
+    res["ll_device_ms_sum"] = float(sum(ms))
 
     times = []
     for _ in range(3):
         t0 = time.perf_counter()
         f.predict(P, outputs=(False, False, False))
         times.append(time.perf_counter() - t0)
+    res["predict_device_ms"] = dict(zip(("smooth", "combine"), f.predict_profile()))
     res["predict_ms"] = 1e3 * min(times)
     res["predict_rows_per_s"] = n / min(times)
     log(f"-p: {res['predict_ms']:.1f} ms ({res['predict_rows_per_s']:.3g} rows/s)")
