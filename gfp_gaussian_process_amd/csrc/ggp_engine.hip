@@ -1786,10 +1786,14 @@ __global__ __launch_bounds__(256) void k_combine(const double *__restrict__ ptab
     for (int k = 0; k < 4; ++k) { m[k] = f[k]; mb[k] = b[k]; }
 #pragma unroll
     for (int k = 0; k < 16; ++k) { C[k] = f[4 + k]; Cb[k] = b[4 + k]; }
-    ggp::mult_gauss<FAST>(m, C, mb, Cb);
     int s = prior_seg[r];
     if (s < 0 || s >= n_seg) s = 0;
-    ggp::divide_prior<FAST>(m, C, ptab + 11 * s);
+    if constexpr (FAST) {
+        ggp::combine_info(m, C, mb, Cb, ptab + 11 * s);
+    } else {   // the oracle's operations (GGP_COMBINE_EXACT=1): multiply_gaussian, then divide_by_prior
+        ggp::mult_gauss<false>(m, C, mb, Cb);
+        ggp::divide_prior<false>(m, C, ptab + 11 * s);
+    }
     store20(out + (size_t)20 * r, m, C);
 }
 

@@ -29,10 +29,12 @@ for kern in ("auto", "lane"):
 hp = g.HostForest.synthetic(20000, 500)
 fp = g.Forest(hp)
 fp.predict(P, outputs=(False, False, False))
-sm = 0.0
+sm = cb = 0.0
 for _ in range(5):
     fp.predict(P, outputs=(False, False, False))
-    sm += fp.predict_profile()[0]
+    a_, b_ = fp.predict_profile()
+    sm += a_
+    cb += b_
 rows = fp.predict_rows(0, hp.n_rows)
-out.append(f"smooth {sm / 5:.4f} ms sha={hashlib.sha256(rows.tobytes()).hexdigest()[:16]}")
+out.append(f"smooth {sm / 5:.4f} ms combine {cb / 5:.4f} ms sha={hashlib.sha256(rows.tobytes()).hexdigest()[:16]}")
 print(" | ".join(out), flush=True)
