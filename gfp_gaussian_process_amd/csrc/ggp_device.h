@@ -32,6 +32,18 @@ using std::min;
 #define GGP_DEV __device__ __forceinline__
 #endif
 
+// GGP_CONTRACT, first statement of a lane-schedule body: FMA contraction within each source
+// expression of that body (clang's "on": a*b + c of one expression becomes one fma; nothing is
+// fused across statements).  What fuses is decided by the expression alone, so the lane, group,
+// lane-pair, batch and smoother kernels, which all run these bodies, stay bitwise equal to one
+// another.  The wave schedule (ggp_wave.h) and the oracle keep their own forms.  -DGGP_NO_CONTRACT
+// builds the uncontracted bodies (A/B, DESIGN.md "Parity").
+#if defined(GGP_HOST_SIM) || defined(GGP_NO_CONTRACT)
+#define GGP_CONTRACT
+#else
+#define GGP_CONTRACT _Pragma("clang fp contract(on)")
+#endif
+
 // ------------------------------------------------------------------------------------------
 // Dawson: w_im on y = 1/(1+|x|) with 97 polynomial pieces (degree 6..8, zero-padded to 9),
 // Taylor for y100 >= 97, continued fraction for |x| > 45.
@@ -58,6 +70,7 @@ GGP_DEV double ggp_div_ge1(const double x, const double d)
 
 GGP_DEV double ggp_w_im_abs(double ax, const double *tab)
 {
+    GGP_CONTRACT
     const double y100 = ggp_div_ge1(100.0, 1.0 + ax);
     const int k = min((int)y100, GGP_DAWSON_NINT - 1);
     const double *c = tab + GGP_DAWSON_NCOEF * k;
@@ -102,6 +115,7 @@ struct ggp_innov {
 GGP_DEV void ggp_innovation(const double *m, const double *C, const double var_x, const double var_g,
                             const int scaled, const double fp_auto, ggp_innov &v)
 {
+    GGP_CONTRACT
     const double d11 = scaled ? var_g * (m[1] + fp_auto) : var_g;
     v.S00 = C[0] + var_x;
     v.S01 = C[1] + 0.0;
@@ -134,6 +148,7 @@ GGP_DEV double ggp_det_pplu(double s00, double s01, double s10, double s11)
 // log_likelihood (likelihood.h:26-32). two_log_2pi is 2*log(2*M_PI) as the host folds it.
 GGP_DEV double ggp_ll_term(const double x0, const double x1, const ggp_innov &v, const double two_log_2pi)
 {
+    GGP_CONTRACT
     const double h0 = -0.5 * x0, h1 = -0.5 * x1;
     const double r0 = h0 * v.si00 + h1 * v.si10;
     const double r1 = h0 * v.si01 + h1 * v.si11;
@@ -143,6 +158,7 @@ GGP_DEV double ggp_ll_term(const double x0, const double x1, const ggp_innov &v,
 
 GGP_DEV void ggp_posterior(double *m, double *C, const double x0, const double x1, const ggp_innov &v)
 {
+    GGP_CONTRACT
     double K[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) K[i] = C[i];

@@ -227,9 +227,9 @@ constexpr int kOSlots = 10;
 constexpr int kParts[2][4] = {{1 | 2, 4 | 8, 0, 0}, {1, 2, 4, 8}};
 
 template <int OFF, size_t... J>
-GGP_DEV void exps(const ggp::Step &S, double *X, std::index_sequence<J...> seq)
+GGP_DEV void exps(const ggp::Step &S, double *Xc, std::index_sequence<J...> seq)
 {
-    ggp::lane_exps_flagged<OFF>(S, X, seq);   // the lane schedule's exponentials (ggp_prop.h), tasks OFF + J
+    ggp::lane_exps_flagged<OFF>(S, Xc, seq);   // the lane schedule's computed exponentials (ggp_prop.h), OFF + J
 }
 template <int OFF, size_t... J>
 GGP_DEV void dawsons(const ggp::Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
@@ -266,24 +266,24 @@ template <int W, int Q, int CPW>
 GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, const double *tab, double *Xl,
                        double *Dl, double *Il, double *Ol, const int lane)
 {
-    constexpr int X0 = ggp::NXT * W / Q, XN = ggp::NXT * (W + 1) / Q - X0;
+    constexpr int X0 = ggp::NXC * W / Q, XN = ggp::NXC * (W + 1) / Q - X0;
     constexpr int D0 = ggp::ND * W / Q, DN = ggp::ND * (W + 1) / Q - D0;
     constexpr int I0 = ggp::NI * W / Q, IN = ggp::NI * (W + 1) / Q - I0;
     ggp::Step S;
     ggp::step_init(S, m, C, t, P);
-    double X[ggp::NX], Dw[ggp::ND];
-    exps<X0>(S, X, std::make_index_sequence<XN>{});
-    X[ggp::X_ONE] = 1.0;
+    double Xc[ggp::NXC], X[ggp::NXE], Dw[ggp::ND];
+    exps<X0>(S, Xc, std::make_index_sequence<XN>{});
     dawsons<D0>(S, Dw, tab, std::make_index_sequence<DN>{});
     const bool own = lane < CPW;   // lanes past CPW hold no cell and store nothing
     const int ln = own ? lane : 0;
     if (own) {
-        put_part<ggp::NXT, W, Q, CPW>(X, Xl, lane);
+        put_part<ggp::NXC, W, Q, CPW>(Xc, Xl, lane);
         put_part<ggp::ND, W, Q, CPW>(Dw, Dl, lane);
     }
     __syncthreads();
-    get_rest<ggp::NXT, W, Q, CPW>(X, Xl, ln);
+    get_rest<ggp::NXC, W, Q, CPW>(Xc, Xl, ln);
     get_rest<ggp::ND, W, Q, CPW>(Dw, Dl, ln);
+    ggp::lane_expand(Xc, X);   // the slots, X_ONE and the products, in every wave
     double PW[ggp::NPW];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
 {
     static_assert(Q == 2 || Q == 4, "two or four waves per workgroup");
     __shared__ double s_tab[kDawsonTab];
-    __shared__ double s_x[ggp::NXT * CPW], s_d[ggp::ND * CPW], s_i[ggp::NI * CPW],
+    __shared__ double s_x[ggp::NXC * CPW], s_d[ggp::ND * CPW], s_i[ggp::NI * CPW],
         s_o[pair::kOSlots * CPW];
     __shared__ int s_rows[64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -549,7 +549,7 @@ __device__ unsigned long long g_pstamp[2][9];   // [level > 1024 cells][phase], 
 #define GGP_PSTAMP_FLUSH()
 #endif
 
-constexpr int kSlot = ggp::NX + ggp::ND + ggp::NPW + ggp::NI + ggp::SB_N;   // doubles of LDS per cell
+constexpr int kSlot = ggp::NXE + ggp::ND + ggp::NPW + ggp::NI + ggp::SB_N;   // doubles of LDS per cell
 
 
 template <int G>
@@ -560,7 +560,8 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
                                                      int32_t *__restrict__ cell_nan)
 {
     constexpr int CPW = 64 / G;
-    constexpr int NXB = (ggp::NXT + G - 1) / G;   // exponential slots per lane
+    constexpr int NXB = (ggp::NXC + G - 1) / G;   // computed exponentials per lane
+    constexpr int NPB = (ggp::NXP + G - 1) / G;   // product exponentials per lane
     constexpr int NDB = (ggp::ND + G - 1) / G;    // Dawson slots per lane
     constexpr int NCB = (ggp::NI + G - 1) / G;    // integral slots per lane
     __shared__ double lds[CPW * kSlot];
@@ -572,19 +573,26 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
     const int i = blockIdx.x * CPW + slot;
     const bool valid = i < n;
     double *Xl = lds + slot * kSlot;
-    double *Dl = Xl + ggp::NX;
+    double *Dl = Xl + ggp::NXE;
     double *Pl = Dl + ggp::ND;
     double *Il = Pl + ggp::NPW;
     double *Sb = Il + ggp::NI;        // the step block (ggp_prop.h)
     // this lane's task descriptors never change: keep them in registers (no loads in the step
     // loop).  Slots past the end of a list run task 0 and are not stored, so every slot is
     // computed unconditionally and the compiler can overlap their dependency chains.
-    uint32_t xd[NXB], dd[NDB];
+    uint32_t xd[NXB], xj[NXB], pd[NPB], dd[NDB];
     ggp::ITask cd[NCB];
 #pragma unroll
     for (int q = 0; q < NXB; ++q) {
         const int j = lg + q * G;
-        xd[q] = ggp::pack_x(ggp::kXT[j < ggp::NXT ? j : 0]);
+        xd[q] = ggp::pack_x(ggp::kXC.T[j < ggp::NXC ? j : 0]);
+        xj[q] = ggp::kXC.j[j < ggp::NXC ? j : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < NPB; ++q) {
+        const int j = lg + q * G;
+        const ggp::XProd d = ggp::kXP[j < ggp::NXP ? j : 0];
+        pd[q] = d.j | d.rep << 8 | (uint32_t)d.fac << 16;
     }
 #pragma unroll
     for (int q = 0; q < NDB; ++q) {
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
             const double pw = ggp::pow_task(S, lg < 3 ? lg : 0);
 #pragma unroll
             for (int q = 0; q < NXB; ++q)
-                if (lg + q * G < ggp::NXT) Xl[lg + q * G] = ev[q];
+                if (lg + q * G < ggp::NXC) Xl[xj[q]] = ev[q];
 #pragma unroll
             for (int q = 0; q < NDB; ++q)
                 if (lg + q * G < ggp::ND) Dl[lg + q * G] = dv[q];
@@ -656,6 +664,12 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
             }
         }
         GGP_STAMP(2);
+        __syncthreads();
+        if (prop) {   // the product exponentials (ggp_prop.h kXP), from the computed ones
+#pragma unroll
+            for (int q = 0; q < NPB; ++q)
+                if (lg + q * G < ggp::NXP) Xl[pd[q] & 0xff] = Xl[pd[q] >> 8 & 0xff] * Xl[pd[q] >> 16];
+        }
         __syncthreads();
         GGP_STAMP(3);
         if (prop) {
@@ -1477,6 +1491,10 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
     const double *pi = seg_params(F, ptab, n_seg, r1 - 1);          // :376-378
     const int d1 = F.d1[c], d2 = F.d2[c];
     double m[4], C[16];
+    // the propagation before row r's update (one call site: the division's and the rows' steps)
+    bool pend = false;
+    double dtp = 0.0;
+    const double *pq = pi;   // its parameters (the reversed model)
     if (d1 < 0 && d2 < 0) {
         // init_sc_distribution_r leaf branch (:317-332): on top of the forward final state
         const double *st = pstate + (size_t)20 * c;
@@ -1511,12 +1529,19 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
             ggp::division_map_r(m2, C2, pi[9], pi[10], F.binomial, F.log2);
             ggp::mult_gauss(m, C, m2, C2);
         }
-        const double dt = F.time[F.row_off[d1]] - F.time[r1 - 1];
-        ggp::propagate_lane(m, C, dt, ggp::make_ou(-pi[0], pi[1], pi[2], -pi[3], pi[4], pi[5], -pi[6]), s_tab);
+        dtp = F.time[F.row_off[d1]] - F.time[r1 - 1];
+        pend = true;
     }
     const double *ou_src = nullptr;   // as k_fwd_level: the OU constants per segment change only
     ggp::OU ou{};
     for (int64_t r = r1 - 1; r >= r0; --r) {
+        if (pend) {
+            if (pq != ou_src) {
+                ou = ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]);
+                ou_src = pq;
+            }
+            ggp::propagate_lane(m, C, dtp, ou, s_tab);
+        }
         double rm[4], rC[16];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rm[k] = m[k];
@@ -1530,13 +1555,10 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
         ggp_innov v;
         ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
         ggp_posterior(m, C, x0, x1, v);
-        if (r > r0) {
-            const double *q = seg_params(F, ptab, n_seg, r - 1);
-            if (q != ou_src) {
-                ou = ggp::make_ou(-q[0], q[1], q[2], -q[3], q[4], q[5], -q[6]);
-                ou_src = q;
-            }
-            ggp::propagate_lane(m, C, F.time[r] - F.time[r - 1], ou, s_tab);
+        pend = r > r0;
+        if (pend) {
+            pq = seg_params(F, ptab, n_seg, r - 1);
+            dtp = F.time[r] - F.time[r - 1];
         }
     }
     store20(pstate + (size_t)20 * c, m, C);
@@ -1580,7 +1602,7 @@ GGP_DEV void adopt_lane0(const bool valid, double *m, double *C, double &dt)
 
 #define GGP_PAIR_LDS(CPW)                                                                         \
     __shared__ double s_tab[kDawsonTab];                                                          \
-    __shared__ double s_x[ggp::NXT * (CPW)], s_d[ggp::ND * (CPW)], s_i[ggp::NI * (CPW)],          \
+    __shared__ double s_x[ggp::NXC * (CPW)], s_d[ggp::ND * (CPW)], s_i[ggp::NI * (CPW)],          \
         s_o[pair::kOSlots * (CPW)];                                                               \
     __shared__ int s_rows[64]
 
@@ -1738,9 +1760,10 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
             for (int q = 0; q < 16; ++q) C[q] = Cn[q];
         }
     };
-    if (__builtin_amdgcn_ballot_w64(internal)) prop(internal, dt);
     bool live = valid && nrows > 0;
+    bool pend = internal;   // the propagation before this row's update (one call site)
     for (int k = 0; k < kmax; ++k) {
+        if (__builtin_amdgcn_ballot_w64(pend)) prop(pend, dt);
         const int64_t r = r1 - 1 - k;
         bool more = false;
         if (live) {
@@ -1763,7 +1786,7 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
                 dt = F.time[r] - F.time[r - 1];
             }
         }
-        if (__builtin_amdgcn_ballot_w64(more)) prop(more, dt);
+        pend = more;
         live = more;
     }
     if (valid && w == 0) store20(pstate + (size_t)20 * c, m, C);

@@ -153,6 +153,60 @@ constexpr XTask kXT[NXT] = {
     {KX_Z, 3, cF, 1}, {KX_Z, 3, cF, 2}, {KX_Z, 5, cH, 1}, {KX_Z, 5, cH, 2},
 };
 
+// ---- the lane schedules' exponentials: 54 computed, 22 products ------------------------------
+// Several c values differ by a multiple of t: c_B = c_A - gl t, c_J = c_I = c_A - gq t,
+// c_G = c_A - b t, c_E = c_C, c_D = c_C - gq t, c_F = c_C + gq t.  So 22 of the 74 slots are
+// exp(c_rep + ...) exp(+-k t): the product of a computed exponential and one of exp(-gl t),
+// exp(-gq t) (slots XS_gl, XS_gq), exp(-b t) or exp(gq t) (two more exponentials, slots XF_MBT
+// and XF_PGQ past NX), or a copy (factor X_ONE = 1).  The argument of a product's factors is O(1)
+// with no cancellation, so a product is within ~2 ulp of the direct exponential (ggp_wave.h
+// forms the same products).  The lane, lane-pair, group, batch and smoother kernels all take the
+// products, so they stay bitwise equal to one another.
+enum { XF_MBT = NX, XF_PGQ, NXE };   // slots of the lane schedules' X arrays (NXE doubles)
+constexpr XTask kXF[2] = {{KX_S, 6, 0, 0}, {KX_S, 7, 0, 0}};   // exp(-b t), exp(gq t): pickSV 6, 7
+
+struct XProd { unsigned char j, rep, fac; };   // X[j] = X[rep] * X[fac]
+constexpr XProd kXP[] = {
+    {XC_B, XC_A, XS_gl},     {XC_J, XC_A, XS_gq},     {XC_G, XC_A, XF_MBT},    {XC_I, XC_A, XS_gq},
+    {XC_D, XC_C, XS_gq},     {XC_E, XC_C, X_ONE},     {XC_F, XC_C, XF_PGQ},
+    {XZ_1Bt, XZ_1At, XS_gl}, {XZ_1Jt, XZ_1At, XS_gq}, {XZ_1Gt, XZ_1At, XF_MBT},
+    {XZ_2Bt, XZ_2At, XS_gl}, {XZ_2Jt, XZ_2At, XS_gq}, {XZ_2It, XZ_2At, XS_gq}, {XZ_2Gt, XZ_2At, XF_MBT},
+    {XZ_3Et, XZ_3Ct, X_ONE}, {XZ_3Dt, XZ_3Ct, XS_gq}, {XZ_4Et, XZ_4Ct, X_ONE}, {XZ_4Ft, XZ_4Ct, XF_PGQ},
+    {XZ_3E2, XZ_3C2, X_ONE}, {XZ_3D2, XZ_3C2, XS_gq}, {XZ_4E2, XZ_4C2, X_ONE}, {XZ_4F2, XZ_4C2, XF_PGQ},
+};
+constexpr int NXP = sizeof(kXP) / sizeof(kXP[0]);
+constexpr int NXC = NXT - NXP + 2;   // exponentials computed per step
+
+constexpr bool x_is_product(const int j)
+{
+    for (int p = 0; p < NXP; ++p)
+        if (kXP[p].j == j) return true;
+    return false;
+}
+struct XCList {
+    unsigned char j[NXC];   // destination slot
+    XTask T[NXC];
+};
+constexpr XCList make_xc()
+{
+    XCList L{};
+    int n = 0;
+    for (int j = 0; j < NXT; ++j)
+        if (!x_is_product(j)) { L.j[n] = (unsigned char)j; L.T[n] = kXT[j]; ++n; }
+    L.j[n] = XF_MBT; L.T[n] = kXF[0]; ++n;
+    L.j[n] = XF_PGQ; L.T[n] = kXF[1]; ++n;
+    return L;
+}
+constexpr XCList kXC = make_xc();
+static_assert(NXP == 22 && NXC == 54, "54 computed exponentials, 22 products");
+constexpr bool check_products()
+{
+    for (int p = 0; p < NXP; ++p)   // every operand is a computed slot
+        if (x_is_product(kXP[p].rep) || x_is_product(kXP[p].fac)) return false;
+    return true;
+}
+static_assert(check_products(), "a product's operands are computed exponentials");
+
 // Dawson slots D(B, t_i)
 enum { D_1_0 = 0, D_1_t, D_2_0, D_2_t, D_3_0, D_3_t, D_3_2, D_4_0, D_4_t, D_4_2, D_5_0, D_5_t,
        D_6_t, D_6_2, ND };
@@ -272,6 +326,7 @@ struct Step {
 
 GGP_DEV void step_init(Step &S, const double *m, const double *C, const double t, const OU &P)
 {
+    GGP_CONTRACT
     const double ml = P.ml, gl = P.gl, gq = P.gq, b = P.b;
     S.bx = m[0]; S.bg = m[1]; S.bl = m[2]; S.bq = m[3];
     S.Cxx = C[0]; S.Cxg = C[1]; S.Cxl = C[2]; S.Cxq = C[3];
@@ -324,10 +379,13 @@ GGP_DEV double pickC(const Step &S, int i)
          : i == 5 ? S.c5 : i == 6 ? S.c6 : i == 7 ? S.c7 : i == 8 ? S.c8 : S.c9;
 }
 GGP_DEV double pickT(const Step &S, int i) { return i == 0 ? 0.0 : i == 1 ? S.t : S.t2; }
-// the exponents s of exp(s t) (mean_cov_model.h: b, b + gl, 2b, b + gq, -gl, -gq)
+// the exponents s of exp(s t) (mean_cov_model.h: b, b + gl, 2b, b + gq, -gl, -gq; then the
+// product factors' -b, gq)
+constexpr int NSV = 8;
 GGP_DEV double pickSV(const Step &S, int s)
 {
-    return s == 0 ? S.b : s == 1 ? S.b + S.gl : s == 2 ? 2 * S.b : s == 3 ? S.b + S.gq : s == 4 ? -S.gl : -S.gq;
+    return s == 0 ? S.b : s == 1 ? S.b + S.gl : s == 2 ? 2 * S.b : s == 3 ? S.b + S.gq : s == 4 ? -S.gl
+         : s == 5 ? -S.gq : s == 6 ? -S.b : S.gq;
 }
 GGP_DEV double Step::Bv(int i) const { return pickB(*this, i); }
 GGP_DEV double Step::Cv(int i) const { return pickC(*this, i); }
@@ -340,7 +398,7 @@ GGP_DEV double Step::SVv(int s) const { return pickSV(*this, s); }
 // the task stages.  Values are copies, so results are bitwise those of the register form.
 enum {
     SB_B = 0, SB_C = SB_B + 6, SB_T = SB_C + 10, SB_SV = SB_T + 3,
-    SB_A = SB_SV + 6, SB_TWO_A, SB_FOUR_A, SB_R_FOUR_A, SB_TWO_SA, SB_R_TWO_SA, SB_M2SA, SB_FOUR_AA,
+    SB_A = SB_SV + NSV, SB_TWO_A, SB_FOUR_A, SB_R_FOUR_A, SB_TWO_SA, SB_R_TWO_SA, SB_M2SA, SB_FOUR_AA,
     SB_STATE,                         // bx bg bl bq Cxx Cxg Cxl Cxq Cgg Cgl Cgq Cll Clq Cqq
     SB_N = SB_STATE + 14
 };
@@ -372,7 +430,7 @@ GGP_DEV void store_step(const Step &S, double *sb)
 #pragma unroll
     for (int i = 0; i < 3; ++i) sb[SB_T + i] = pickT(S, i);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) sb[SB_SV + i] = pickSV(S, i);
+    for (int i = 0; i < NSV; ++i) sb[SB_SV + i] = pickSV(S, i);
     sb[SB_A] = S.a; sb[SB_TWO_A] = S.two_a; sb[SB_FOUR_A] = S.four_a; sb[SB_R_FOUR_A] = S.r_four_a;
     sb[SB_TWO_SA] = S.two_sa; sb[SB_R_TWO_SA] = S.r_two_sa; sb[SB_M2SA] = S.m2sa; sb[SB_FOUR_AA] = S.four_aa;
     const double st[14] = {S.bx, S.bg, S.bl, S.bq, S.Cxx, S.Cxg, S.Cxl, S.Cxq, S.Cgg, S.Cgl, S.Cgq, S.Cll, S.Clq, S.Cqq};
@@ -420,6 +478,7 @@ struct StepL {
 template <class ST>
 GGP_DEV double zval(const ST &S, int iB, int it)
 {
+    GGP_CONTRACT
     const double B = S.Bv(iB);
     const double num = it == 0 ? B : B + S.two_a * S.Tv(it);
     return rdiv(num, S.two_sa, S.r_two_sa);
@@ -428,6 +487,7 @@ GGP_DEV double zval(const ST &S, int iB, int it)
 template <class ST>
 GGP_DEV double exp_arg_body(const ST &S, const XTask T)
 {
+    GGP_CONTRACT
     // branch-free: every candidate argument is formed from selected operands and the kind
     // picks one, so lanes holding different kinds do not serialise (group schedule)
     const double ti = S.Tv(T.it);
@@ -485,6 +545,7 @@ constexpr int NPW = 6;   // 3 denominators + 3 reciprocals
 template <class ST, class XA, class DA, class PA>
 GGP_DEV double tau_body(const ST &S, const ITask T, const XA &X, const DA &Dw, const PA &PW)
 {
+    GGP_CONTRACT
     const double D0 = Dw[T.d0], D1 = Dw[T.d1];
     if (T.k == 0) {   // zerotauint
         const double Z0 = X[T.x0], Z1 = X[T.x1];
@@ -554,10 +615,11 @@ GGP_DEV double tau_task(const Step &S, int j, const XA &X, const DA &Dw, const P
 template <int PARTS = 15, class IA, class XA>
 GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double *C)
 {
+    GGP_CONTRACT
     const double t = S.t, bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
     const double Cxx = S.Cxx, Cxg = S.Cxg, Cxl = S.Cxl, Cxq = S.Cxq, Cgg = S.Cgg, Cgl = S.Cgl;
     const double Cgq = S.Cgq, Cll = S.Cll, Clq = S.Clq, Cqq = S.Cqq;
-    const double ml = S.ml, gl = S.gl, sl2 = S.sl2, mq = S.mq, gq = S.gq, sq2 = S.sq2;
+    const double ml = S.ml, gl = S.gl, mq = S.mq, gq = S.gq, sq2 = S.sq2;
     const double rgl = S.r_gl, rgq = S.r_gq;
     const double ebt = X[XS_bt], ebglt = X[XS_bglt], e2bt = X[XS_2bt], ebgqt = X[XS_bgqt];
     const double egl = X[XS_gl], egq = X[XS_gq];
@@ -698,6 +760,7 @@ GGP_DEV void outputs(const Step &S, const IA &I, const XA &X, double *m, double 
 template <class IA, class XA>
 GGP_DEV void cross_outputs(const Step &S, const IA &I, const XA &X, double *K)
 {
+    GGP_CONTRACT
     const double bx = S.bx, bg = S.bg, bl = S.bl, bq = S.bq;
     const double Cxx = S.Cxx, Cxg = S.Cxg, Cxl = S.Cxl, Cxq = S.Cxq, Cgg = S.Cgg, Cgl = S.Cgl;
     const double Cgq = S.Cgq, Cll = S.Cll, Clq = S.Clq, Cqq = S.Cqq;
@@ -738,17 +801,37 @@ GGP_DEV void lane_exps(const Step &S, double *X, std::index_sequence<J...>)
 {
     ((X[J] = exp_body(S, XTask{kXT[J].kind, kXT[J].iB, kXT[J].ic, kXT[J].it})), ...);
 }
+// the computed exponentials kXC, tasks K: Xc[K] (the list's order; lane_expand puts them in
+// their slots)
+template <size_t... K>
+GGP_DEV void lane_exps_c(const Step &S, double *Xc, std::index_sequence<K...>)
+{
+    ((Xc[K] = exp_body(S, XTask{kXC.T[K].kind, kXC.T[K].iB, kXC.T[K].ic, kXC.T[K].it})), ...);
+}
 // the same values with exp_lane (one compare per exponential instead of ocml's checks): faster
 // where registers allow (the lane-pair schedule's share of the tasks: C4 shard 0.81 -> 0.79 ms),
-// slower in the one-wave lane and smoother kernels, which keep lane_exps (tools/lane_ab.py)
-template <size_t OFF, size_t... J>
-GGP_DEV void lane_exps_flagged(const Step &S, double *X, std::index_sequence<J...>)
+// slower in the one-wave lane and smoother kernels, which keep lane_exps_c (tools/lane_ab.py)
+template <size_t OFF, size_t... K>
+GGP_DEV void lane_exps_flagged(const Step &S, double *Xc, std::index_sequence<K...>)
 {
     bool big = false;
-    ((X[OFF + J] = exp_lane(exp_arg_body(S, XTask{kXT[OFF + J].kind, kXT[OFF + J].iB, kXT[OFF + J].ic, kXT[OFF + J].it}),
-                            big)), ...);
+    ((Xc[OFF + K] = exp_lane(exp_arg_body(S, XTask{kXC.T[OFF + K].kind, kXC.T[OFF + K].iB, kXC.T[OFF + K].ic,
+                                                    kXC.T[OFF + K].it}), big)), ...);
     if (big)   // an argument beyond kExpFastMax (inf / NaN states): ocml's exp for this lane's set
-        ((X[OFF + J] = exp_body(S, XTask{kXT[OFF + J].kind, kXT[OFF + J].iB, kXT[OFF + J].ic, kXT[OFF + J].it})), ...);
+        ((Xc[OFF + K] = exp_body(S, XTask{kXC.T[OFF + K].kind, kXC.T[OFF + K].iB, kXC.T[OFF + K].ic,
+                                          kXC.T[OFF + K].it})), ...);
+}
+// Xc (the computed list) into the slots of X [NXE], X_ONE, then the 22 products
+template <size_t... K, size_t... P>
+GGP_DEV void lane_expand(const double *Xc, double *X, std::index_sequence<K...>, std::index_sequence<P...>)
+{
+    ((X[kXC.j[K]] = Xc[K]), ...);
+    X[X_ONE] = 1.0;
+    ((X[kXP[P].j] = X[kXP[P].rep] * X[kXP[P].fac]), ...);
+}
+GGP_DEV void lane_expand(const double *Xc, double *X)
+{
+    lane_expand(Xc, X, std::make_index_sequence<NXC>{}, std::make_index_sequence<NXP>{});
 }
 template <size_t... J>
 GGP_DEV void lane_dawsons(const Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
@@ -774,9 +857,13 @@ GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, c
 {
     Step S;
     step_init(S, m, C, t, P);
-    double X[NX];
-    lane_exps(S, X, std::make_index_sequence<NXT>{});
-    X[X_ONE] = 1.0;
+    double Xc[NXC], X[NXE];
+#ifdef GGP_LANE_FLAGGED
+    lane_exps_flagged<0>(S, Xc, std::make_index_sequence<NXC>{});
+#else
+    lane_exps_c(S, Xc, std::make_index_sequence<NXC>{});
+#endif
+    lane_expand(Xc, X);
     double Dw[ND];
     lane_dawsons(S, Dw, tab, std::make_index_sequence<ND>{});
     double PW[NPW];

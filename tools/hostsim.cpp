@@ -110,3 +110,29 @@ void hs_mcm_wave(double *m, double *C, double t, const double *p)
     out_store(o, m, C);
 }
 }
+
+// ---- the lane step with a chosen subset of the 22 product exponentials (kXP): products whose
+// bit is clear in hs_xp_mask are computed directly (exp of their own argument) ----
+static unsigned long long hs_xp_mask = ~0ull;
+extern "C" {
+void hs_set_xp_mask(unsigned long long m) { hs_xp_mask = m; }
+void hs_mcm_lane_mask(double *m, double *C, double t, const double *p)
+{
+    using namespace ggp;
+    const OU P = make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+    Step S;
+    step_init(S, m, C, t, P);
+    double Xc[NXC], X[NXE];
+    lane_exps_c(S, Xc, std::make_index_sequence<NXC>{});
+    lane_expand(Xc, X);
+    for (int q = 0; q < NXP; ++q)
+        if (!((hs_xp_mask >> q) & 1)) X[kXP[q].j] = exp_body(S, kXT[kXP[q].j]);
+    double Dw[ND];
+    lane_dawsons(S, Dw, ggp_dawson_coef, std::make_index_sequence<ND>{});
+    double PW[NPW];
+    for (int q = 0; q < 3; ++q) { PW[q] = pow_task(S, q); PW[3 + q] = frcp(PW[q]); }
+    double I[NI];
+    lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
+    outputs(S, I, X, m, C);
+}
+}
