@@ -875,7 +875,11 @@ GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, c
     double I[NI];
     lane_taus(S, X, Dw, PW, I, std::make_index_sequence<NI>{});
     if (K) cross_outputs(S, I, X, K);
+#ifdef GGP_STUB_OUT   // diagnostic probe only (tools/gpu_r4g.sh): the outputs stage left out
+    for (int j = 0; j < NI; ++j) C[j & 15] += 1e-300 * (I[j] * X[XS_bt + (j % 6)]);
+#else
     outputs(S, I, X, m, C);
+#endif
 }
 
 // division map of mean_cov_after_division (predictions.h:40-60), after the propagation
