@@ -7,9 +7,10 @@
 //   ggp_posterior
 // The propagator (mean_cov_model.h) is in ggp_prop.h.
 //
-// Evaluation order follows the reference expression by expression (no FMA contraction:
-// the library is built with -ffp-contract=off).  Transcendental libm differences (ocml vs
-// glibc, <= 1 ulp) move the total log-likelihood by ~1e-11 relative (measured).
+// Evaluation order follows the reference expression by expression.  The library is built with
+// -ffp-contract=off; the bodies the lane schedules run fuse a*b + c within one expression
+// (GGP_CONTRACT below).  Rounding at that level, like ocml's exp against glibc's (<= 1 ulp),
+// moves the total log-likelihood by ~1e-10 relative at most (measured, DESIGN.md "Parity").
 #pragma once
 #include <math.h>
 

@@ -454,8 +454,8 @@ __global__ __launch_bounds__(256) void k_replicate(const double *__restrict__ sr
 // ------------------------------------------------------------------------------------------
 // GROUP schedule: G lanes per cell, 64/G cells per single-wave workgroup.  The Kalman update
 // and the scalar bookkeeping run redundantly in the G lanes of a cell; the propagation's
-// 74 exponentials + 14 Dawson values + 3 powers and then its 45 integrals are spread over
-// the G lanes through LDS (ggp_prop.h tasks), cutting the per-step latency that bounds
+// 54 computed exponentials (then the 22 products) + 14 Dawson values + 3 powers and then its
+// 45 integrals are spread over the G lanes through LDS (ggp_prop.h tasks), cutting the per-step latency that bounds
 // small forests.  Bitwise identical to the lane schedule.
 // ------------------------------------------------------------------------------------------
 // Optional launch timeline (tools/timeline.hip builds this file with GGP_TIMELINE; the shipped

@@ -5,10 +5,12 @@
 //                  (unrolled), arrays live in registers;
 //   group kernel : G lanes own a cell; lane l runs tasks l, l+G, ...; arrays live in LDS.
 //
-// Both schedules execute the SAME expression for every value, so they are bitwise equal
-// (tests/test_gpu_parity.py).  Every expression keeps the reference's evaluation order;
-// the 59 tauint calls of one step dedupe to 45 distinct integrals over 74 distinct
-// exponentials and 14 Dawson values (identical inputs -> identical bits).
+// Both schedules (and the lane-pair, batch and smoother kernels) execute the SAME expression
+// for every value, so they are bitwise equal (tests/test_gpu_parity.py).  The expressions are
+// the reference's, term by term, with two departures that all these kernels share: a*b + c
+// inside one expression is one fma (GGP_CONTRACT), and 22 of the 74 exponentials are products
+// of two others (kXP below).  The 59 tauint calls of one step dedupe to 45 distinct integrals
+// over 74 distinct exponentials (54 computed) and 14 Dawson values.
 //
 // Division: x/d for a denominator used several times per step is evaluated as
 // q = x*r, e = fma(-q,d,x), q' = fma(e,r,q) with r = 1/d correctly rounded (Markstein):
