@@ -110,19 +110,27 @@ def make_forest(a: dict) -> OraForest:
 class OracleForest:
     """CPU oracle over the same arrays, with its own carried state."""
 
-    def __init__(self, arrays: dict, exp_ulp_noise: int = 0):
+    def __init__(self, arrays: dict, exp_ulp_noise: int = 0, ref_dawson: bool = False):
         """exp_ulp_noise != 0: run on the conditioning-probe build with exp() moved +-1 ulp at
-        random (seeded) -- tells a test which outputs rounding alone can move"""
+        random (seeded) -- tells a test which outputs rounding alone can move.
+        ref_dawson: every Dawson value from the reference's own Faddeeva::Dawson (Faddeeva.cc,
+        compiled in place into oracle/_ref; build container only) instead of the restatement's
+        table -- the likelihood then runs the reference's own Dawson arithmetic"""
         self.f = make_forest(arrays)
         self._noise = int(exp_ulp_noise)
+        self._ref_dawson = bool(ref_dawson)
+        if self._ref_dawson and faddeeva_ref() is None:
+            raise FileNotFoundError(f"{REF_FADDEEVA} is missing: `make -C oracle ref` (needs /root/reference)")
         self.state = np.zeros((self.f.n_cells, 20))
         self.cell_ll = np.zeros(self.f.n_cells)
 
     def _L(self):
-        if not self._noise:
+        if not self._noise and not self._ref_dawson:
             return lib()
         L = lib(sens=True)
-        L.ora_set_exp_ulp_noise(self._noise)    # re-seeded per call: deterministic
+        L.ora_set_exp_ulp_noise(self._noise)    # re-seeded per call: deterministic (0: exact exp)
+        hook = ctypes.c_void_p.in_dll(L, "ora_dawson_hook")
+        hook.value = ctypes.cast(faddeeva_ref(), ctypes.c_void_p).value if self._ref_dawson else None
         return L
 
     def total_likelihood(self, params):
@@ -178,13 +186,19 @@ def mean_cov_model(mean, cov, t: float, p7):
     return m, C.reshape(4, 4)
 
 
+_faddeeva = None
+
+
 def faddeeva_ref():
     """Faddeeva::Dawson(double) of the reference's own Faddeeva.cc, compiled in place into
     oracle/_ref by `make -C oracle ref` (only where /root/reference exists)."""
-    if not os.path.exists(REF_FADDEEVA):
-        return None
-    L = ctypes.CDLL(REF_FADDEEVA)
-    fn = L._ZN8Faddeeva6DawsonEd
-    fn.restype = ctypes.c_double
-    fn.argtypes = [ctypes.c_double]
-    return fn
+    global _faddeeva
+    if _faddeeva is None:
+        if not os.path.exists(REF_FADDEEVA):
+            return None
+        L = ctypes.CDLL(REF_FADDEEVA)
+        fn = L._ZN8Faddeeva6DawsonEd
+        fn.restype = ctypes.c_double
+        fn.argtypes = [ctypes.c_double]
+        _faddeeva = fn
+    return _faddeeva

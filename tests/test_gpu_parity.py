@@ -57,6 +57,28 @@ def test_example_carried_state_chain(example_forests, noise, div, params, kernel
         assert _rel(vg, vo) < REL, (call, vg, vo)
 
 
+REF_DAWSON = json.load(open(os.path.join(GOLDEN, "oracle_example_refdawson.json")))
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_example_chain_vs_reference_dawson_totals(example_forests, kernel):
+    """the same chains against the oracle run on the reference's own Faddeeva::Dawson
+    (tests/golden/oracle_example_refdawson.json, make_refdawson.py): the device holds the 1e-9
+    bar against the reference's Dawson arithmetic as well as against the oracle's table"""
+    import gfp_gaussian_process_amd as g
+    worst = 0.0
+    for key, v in REF_DAWSON.items():
+        noise, div, _ = key.split("/")
+        fg = g.Forest(example_forests[(noise, div)], kernel=kernel)
+        params = [float.fromhex(x) for x in v["params"]]
+        for call in range(3):
+            vg = fg.total_likelihood(params)
+            vr = float.fromhex(v["ll"][call])
+            worst = max(worst, _rel(vg, vr))
+            assert _rel(vg, vr) < REL, (key, call, vg, vr)
+    print(f"{kernel}: worst rel vs the reference-Dawson totals {worst:.2e}")
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_example_state_matches_oracle(example_forests, kernel):
     import gfp_gaussian_process_amd as g
