@@ -2442,6 +2442,10 @@ struct Shard {
     double *d_j_ptab = nullptr, *d_j_pstate = nullptr, *d_j_fwd = nullptr, *d_j_bwd = nullptr;
     double *d_j_back = nullptr, *d_j_cond = nullptr, *d_j_start = nullptr;
     std::vector<double> j_params;      // the table the joint tables hold (empty: none)
+    // -j per-call buffers, grow-only (no hipMalloc / synchronising hipFree per start-row range):
+    // the walks' stacks and counts, sized by start rows x depth, and the emitted joints
+    void *d_jw_stack = nullptr, *d_jw_small = nullptr, *d_jw_out = nullptr;
+    size_t jw_stack_bytes = 0, jw_small_bytes = 0, jw_out_bytes = 0;
 };
 
 // RCCL entry points, resolved at run time from the library the caller names (the one torch
@@ -2718,7 +2722,29 @@ void shard_free_joints(Shard *f)
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    for (void **p : {&f->d_jw_stack, &f->d_jw_small, &f->d_jw_out}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    f->jw_stack_bytes = f->jw_small_bytes = f->jw_out_bytes = 0;
     f->j_params.clear();
+}
+
+// a grow-only device buffer of at least `bytes` (the stream is idle when this is called)
+void *jw_reserve(void **buf, size_t *have, size_t bytes)
+{
+    bytes = std::max<size_t>(bytes, 256);
+    if (*buf && *have >= bytes) return *buf;
+    const size_t want = std::max(bytes, *have + *have / 2);
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    if (hipMalloc(buf, want) != hipSuccess) {
+        *buf = nullptr;
+        return nullptr;
+    }
+    *have = want;
+    return *buf;
 }
 
 void batch_free(Shard *f)
@@ -3164,23 +3190,18 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
         }
         if (e == hipSuccess) f->j_params = key;
     }
-    std::vector<void *> bufs;
-    auto alloc = [&](size_t bytes) -> void * {
-        void *p = nullptr;
-        if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
-        bufs.push_back(p);
-        return p;
-    };
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(f->stream);
-        for (void *p : bufs) (void)hipFree(p);
-    };
+    auto cleanup = [&]() { (void)hipStreamSynchronize(f->stream); };
+    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);   // the grow-only buffers are idle
     const int64_t ns = r_hi - r_lo;
     const int depth = (int)f->level_start.size();   // generations below any start, plus one
-    auto *d_stack_j = (double *)alloc((size_t)ns * depth * kJStart * sizeof(double));
-    auto *d_stack_c = (int32_t *)alloc((size_t)ns * depth * sizeof(int32_t));
-    auto *d_counts = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
-    if (!d_stack_j || !d_stack_c || !d_counts) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
+    const size_t b_stack_j = (size_t)ns * depth * kJStart * sizeof(double);
+    const size_t b_stack_c = ((size_t)ns * depth * sizeof(int32_t) + 255) & ~(size_t)255;
+    auto *stack = (char *)jw_reserve(&f->d_jw_stack, &f->jw_stack_bytes, b_stack_j + b_stack_c);
+    auto *small = (int64_t *)jw_reserve(&f->d_jw_small, &f->jw_small_bytes, (size_t)2 * ns * sizeof(int64_t));
+    if (!stack || !small) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
+    auto *d_stack_c = (int32_t *)stack;
+    auto *d_stack_j = (double *)(stack + b_stack_c);
+    int64_t *d_counts = small, *d_off = small + ns;
     const unsigned wblocks = (unsigned)((ns + 63) / 64);
     if (e == hipSuccess) {   // pass 1: count
         hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, f->d_j_ptab, n_seg,
@@ -3199,10 +3220,11 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
     }
     *n_out = total;
     if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
-        auto *d_off = (int64_t *)alloc((size_t)ns * sizeof(int64_t));
-        auto *d_idx = (int64_t *)alloc((size_t)total * 2 * sizeof(int64_t));
-        auto *d_val = (double *)alloc((size_t)total * kJStart * sizeof(double));
-        if (!d_off || !d_idx || !d_val) {
+        const size_t b_idx = (size_t)total * 2 * sizeof(int64_t);
+        auto *out = (char *)jw_reserve(&f->d_jw_out, &f->jw_out_bytes, b_idx + (size_t)total * kJStart * sizeof(double));
+        auto *d_idx = (int64_t *)out;
+        auto *d_val = (double *)(out + b_idx);
+        if (!out) {
             cleanup();
             g_last_err = "ggp_joints: device allocation failed";
             return GGP_ENOMEM;

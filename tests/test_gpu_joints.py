@@ -293,3 +293,26 @@ def test_joints_c5_shape_subset_cli_and_oracle(tmp_path):
     assert lines == total, (lines, total)
     for s in sample:
         assert got[s] == want[s], (s, got[s][:2], want[s][:2])
+
+
+def test_joints_into_reused_buffers_and_growing_workspace():
+    """Forest.joints(out=...) fills caller-owned buffers with the same joints as fresh arrays, range
+    after range (the engine's grow-only -j workspace: a small range, a larger one, a small one
+    again); a too-small buffer reports the count without writing past it"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(6, 200, seed=7)
+    f = g.Forest(hf)
+    nr = hf.n_rows
+    buf = (np.zeros((1 << 18, 2), np.int64), np.zeros((1 << 18, 72)))
+    for lo, hi in ((0, 17), (0, nr), (nr // 3, nr // 3 + 5), (nr - 40, nr)):
+        i0, v0 = f.joints(P, 1e-10, lo, hi, cap=1 << 18)
+        i1, v1 = f.joints(P, 1e-10, lo, hi, out=buf)
+        assert np.shares_memory(i1, buf[0]) and np.shares_memory(v1, buf[1])
+        assert np.array_equal(i0, i1) and np.array_equal(v0, v1), (lo, hi)
+    small = (np.full((4, 2), -7, np.int64), np.full((4, 72), -7.0))
+    with pytest.raises(g.GGPError):
+        f.joints(P, 1e-10, 0, nr, out=small)
+    assert np.all(small[0] == -7) and np.all(small[1] == -7.0)
+    with pytest.raises(ValueError):
+        f.joints(P, 1e-10, 0, 4, out=(np.zeros((4, 2), np.int32), np.zeros((4, 72))))
+    f.close()
