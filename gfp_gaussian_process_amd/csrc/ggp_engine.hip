@@ -1474,10 +1474,17 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
     store20(pstate + (size_t)20 * c, m, C);
 }
 
-// prediction_backward / sc_prediction_backward (predictions.h:368-444), levels bottom-up
+// prediction_backward / sc_prediction_backward (predictions.h:368-444), levels bottom-up.
+// COMB: combine_predictions (predictions.h:466-499, k_combine<true>'s combine_info) fused in: each
+// row's backward prior is combined with its forward row as soon as it is formed, into comb; the
+// backward rows themselves are stored only when out is given.  The same operations per row as
+// k_combine<true>, so the combined rows are bitwise the separate kernel's.
+template <bool COMB>
 __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
                                                   const int32_t *__restrict__ cells, int n, int cpw,
-                                                  double *__restrict__ pstate, double *__restrict__ out)
+                                                  double *__restrict__ pstate, double *__restrict__ out,
+                                                  const int32_t *__restrict__ prior_seg,
+                                                  const double *__restrict__ fwd, double *__restrict__ comb)
 {
     __shared__ double s_tab[kDawsonTab];
     const int lane = threadIdx.x;
@@ -1548,7 +1555,19 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
 #pragma unroll
         for (int k = 0; k < 16; ++k) rC[k] = C[k];
         ggp::reverse_state(rm, rC);
-        store20(out + (size_t)20 * r, rm, rC);                    // the prior, before the update
+        if (!COMB || out) store20(out + (size_t)20 * r, rm, rC);  // the prior, before the update
+        if constexpr (COMB) {   // k_combine<true> on this row
+            double mf[4], Cf[16];
+            const double *fr = fwd + (size_t)20 * r;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) mf[k] = fr[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) Cf[k] = fr[4 + k];
+            int sp = prior_seg[r];
+            if (sp < 0 || sp >= n_seg) sp = 0;
+            ggp::combine_info(mf, Cf, rm, rC, ptab + 11 * sp);
+            store20(comb + (size_t)20 * r, mf, Cf);
+        }
         const double *p = seg_params(F, ptab, n_seg, r);
         const double x0 = F.logl[r] - m[0];
         const double x1 = F.fp[r] - m[1];
@@ -2362,6 +2381,7 @@ struct Shard {
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
     bool combine_exact = false;                  // GGP_COMBINE_EXACT=1: k_combine with the oracle's operations
+    bool combine_fused = true;                   // GGP_COMBINE_FUSED=0: k_combine after the backward pass always
     int tune_pair_q = 0;                         // GGP_PAIR_Q: waves per cell (2, 4; 0 = by level size)
     bool smoother_lane = false;                  // GGP_SMOOTHER_LANE=1: the lane smoother on every level
     int kernel_used = GGP_KERNEL_LANE;
@@ -2663,9 +2683,24 @@ int shard_wait(Shard *s)
     return GGP_OK;
 }
 
+// whether every level of the smoother takes the lane kernels (no lane-pair level): the backward
+// pass can then form the combined rows itself (k_bwd_level<true>)
+bool smoother_all_lane(const Shard *f)
+{
+    if (f->smoother_lane) return true;
+    for (size_t L = 0; L + 1 < f->level_start.size(); ++L) {
+        const int64_t n = f->level_start[L + 1] - f->level_start[L];
+        if (n > 0 && n <= f->pair_max_cells) return false;
+    }
+    return true;
+}
+
 // forward then backward pass of the smoother (predictions.h:93-444) into device buffers; pstate
-// is left holding every cell's backward final state (MOMAdata::mean/cov after -p)
-hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd, double *d_bwd)
+// is left holding every cell's backward final state (MOMAdata::mean/cov after -p).  d_comb (only
+// when smoother_all_lane): the backward pass also forms the combined rows there, and d_bwd may
+// then be null (the backward rows not stored)
+hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pstate, double *d_fwd, double *d_bwd,
+                        double *d_comb = nullptr)
 {
     const int n_levels = (int)f->level_start.size() - 1;
     // a level up to pair_max_cells takes the lane-pair split (four waves per cell while one
@@ -2693,9 +2728,14 @@ hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pst
         if (fwd)
             hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
                                f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        else if (d_comb)
+            hipLaunchKernelGGL(k_bwd_level<true>, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab,
+                               n_seg, f->d_level_cells + a, n, cpw, d_pstate, d_bwd, f->d_prior_seg,
+                               (const double *)d_fwd, d_comb);
         else
-            hipLaunchKernelGGL(k_bwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd);
+            hipLaunchKernelGGL(k_bwd_level<false>, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab,
+                               n_seg, f->d_level_cells + a, n, cpw, d_pstate, d_bwd, (const int32_t *)nullptr,
+                               (const double *)nullptr, (double *)nullptr);
     };
     hipError_t e = hipMemsetAsync(d_pstate, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream);
     for (int L = 0; L < n_levels && e == hipSuccess; ++L) {        // forward: roots first
@@ -2878,6 +2918,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_PAIR_CPW")) f->tune_pair_cpw = atoi(e) == 32 ? 32 : 64;
     if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
     if (const char *e = getenv("GGP_COMBINE_EXACT")) f->combine_exact = atoi(e) != 0;
+    if (const char *e = getenv("GGP_COMBINE_FUSED")) f->combine_fused = atoi(e) != 0;
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
@@ -4320,9 +4361,14 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
             e = hipMemcpyAsync(s->d_sm_ptab, params, (size_t)n_seg * 11 * sizeof(double), hipMemcpyHostToDevice,
                                s->stream);
         if (e == hipSuccess) e = hipEventRecord(s->ev_pred[0], s->stream);
-        if (e == hipSuccess) e = run_smoother(s, s->d_sm_ptab, n_seg, s->d_sm_pstate, dv->sm_fwd, dv->sm_bwd);
+        // the combine fused into the backward pass where every level runs the lane smoother (C5-sized
+        // levels; the same rows bitwise), else k_combine after it
+        const bool fuse = s->combine_fused && !s->combine_exact && smoother_all_lane(s);
+        if (e == hipSuccess)
+            e = run_smoother(s, s->d_sm_ptab, n_seg, s->d_sm_pstate, dv->sm_fwd, fuse && !out_bwd ? nullptr : dv->sm_bwd,
+                             fuse ? s->d_sm_comb : nullptr);
         if (e == hipSuccess) e = hipEventRecord(s->ev_pred[1], s->stream);
-        if (e == hipSuccess) {
+        if (e == hipSuccess && !fuse) {
             const int64_t blocks = (s->n_rows + 255) / 256;
             auto *kc = s->combine_exact ? k_combine<false> : k_combine<true>;
             hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), 0, s->stream, s->d_sm_ptab, n_seg,

@@ -415,6 +415,34 @@ def test_predict_split_smoother_bitwise_lane(example_forests, which, monkeypatch
         assert np.array_equal(x, y), name
 
 
+@pytest.mark.parametrize("which", ["segments", "example"])
+def test_combine_fused_into_backward_pass_bitwise(example_forests, which, monkeypatch):
+    """with every level on the lane smoother the backward pass forms the combined rows itself
+    (k_bwd_level<true>); GGP_COMBINE_FUSED=0 runs k_combine after it: the same rows bitwise,
+    whether or not the backward rows are asked for (the fused pass then does not store them)"""
+    import gfp_gaussian_process_amd as g
+    if which == "segments":
+        hf = g.HostForest.synthetic(60, 40)
+        hf.a["segment"] = (hf.a["time"] >= np.median(hf.a["time"])).astype(np.int32)
+        P0 = np.array(CONFIGS[0][2])
+        P1 = P0.copy()
+        P1[0] *= 1.1
+        P1[7] *= 1.2
+        params = np.stack([P0, P1])
+    else:
+        hf, params = example_forests[("scaled", "binomial")], CONFIGS[0][2]
+    monkeypatch.setenv("GGP_SMOOTHER_LANE", "1")
+    fused = g.Forest(hf)
+    full = fused.predict(params)
+    comb_only = fused.predict(params, outputs=(False, False, True))[2]
+    rows = fused.predict_rows(0, hf.n_rows)
+    monkeypatch.setenv("GGP_COMBINE_FUSED", "0")
+    sep = g.Forest(hf).predict(params)
+    for name, x, y in zip(("forward", "backward", "combined"), full, sep):
+        assert np.array_equal(x, y), name
+    assert np.array_equal(comb_only, sep[2]) and np.array_equal(rows, sep[2])
+
+
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
 def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
     """k_combine's fast form (the default: reciprocal pivots, reassociated mean) against the

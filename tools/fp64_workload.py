@@ -31,6 +31,7 @@ for _ in range(3):
 out["pair"] = {"trees": 12500, "rows": hf.n_rows, "evals": 3}
 f.close()
 hf = g.HostForest.synthetic(125000, 500)                # bench.py predict
+os.environ["GGP_COMBINE_FUSED"] = "0"   # the smoother and the combine counted apart (the bench fuses them)
 f = g.Forest(hf)
 for _ in range(2):
     f.predict(P, outputs=(False, False, False))
