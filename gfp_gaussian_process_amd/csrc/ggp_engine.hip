@@ -486,8 +486,25 @@ __device__ unsigned long long g_cnt[4];
             g_tl[blockIdx.x * 8 + 7] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |  \
                                        ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32); \
     } while (0)
+// the hand-off to a second daughter: the parent's publish time by cell (g_tlc), and in the
+// daughter's block the time its wait saw the flag and its first step began (g_tlx[block][0..1])
+__device__ unsigned long long g_tlc[1 << 16];
+__device__ unsigned long long g_tlx[8192 * 2];
+#define GGP_TL_PUB(c)                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && (c) < (1 << 16))                            \
+            __hip_atomic_store(&g_tlc[(c)], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_AGENT);                                      \
+    } while (0)
+#define GGP_TL_SEEN(k)                                                                         \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8192)                          \
+            g_tlx[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime();                    \
+    } while (0)
 #else
 #define GGP_TL(k)
+#define GGP_TL_PUB(c)
+#define GGP_TL_SEEN(k)
 #define GGP_TL_HWID()
 #define GGP_TL_CNT_DECL
 #define GGP_TL_CNT(k, cond)
@@ -1166,6 +1183,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         if (CHAIN && carried_prev && !chain_broken &&
             ld_agent_i(cell_nan + (wdone - cell_done) + F.dfs_rank[c]) == kRowStall)
             chain_broken = true;
+        if (i == i_lo && wc >= 0) GGP_TL_SEEN(0);
         const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
         double dt = 0.0;
         bool pending;
@@ -1198,6 +1216,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         prev_last = r1 - 1;
         GGP_PSTAMP(3);
         if (i == i_lo) GGP_TL(3);
+        if (i == i_lo && ch.x >= 0) GGP_TL_SEEN(1);
         // the rows of the chunk [base, base + 64) go to LDS once (one coalesced load per lane)
         auto load_chunk = [&](const int64_t base) {
             const int64_t rr = base + lane;
@@ -1392,6 +1411,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
         if (publish) {
             __builtin_amdgcn_s_waitcnt(0);   // every lane's stores at the coherence point, then the flag
+            GGP_TL_PUB(c);
             if (lane == 0) __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         GGP_PSTAMP(7);

@@ -67,6 +67,32 @@ int main(int argc, char **argv)
             printf("  %-28s min %8.2f  p10 %8.2f  med %8.2f  p90 %8.2f  max %8.2f us\n", names[k], v[0], v[v.size() / 10],
                    v[v.size() / 2], v[v.size() * 9 / 10], v.back());
         }
+        // the hand-off to second daughters: the parent's publish -> the daughter's wait seeing it
+        // -> its first step (blocks whose first cell waited: g_tlx set this evaluation)
+        {
+            std::vector<unsigned long long> tlx((size_t)nb * 2), tlc(1 << 16);
+            (void)hipMemcpyFromSymbol(tlx.data(), HIP_SYMBOL(g_tlx), tlx.size() * 8);
+            (void)hipMemcpyFromSymbol(tlc.data(), HIP_SYMBOL(g_tlc), tlc.size() * 8);
+            std::vector<int32_t> pc((size_t)nb + 1), cells;
+            const Shard *sh = f->shards[0];
+            (void)hipMemcpy(pc.data(), sh->d_path_seq, pc.size() * 4, hipMemcpyDeviceToHost);
+            cells.resize((size_t)pc[nb]);
+            (void)hipMemcpy(cells.data(), sh->d_path_cells, cells.size() * 4, hipMemcpyDeviceToHost);
+            std::vector<double> g1, g2;
+            for (int b = 0; b < nb; ++b) {
+                const int c = cells[(size_t)pc[b]];
+                if (tlx[(size_t)b * 2] < t0 || tlx[(size_t)b * 2 + 1] < t0) continue;   // not a waiting block
+                const int p = d.parent[c];
+                if (p < 0 || p >= (1 << 16) || tlc[(size_t)p] < t0) continue;
+                g1.push_back(((long long)tlx[(size_t)b * 2] - (long long)tlc[(size_t)p]) / 100.0);
+                g2.push_back(((long long)tlx[(size_t)b * 2 + 1] - (long long)tlx[(size_t)b * 2]) / 100.0);
+            }
+            for (auto *v : {&g1, &g2}) std::sort(v->begin(), v->end());
+            if (!g1.empty())
+                printf("  hand-off (%zu second daughters): publish -> flag seen med %.2f p90 %.2f max %.2f us; "
+                       "flag seen -> first step med %.2f p90 %.2f max %.2f us\n", g1.size(), g1[g1.size() / 2],
+                       g1[g1.size() * 9 / 10], g1.back(), g2[g2.size() / 2], g2[g2.size() * 9 / 10], g2.back());
+        }
         // per block phase durations (median over blocks)
         const char *dn[6] = {"table", "lane setup", "to first step", "steps (all cells)", "stores", "reduction"};
         printf("  per-block durations (median):");
