@@ -139,6 +139,24 @@ def test_cli_prediction_text_is_the_rows_formatted(tmp_path, example_paths, orac
     assert n == hf.n_rows and body == want
 
 
+def test_cli_predict_binary_rows_fused_combine_identical(tmp_path, example_paths):
+    """-p -pbin on the example with every smoother level on the lane kernels (GGP_SMOOTHER_LANE=1:
+    the combine fused into the backward pass), with the separate combine (GGP_COMBINE_FUSED=0), and
+    with the default schedule (lane-pair levels, the separate combine): the same binary rows"""
+    pf = _param_file(tmp_path / "p.txt", {})
+    files = []
+    for tag, extra_env in (("fused", {"GGP_SMOOTHER_LANE": "1"}),
+                           ("sep", {"GGP_SMOOTHER_LANE": "1", "GGP_COMBINE_FUSED": "0"}), ("auto", {})):
+        env = dict(os.environ, **extra_env)
+        r = subprocess.run([CLI, "-i", example_paths["csv"], "-b", pf, "-c", example_paths["config"], "-p", "-pbin",
+                            "-o", str(tmp_path / tag)], capture_output=True, text=True, timeout=600, cwd=tmp_path,
+                           env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        files.append(open(tmp_path / tag / "input_f_b_prediction.bin", "rb").read())
+    assert files[0][:8] == b"GGPP0001" and len(files[0]) > 16
+    assert files[0] == files[1] == files[2]
+
+
 def test_cli_minimize_matches_oracle_trajectory(tmp_path, example_paths, oracle_example):
     """-m, log space, two free parameters: the GPU run's iteration log follows the same
     Nelder-Mead steps as the restatement driven by the oracle objective"""
