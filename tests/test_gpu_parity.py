@@ -387,6 +387,24 @@ def test_predict_segments_vs_oracle():
     _check_predict(hf, np.stack([P0, P1]))
 
 
+@pytest.mark.parametrize("lane_smoother", [False, True])
+def test_predict_four_segments_vs_oracle(lane_smoother, monkeypatch):
+    """four parameter segments by time quartile, every parameter of each moved: the default
+    schedule (lane-pair levels, k_combine after the backward pass) and the lane smoother with the
+    combine fused into the backward pass, both against the oracle"""
+    import gfp_gaussian_process_amd as g
+    if lane_smoother:
+        monkeypatch.setenv("GGP_SMOOTHER_LANE", "1")
+    hf = g.HostForest.synthetic(50, 60, seed=11)
+    t = hf.a["time"]
+    hf.a["segment"] = np.searchsorted(np.quantile(t, [0.25, 0.5, 0.75]), t, side="right").astype(np.int32)
+    assert set(np.unique(hf.a["segment"])) == {0, 1, 2, 3}
+    P0 = np.array(CONFIGS[0][2])
+    rng = np.random.default_rng(5)
+    params = np.stack([P0 * np.exp(rng.uniform(-0.1, 0.1, 11)) if k else P0 for k in range(4)])
+    _check_predict(hf, params)
+
+
 @pytest.mark.parametrize("which", ["example", "segments", "ragged", "wide"])
 def test_predict_split_smoother_bitwise_lane(example_forests, which, monkeypatch):
     """the smoother's levels on the lane-pair split (k_fwd_pair / k_bwd_pair, four or two waves
