@@ -145,6 +145,26 @@ def test_joints_synthetic_vs_oracle(noise, div):
     assert ig.tolist() == io.tolist()
 
 
+def test_joints_two_segments_vs_oracle():
+    """per-row parameters (two segments switching along time): the walks' conditionals and the
+    backward factors take each row's segment, as the oracle's"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(4, 40, seed=3)
+    t = hf.a["time"]
+    hf.a["segment"] = (t >= np.median(t)).astype(np.int32)
+    P1 = list(P)
+    P1[0] *= 1.1
+    P1[3] *= 0.95
+    P1[7] *= 1.2
+    params = np.stack([P, P1])
+    ig, vg = g.Forest(hf).joints(params, 1e-10)
+    io, vo = O.OracleForest(hf.a).joints(params, 1e-10)
+    err, _, n, worst = _compare(ig, vg, io, vo)
+    print(f"two segments: {n} pairs, max err {err:.2e}, worst event ratio {worst:.2f} tol")
+    assert n > 0 and err < 1e-6, (err, n)
+
+
 def test_joints_example_subset_vs_oracle(example_paths):
     """the reference's example, start rows in the first root cell and around a division.
     The example's joints are far less well conditioned than the synthetic forest's: the oracle
