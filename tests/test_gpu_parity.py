@@ -198,6 +198,43 @@ def test_rescaled_time_units(kernel):
     assert math.isfinite(vo) and _rel(vg, vo) < REL
 
 
+def _irregular_times(hf, seed):
+    """every cell sampled at irregular steps (0.3-2.5 time units apart), a daughter's first row
+    0.5-2 units after its parent's last: a different dt at almost every step"""
+    a = hf.a
+    rng = np.random.default_rng(seed)
+    ro, par = a["row_offset"], a["parent"]
+    t = np.zeros(len(a["time"]))
+    for c in range(len(par)):
+        r0, r1 = ro[c], ro[c + 1]
+        start = 0.0 if par[c] < 0 else t[ro[par[c] + 1] - 1] + rng.uniform(0.5, 2.0)
+        assert par[c] < c
+        t[r0:r1] = start + np.concatenate([[0.0], np.cumsum(rng.uniform(0.3, 2.5, r1 - r0 - 1))])
+    a["time"] = t
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_irregular_sampling_chain_vs_oracle(kernel):
+    """irregular time steps (no two steps share a dt: the wave schedule's dt cache misses, every
+    exp(s t) and product factor differs from step to step), three chained calls against the oracle"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(60, 40, seed=9)
+    _irregular_times(hf, 1)
+    P = CONFIGS[0][2]
+    fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
+    for call in range(3):
+        vg, vo = fg.total_likelihood(P), of.total_likelihood(P)[0]
+        assert math.isfinite(vo) and _rel(vg, vo) < REL, (call, vg, vo)
+
+
+def test_irregular_sampling_predict_vs_oracle():
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(30, 40, seed=4)
+    _irregular_times(hf, 2)
+    _check_predict(hf, CONFIGS[0][2])
+
+
 def test_empty_forest():
     import gfp_gaussian_process_amd as g
     a = dict(g.HostForest.synthetic(1, 8).a)
