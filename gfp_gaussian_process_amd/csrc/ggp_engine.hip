@@ -145,7 +145,12 @@ GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t
     bool divide = pending;
     double cl = 0.0;
     int nan_row = kNanNone;
+    double t_cur = F.time[r0];
     for (int64_t r = r0; r < r1; ++r) {
+        // this row's data and the next row's time, loaded before the propagation they would
+        // otherwise wait behind (the same values)
+        const double y_l = F.logl[r], y_f = F.fp[r];
+        const double t_next = r + 1 < r1 ? F.time[r + 1] : 0.0;
         if (pending) {   // mean_cov_model over dt (likelihood.h:97-101 / predictions.h:28-31)
             ggp::propagate_lane(m, C, dt, ou, s_tab);
             if (divide) {
@@ -153,8 +158,8 @@ GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t
                 divide = false;
             }
         }
-        const double x0 = F.logl[r] - m[0];
-        const double x1 = F.fp[r] - m[1];
+        const double x0 = y_l - m[0];
+        const double x1 = y_f - m[1];
         ggp_innov v;
         ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
         cl += ggp_ll_term(x0, x1, v, F.two_log_2pi);
@@ -164,7 +169,8 @@ GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t
         }
         ggp_posterior(m, C, x0, x1, v);
         pending = r + 1 < r1;
-        if (pending) dt = F.time[r + 1] - F.time[r];
+        if (pending) dt = t_next - t_cur;
+        t_cur = t_next;
     }
     double *st = state + (size_t)20 * c;
 #pragma unroll
@@ -1468,7 +1474,12 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
     // the OU constants (six divisions and a pow) are formed again only when the segment changes
     const double *ou_src = nullptr;
     ggp::OU ou{};
+    double t_cur = F.time[r0];
     for (int64_t r = r0; r < r1; ++r) {
+        // this row's data, parameters and the next row's time, loaded before the propagation
+        const double *p = seg_params(F, ptab, n_seg, r);
+        const double y_l = F.logl[r], y_f = F.fp[r], var_x = p[7], var_g = p[8];
+        const double t_next = r + 1 < r1 ? F.time[r + 1] : 0.0;
         if (pending) {
             if (pprop != ou_src) {
                 ou = ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]);
@@ -1480,15 +1491,15 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
                 divide = false;
             }
         }
-        const double *p = seg_params(F, ptab, n_seg, r);
-        const double x0 = F.logl[r] - m[0];
-        const double x1 = F.fp[r] - m[1];
+        const double x0 = y_l - m[0];
+        const double x1 = y_f - m[1];
         ggp_innov v;
-        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+        ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
         ggp_posterior(m, C, x0, x1, v);
         store20(out + (size_t)20 * r, m, C);
         pending = r + 1 < r1;
-        if (pending) dt = F.time[r + 1] - F.time[r];
+        if (pending) dt = t_next - t_cur;
+        t_cur = t_next;
         pprop = p;   // the step t -> t+1 uses row t's parameters (:143-146)
     }
     store20(pstate + (size_t)20 * c, m, C);
@@ -1562,6 +1573,17 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
     const double *ou_src = nullptr;   // as k_fwd_level: the OU constants per segment change only
     ggp::OU ou{};
     for (int64_t r = r1 - 1; r >= r0; --r) {
+        // this row's data and parameters, the previous row's time and parameters, and (fused) the
+        // row's prior segment, loaded before the propagation they would otherwise wait behind
+        const double *p = seg_params(F, ptab, n_seg, r);
+        const double y_l = F.logl[r], y_f = F.fp[r], var_x = p[7], var_g = p[8];
+        const double t_r = F.time[r], t_prev = r > r0 ? F.time[r - 1] : 0.0;
+        const double *q_next = r > r0 ? seg_params(F, ptab, n_seg, r - 1) : pq;
+        int sp = 0;
+        if constexpr (COMB) {
+            sp = prior_seg[r];
+            if (sp < 0 || sp >= n_seg) sp = 0;
+        }
         if (pend) {
             if (pq != ou_src) {
                 ou = ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]);
@@ -1583,21 +1605,18 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
             for (int k = 0; k < 4; ++k) mf[k] = fr[k];
 #pragma unroll
             for (int k = 0; k < 16; ++k) Cf[k] = fr[4 + k];
-            int sp = prior_seg[r];
-            if (sp < 0 || sp >= n_seg) sp = 0;
             ggp::combine_info(mf, Cf, rm, rC, ptab + 11 * sp);
             store20(comb + (size_t)20 * r, mf, Cf);
         }
-        const double *p = seg_params(F, ptab, n_seg, r);
-        const double x0 = F.logl[r] - m[0];
-        const double x1 = F.fp[r] - m[1];
+        const double x0 = y_l - m[0];
+        const double x1 = y_f - m[1];
         ggp_innov v;
-        ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
+        ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
         ggp_posterior(m, C, x0, x1, v);
         pend = r > r0;
         if (pend) {
-            pq = seg_params(F, ptab, n_seg, r - 1);
-            dtp = F.time[r] - F.time[r - 1];
+            pq = q_next;
+            dtp = t_r - t_prev;
         }
     }
     store20(pstate + (size_t)20 * c, m, C);
