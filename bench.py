@@ -196,6 +196,52 @@ def inprocess_child(argv) -> int:
     return 0
 
 
+def example_parity(kernels=("auto", "lane")) -> dict:
+    """North star's parity config: the example's total log-likelihood against the CPU oracle.  The
+    five committed configurations x three chained calls (tests/golden/oracle_example.json, the oracle
+    on its own Dawson table) and the same chains with the reference's own Faddeeva::Dawson
+    (oracle_example_refdawson.json); worst relative distance per schedule, on the engine this
+    process loaded (_native.engine_name())"""
+    import gzip
+    import shutil
+    import tempfile
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd import _native as N
+    gold = os.path.join(ROOT, "tests", "golden")
+    own = json.load(open(os.path.join(gold, "oracle_example.json")))
+    ref = json.load(open(os.path.join(gold, "oracle_example_refdawson.json")))
+    tmp = tempfile.mkdtemp()
+    csv = os.path.join(tmp, "input.csv")
+    with gzip.open(os.path.join(gold, "example_input.csv.gz"), "rb") as fi, open(csv, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    out = {"engine": N.engine_name(), "calls": 3 * len(own), "bar": 1e-9}
+    for kern in kernels:
+        w_own = w_ref = 0.0
+        for key, v in own.items():
+            noise, div = key.split("/")[:2]
+            hf = g.HostForest.from_csv(csv, os.path.join(gold, "example_csv_config.txt"), -1, noise, div)
+            f = g.Forest(hf, kernel=kern)
+            p = [float.fromhex(x) for x in v["params"]]
+            ll = np.array([f.total_likelihood(p) for _ in range(3)])
+            f.close()
+            a = np.array([float.fromhex(x) for x in v["ll"]])
+            b = np.array([float.fromhex(x) for x in ref[key]["ll"]])
+            w_own = max(w_own, float(np.max(np.abs(ll - a) / np.abs(a))))
+            w_ref = max(w_ref, float(np.max(np.abs(ll - b) / np.abs(b))))
+        out[kern] = {"rel_vs_oracle": w_own, "rel_vs_refdawson": w_ref}
+    shutil.rmtree(tmp)
+    return out
+
+
+def example_parity_child() -> int:
+    """`bench.py --example-parity-child`: example_parity in a process of its own (the engine named by
+    GGP_ENGINE_LIB, e.g. the exact-arithmetic libggp_exact.so); prints one JSON line"""
+    from gfp_gaussian_process_amd import _native as N
+    kern = ("auto", "lane", "pair") if "exact" in N.engine_name() else ("auto", "lane")
+    print(json.dumps(example_parity(kern)))
+    return 0
+
+
 def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: bool = False, note: str = ""):
     """FP64 and VALU-issue fractions of a bench leg from the PMC pass of this build
     (profiles/fp64_counts.json, tools/fp64_summary.py kind `kind`): achieved FP64 = flops per row x
@@ -222,6 +268,8 @@ def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: boo
 def main() -> int:
     if len(sys.argv) > 1 and sys.argv[1] == "--inprocess-child":
         return inprocess_child(sys.argv[2:])
+    if len(sys.argv) > 1 and sys.argv[1] == "--example-parity-child":
+        return example_parity_child()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -251,6 +299,22 @@ def main() -> int:
                          "multi-rank path on one GPU, the per-call 16 B through host memory)")
     ap.add_argument("--device", type=int, default=None,
                     help="HIP ordinal of this rank (default LOCAL_RANK; rehearsal: several ranks on one GPU)")
+    ap.add_argument("--c4-trees", type=int, default=100000,
+                    help="strong-scaling leg: BASELINE configs[3]'s forest (trees x --rows) split over the N ranks, "
+                         "one evaluation per step plus the -s scan (0 = skip)")
+    ap.add_argument("--c4-steps", type=int, default=20, help="evaluations timed in the C4 leg")
+    ap.add_argument("--c4-scan", type=int, default=61, help="samples of the C4 leg's chained -s scan (0 = skip)")
+    ap.add_argument("--c5-trees", type=int, default=1000000,
+                    help="strong-scaling leg: BASELINE configs[4]'s -p on this many trees x --predict-rows split "
+                         "over the N ranks (0 = skip)")
+    ap.add_argument("--c5-chunk-rows", type=int, default=62500000,
+                    help="rows per shard of the C5 leg's handle (a rank's share above it is smoothed in chunks)")
+    ap.add_argument("--engine-comm-leg", type=int, default=1,
+                    help="N > 1 with nccl: also time the C4 leg with the engine's own RCCL all-gather "
+                         "(ggp_comm_attach), after the headline; a failure is reported in the line (0 = skip)")
+    ap.add_argument("--example-parity", type=int, default=1,
+                    help="N = 1: the example's 15 totals against the committed oracle fixtures, on this engine "
+                         "and on the exact-arithmetic engine (libggp_exact.so, a child process) (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -567,6 +631,131 @@ def main() -> int:
                        "the GPU and copied to the host (72 doubles each), parameter tables cached per parameters"}
         fj.close()
 
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---- strong scaling, BASELINE configs[3] (C4): ONE forest of --c4-trees x --rows split over the
+    # N ranks by whole trees (contiguous blocks: every tree has the same rows, so this is the LPT
+    # split), the init statistics of the whole forest on every rank (one all_reduce at setup); one
+    # evaluation per step with one all_gather of the partials; then the chained -s scan
+    # (main.cpp:77-112) -- every rank chains its shard, one all_gather of the per-sample partials ----
+    c4s = None
+    if args.c4_trees > 0:
+        from gfp_gaussian_process_amd.distributed import global_init_stats
+        from gfp_gaussian_process_amd.optimize import arange
+        T4 = args.c4_trees
+        lo4, hi4 = rank * T4 // world, (rank + 1) * T4 // world
+        h4 = g.HostForest.synthetic(hi4 - lo4, args.rows, seed=SEED, first_tree=3 * 10 ** 6 + lo4)
+        if world > 1:
+            global_init_stats(h4)
+        f4 = g.Forest(h4, device=local, kernel=args.kernel)
+        o4 = ShardedObjective(f4)
+        for _ in range(3):
+            o4.total_likelihood(P_EXAMPLE)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.c4_steps):
+            ll4 = o4.total_likelihood(P_EXAMPLE)
+        barrier()
+        el4 = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
+        rows4 = torch.tensor([h4.n_rows], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(rows4)
+        rows4 = int(rows4.item())
+        c4s = {"config": f"BASELINE configs[3] (C4): {T4} trees x {args.rows} tp, one forest split over "
+                         f"{world} rank(s) by whole trees; the init statistics of the whole forest",
+               "trees": T4, "rows": rows4, "trees_per_rank": hi4 - lo4, "steps": args.c4_steps,
+               "ms_per_eval": 1e3 * el4, "updates_per_s": rows4 / el4, "scaling": "strong",
+               "total_log_likelihood": ll4, "levels": f4.info()["levels"],
+               "collective": {"kind": "torch all_gather_into_tensor of 16 B per rank, rank-order sum",
+                              "backend": args.backend if world > 1 else None,
+                              "ranks": dist.get_world_size() if world > 1 else 1}}
+        if args.c4_scan > 0:
+            P4 = np.array(P_EXAMPLE)
+            samples = arange(1.0e-03, 8.0e-02, (8.0e-02 - 1.0e-03) / args.c4_scan)[: args.c4_scan]
+            pts = np.repeat(P4[None, :], len(samples), axis=0)
+            pts[:, 1] = samples
+            f4.reset_state()
+            barrier()
+            t1 = time.perf_counter()
+            scan = o4.total_likelihood_chain(pts)
+            barrier()
+            sel4 = max_over_ranks(time.perf_counter() - t1)
+            c4s["scan"] = {"parameter": "gamma_lambda", "samples": len(samples), "seconds": sel4,
+                           "updates_per_s": len(samples) * rows4 / sel4, "first": float(scan[0]),
+                           "last": float(scan[-1]),
+                           "note": "-s: each sample from the carried state the previous left; every rank "
+                                   "chains its trees (ggp_total_loglik_chain), one all_gather of the partials"}
+        f4.close()
+        if world > 1 and args.backend == "nccl" and args.engine_comm_leg:
+            # the engine's own RCCL path (include/ggp.h ggp_comm_attach), after the headline and the
+            # torch leg; a wait inside it is bounded by GGP_COMM_TIMEOUT_S and reported, not raised
+            os.environ.setdefault("GGP_COMM_TIMEOUT_S", "60")
+            eng = {}
+            try:
+                fe = g.Forest(h4, device=local, kernel=args.kernel)
+                oe = ShardedObjective(fe, engine_comm=True)
+                if not oe.engine:
+                    eng["error"] = "the engine's RCCL path was unavailable on some rank (torch's path kept)"
+                else:
+                    eng["rccl_comm_count"] = fe.comm_size()
+                    for _ in range(3):
+                        oe.total_likelihood(P_EXAMPLE)
+                    barrier()
+                    t1 = time.perf_counter()
+                    for _ in range(args.c4_steps):
+                        lle = oe.total_likelihood(P_EXAMPLE)
+                    barrier()
+                    ele = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
+                    eng.update({"ms_per_eval": 1e3 * ele, "updates_per_s": rows4 / ele,
+                                "total_log_likelihood": lle, "same_total_as_torch_path": lle == ll4})
+                fe.close()
+            except Exception as e:   # reported in the line: the headline stands either way
+                eng["error"] = repr(e)[-400:]
+            eng["kind"] = "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
+            c4s["engine_rccl"] = eng
+        del h4
+
+    # ---- strong scaling, BASELINE configs[4] (C5): -p over ONE forest of --c5-trees x --predict-rows
+    # split over the N ranks (no collective on the data path: every rank smooths its trees, the rows
+    # stay in HBM); a rank's share above --c5-chunk-rows is smoothed in chunks through one workspace ----
+    c5s = None
+    if args.c5_trees > 0:
+        from gfp_gaussian_process_amd.distributed import global_init_stats
+        T5 = args.c5_trees
+        lo5, hi5 = rank * T5 // world, (rank + 1) * T5 // world
+        t1 = time.perf_counter()
+        h5 = g.HostForest.synthetic(hi5 - lo5, args.predict_rows, seed=SEED, first_tree=4 * 10 ** 6 + lo5)
+        if world > 1:
+            global_init_stats(h5)
+        synth5 = time.perf_counter() - t1
+        chunk = args.c5_chunk_rows if h5.n_rows > args.c5_chunk_rows else 0
+        f5 = g.Forest(h5, device=local, max_shard_rows=chunk)
+        nsh5 = len(f5.shards())
+        f5.predict(P_EXAMPLE, outputs=(False, False, False))    # warm-up + workspace
+        barrier()
+        t1 = time.perf_counter()
+        reps5 = 2
+        for _ in range(reps5):
+            f5.predict(P_EXAMPLE, outputs=(False, False, False))
+        barrier()
+        el5 = max_over_ranks((time.perf_counter() - t1) / reps5)
+        rows5 = torch.tensor([h5.n_rows], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(rows5)
+        rows5 = int(rows5.item())
+        c5s = {"config": f"BASELINE configs[4] (C5) -p: {T5} trees x {args.predict_rows} tp, one forest split over "
+                         f"{world} rank(s) by whole trees, forward + backward + combine, rows resident in HBM",
+               "trees": T5, "rows": rows5, "trees_per_rank": hi5 - lo5, "shards_per_rank": nsh5,
+               "chunk_rows": chunk, "ms_per_predict": 1e3 * el5, "rows_per_s": rows5 / el5, "scaling": "strong",
+               "synth_s_rank0": synth5}
+        f5.close()
+        del h5
+
     exmp = None
     if world == 1 and args.example_mp:
         exmp = example_mp(os.path.join("/tmp", f"ggp_example_mp_{os.getpid()}"), 3.0 if not args.no_cpu else 0.5)
@@ -625,6 +814,25 @@ def main() -> int:
             result["joints_c5_subset"] = jc5
         if inproc is not None:
             result["inprocess"] = inproc
+        if c4s is not None:
+            result["c4_strong"] = c4s
+        if c5s is not None:
+            result["c5_predict_split"] = c5s
+        if world == 1 and args.example_parity:
+            try:
+                result["example_parity"] = {"default_engine": example_parity(("auto", "lane"))}
+            except Exception as e:
+                result["example_parity"] = {"default_engine": {"error": repr(e)[-300:]}}
+            import subprocess
+            envx = dict(os.environ, GGP_ENGINE_LIB="libggp_exact.so")
+            try:
+                r = subprocess.run([sys.executable, os.path.abspath(__file__), "--example-parity-child"],
+                                   capture_output=True, text=True, timeout=600, env=envx)
+                result["example_parity"]["exact_engine"] = (json.loads(r.stdout.strip().splitlines()[-1])
+                                                            if r.returncode == 0 else
+                                                            {"error": (r.stdout + r.stderr)[-400:]})
+            except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+                result["example_parity"]["exact_engine"] = {"error": repr(e)[-300:]}
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

@@ -88,6 +88,7 @@ ENGINE_SYMBOLS = {
     "ggp_comm_attach": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_char_p]),
     "ggp_comm_nan_rank": (ctypes.c_int32, [ctypes.c_void_p]),
+    "ggp_comm_size": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_comm_local_nan": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),
     "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -177,11 +178,22 @@ def _one_hip_runtime() -> None:
             return
 
 
-def engine():
-    """libggp.so (HIP, gfx950)."""
-    if "libggp.so" not in _cache:
+def engine_name() -> str:
+    """the engine library's file name: libggp.so, or GGP_ENGINE_LIB (A/B builds such as
+    lib/libggp_exact.so, the GGP_EXACT arithmetic)"""
+    return os.environ.get("GGP_ENGINE_LIB", "libggp.so")
+
+
+EXACT_ENGINE = "libggp_exact.so"
+
+
+def engine(name: str | None = None):
+    """libggp.so (HIP, gfx950), or the engine library `name` (EXACT_ENGINE: the same C-ABI in the
+    oracle's arithmetic)."""
+    name = name or engine_name()
+    if name not in _cache:
         _one_hip_runtime()
-    return _load("libggp.so", ENGINE_SYMBOLS)
+    return _load(name, ENGINE_SYMBOLS)
 
 
 def host():

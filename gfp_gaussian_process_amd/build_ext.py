@@ -1,8 +1,10 @@
 """Compile the native libraries in-tree (no JIT cache, no pip install).
 
   lib/libggp.so       HIP engine for gfx950 (hipcc --offload-arch=gfx950)   include/ggp.h
+  lib/libggp_exact.so the same engine in the oracle's arithmetic (GGP_EXACT)  include/ggp.h
   lib/libggp_host.so  host ingest, plain C++17 (g++)                        include/ggp_host.h
   lib/ggp             C++ CLI mirroring the reference's main.cpp modes
+  lib/ggp_exact       the same CLI on libggp_exact.so
 
 ``python -m gfp_gaussian_process_amd.build_ext`` or ``__graft_entry__.build()``.
 """
@@ -51,7 +53,7 @@ def build(verbose: bool = False, force: bool = False) -> dict:
     # --- device engine ---
     eng_src = os.path.join(CSRC, "ggp_engine.hip")
     eng_deps = [eng_src, os.path.join(CSRC, "ggp_device.h"), os.path.join(CSRC, "dawson_table.inc"),
-                os.path.join(INC, "ggp.h")]
+                os.path.join(CSRC, "exp_table.inc"), os.path.join(INC, "ggp.h")]
     for extra in ("ggp_prop.h", "ggp_group.h", "ggp_predict.h", "ggp_joints.h", "ggp_outtab.h",
                   "ggp_out_tables.inc", "ggp_wave.h"):
         p = os.path.join(CSRC, extra)
@@ -65,6 +67,13 @@ def build(verbose: bool = False, force: bool = False) -> dict:
         _run([HIPCC, *HIP_FLAGS, "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src, "-ldl"],
              verbose)
     out["libggp"] = eng
+    # the same engine in the oracle's arithmetic (-DGGP_EXACT: glibc's exp, no products, no fma
+    # contraction; DESIGN.md §2 "Exact arithmetic"), selected with GGP_ENGINE_LIB=libggp_exact.so
+    eng_x = os.path.join(LIB, "libggp_exact.so")
+    if force or not _newer(eng_x, eng_deps):
+        _run([HIPCC, *HIP_FLAGS, "-DGGP_EXACT", "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng_x,
+              eng_src, "-ldl"], verbose)
+    out["libggp_exact"] = eng_x
     # --- host ingest ---
     host_src = os.path.join(CSRC, "host", "ggp_host.cpp")
     host = os.path.join(LIB, "libggp_host.so")
@@ -87,6 +96,12 @@ def build(verbose: bool = False, force: bool = False) -> dict:
             _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", "-o", cli, cli_src, host_src,
                   f"-L{LIB}", "-lggp", "-Wl,-rpath,$ORIGIN", "-lpthread"], verbose)
         out["cli"] = cli
+        # the same CLI on the exact-arithmetic engine (every output in the oracle's arithmetic)
+        cli_x = os.path.join(LIB, "ggp_exact")
+        if force or not _newer(cli_x, deps + [eng_x]):
+            _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", "-o", cli_x, cli_src, host_src,
+                  f"-L{LIB}", "-l:libggp_exact.so", "-Wl,-rpath,$ORIGIN", "-lpthread"], verbose)
+        out["cli_exact"] = cli_x
     return out
 
 

@@ -38,8 +38,9 @@ using std::min;
 // fused across statements).  What fuses is decided by the expression alone, so the lane, group,
 // lane-pair, batch and smoother kernels, which all run these bodies, stay bitwise equal to one
 // another.  The wave schedule (ggp_wave.h) and the oracle keep their own forms.  -DGGP_NO_CONTRACT
-// builds the uncontracted bodies (A/B, DESIGN.md "Parity").
-#if defined(GGP_HOST_SIM) || defined(GGP_NO_CONTRACT)
+// builds the uncontracted bodies (A/B, DESIGN.md "Parity").  A host simulation built by clang
+// with -DGGP_HOST_CONTRACT -mfma contracts exactly as the device does (tools/parity_attrib.cpp).
+#if defined(GGP_NO_CONTRACT) || defined(GGP_EXACT) || (defined(GGP_HOST_SIM) && !defined(GGP_HOST_CONTRACT))
 #define GGP_CONTRACT
 #else
 #define GGP_CONTRACT _Pragma("clang fp contract(on)")
@@ -90,8 +91,16 @@ GGP_DEV double ggp_w_im_abs(double ax, const double *tab)
     return ax > 45.0 ? cf : (y100 >= (double)GGP_DAWSON_NINT ? taylor : poly);
 }
 
+#ifdef GGP_HOST_SIM
+// diagnostic hook (tools/parity_attrib.cpp): every Dawson value from another implementation
+extern double (*ggp_hs_dawson)(double);
+#endif
+
 GGP_DEV double ggp_dawson_tab(double x, const double *tab)
 {
+#ifdef GGP_HOST_SIM
+    if (ggp_hs_dawson) return ggp_hs_dawson(x);
+#endif
     if (x != x) return x;
     const double w = ggp_w_im_abs(fabs(x), tab);
     return GGP_SPI2 * (x < 0.0 ? -w : w);

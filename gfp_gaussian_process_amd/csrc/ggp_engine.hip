@@ -38,7 +38,11 @@
 #include "ggp_predict.h"
 #include "ggp_joints.h"
 
-#define GGP_VERSION "ggp-mi355x 0.1.0 (reference gfp_gaussian_process 0.4.2)"
+#ifdef GGP_EXACT
+#define GGP_VERSION "ggp-mi355x 0.2.0 exact arithmetic (reference gfp_gaussian_process 0.4.2)"
+#else
+#define GGP_VERSION "ggp-mi355x 0.2.0 (reference gfp_gaussian_process 0.4.2)"
+#endif
 
 namespace {
 
@@ -66,7 +70,8 @@ constexpr int kNanNone = 0x7fffffff;
 // L2 round trip per coefficient from constant memory).  Every lane issues all its global loads
 // before the first LDS store (one memory latency per launch, not one per 64 coefficients:
 // the loop form waited for each load, ~8 us of a level launch's fixed cost).
-constexpr int kDawsonTab = GGP_DAWSON_NINT * GGP_DAWSON_NCOEF;
+// (GGP_EXACT: the same array continues with glibc's exp table, ggp_prop.h kPropTabN)
+constexpr int kDawsonTab = ggp::kExact ? ggp::kPropTabN : ggp::kDawsonTabN;
 template <int N, class SRC>
 GGP_DEV void lds_fill(double *dst, const int lane, const SRC &src)
 {
@@ -81,7 +86,7 @@ GGP_DEV void lds_fill(double *dst, const int lane, const SRC &src)
 
 GGP_DEV void load_dawson_table(double *s_tab, int lane)
 {
-    lds_fill<kDawsonTab>(s_tab, lane, [](const int k) { return ggp_dawson_coef[k]; });
+    lds_fill<kDawsonTab>(s_tab, lane, [](const int k) { return ggp::prop_tab_entry(k); });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -233,9 +238,9 @@ constexpr int kOSlots = 10;
 constexpr int kParts[2][4] = {{1 | 2, 4 | 8, 0, 0}, {1, 2, 4, 8}};
 
 template <int OFF, size_t... J>
-GGP_DEV void exps(const ggp::Step &S, double *Xc, std::index_sequence<J...> seq)
+GGP_DEV void exps(const ggp::Step &S, double *Xc, const double *tab, std::index_sequence<J...> seq, bool &cold)
 {
-    ggp::lane_exps_flagged<OFF>(S, Xc, seq);   // the lane schedule's computed exponentials (ggp_prop.h), OFF + J
+    ggp::lane_exps_flagged<OFF>(S, Xc, tab, seq, cold);   // the lane schedule's computed exponentials (ggp_prop.h), OFF + J
 }
 template <int OFF, size_t... J>
 GGP_DEV void dawsons(const ggp::Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
@@ -278,13 +283,25 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
     ggp::Step S;
     ggp::step_init(S, m, C, t, P);
     double Xc[ggp::NXC], X[ggp::NXE], Dw[ggp::ND];
-    exps<X0>(S, Xc, std::make_index_sequence<XN>{});
+    bool cold = false;   // GGP_EXACT: an exponential argument outside exp_glibc's main path
+    exps<X0>(S, Xc, tab, std::make_index_sequence<XN>{}, cold);
     dawsons<D0>(S, Dw, tab, std::make_index_sequence<DN>{});
     const bool own = lane < CPW;   // lanes past CPW hold no cell and store nothing
     const int ln = own ? lane : 0;
     if (own) {
         put_part<ggp::NXC, W, Q, CPW>(Xc, Xl, lane);
         put_part<ggp::ND, W, Q, CPW>(Dw, Dl, lane);
+    }
+    if constexpr (ggp::kExact) {
+        if (__builtin_expect(own && cold, 0)) {   // an argument of this wave's share outside exp_glibc's
+            // main path: the share again through exp_glibc's special paths, one rolled loop (one copy of
+            // the code) into the LDS slots, and this wave's registers back from them
+            for (int k = X0; k < X0 + XN; ++k)
+                Xl[k * CPW + lane] = ggp::exp_glibc(ggp::exp_arg_body(S, ggp::unpack_x(ggp::kXCPacked.w[k])),
+                                                    ggp::exp_tab_of(tab));
+#pragma unroll
+            for (int j = X0; j < X0 + XN; ++j) Xc[j] = Xl[j * CPW + lane];
+        }
     }
     __syncthreads();
     get_rest<ggp::NXC, W, Q, CPW>(Xc, Xl, ln);
@@ -584,7 +601,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 {
     constexpr int CPW = 64 / G;
     constexpr int NXB = (ggp::NXC + G - 1) / G;   // computed exponentials per lane
-    constexpr int NPB = (ggp::NXP + G - 1) / G;   // product exponentials per lane
+    constexpr int NPB = ggp::NXPU ? (ggp::NXPU + G - 1) / G : 1;   // product exponentials per lane
     constexpr int NDB = (ggp::ND + G - 1) / G;    // Dawson slots per lane
     constexpr int NCB = (ggp::NI + G - 1) / G;    // integral slots per lane
     __shared__ double lds[CPW * kSlot];
@@ -614,7 +631,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
 #pragma unroll
     for (int q = 0; q < NPB; ++q) {
         const int j = lg + q * G;
-        const ggp::XProd d = ggp::kXP[j < ggp::NXP ? j : 0];
+        const ggp::XProd d = ggp::kXP[j < ggp::NXPU ? j : 0];
         pd[q] = d.j | d.rep << 8 | (uint32_t)d.fac << 16;
     }
 #pragma unroll
@@ -671,7 +688,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         if (prop) {
             double ev[NXB], dv[NDB];
 #pragma unroll
-            for (int q = 0; q < NXB; ++q) ev[q] = ggp::exp_body(S, ggp::unpack_x(xd[q]));
+            for (int q = 0; q < NXB; ++q) ev[q] = ggp::exp_body(S, ggp::unpack_x(xd[q]), s_tab);
 #pragma unroll
             for (int q = 0; q < NDB; ++q) dv[q] = ggp::dawson_body(S, ggp::unpack_d(dd[q]), s_tab);
             const double pw = ggp::pow_task(S, lg < 3 ? lg : 0);
@@ -691,7 +708,7 @@ __global__ __launch_bounds__(64) void k_loglik_group(DevForest F, ggp_params P,
         if (prop) {   // the product exponentials (ggp_prop.h kXP), from the computed ones
 #pragma unroll
             for (int q = 0; q < NPB; ++q)
-                if (lg + q * G < ggp::NXP) Xl[pd[q] & 0xff] = Xl[pd[q] >> 8 & 0xff] * Xl[pd[q] >> 16];
+                if (lg + q * G < ggp::NXPU) Xl[pd[q] & 0xff] = Xl[pd[q] >> 8 & 0xff] * Xl[pd[q] >> 16];
         }
         __syncthreads();
         GGP_STAMP(3);
@@ -2413,13 +2430,15 @@ struct Shard {
     int64_t n_cells = 0, n_rows = 0;
     int n_cu = 256;
     int kernel_pref = GGP_KERNEL_AUTO;
-    int auto_small = GGP_KERNEL_WAVE;   // auto's schedule for small levels
+    // auto's schedule for small levels; the GGP_EXACT engine has no wave schedule (its table-driven
+    // outputs sum in another order than the reference expressions): the group schedule there
+    int auto_small = ggp::kExact ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     int64_t wave_max_cells = 5120;    // auto: wave schedule for levels up to this size
     int64_t group_max_cells = 8192;   // auto with GGP_AUTO_SMALL=group: group schedule above that
     int64_t pair_max_cells = 32768;   // auto: lane-pair schedule above that, up to this size
     int tune_lane_cpw = 0, tune_group_cpw = 0;   // GGP_LANE_CPW / GGP_GROUP_CPW (tuning only)
     int tune_pair_cpw = 64;                      // GGP_PAIR_CPW: cells per lane-pair workgroup (32, 64)
-    bool combine_exact = false;                  // GGP_COMBINE_EXACT=1: k_combine with the oracle's operations
+    bool combine_exact = ggp::kExact;            // GGP_COMBINE_EXACT=1: k_combine with the oracle's operations
     bool combine_fused = true;                   // GGP_COMBINE_FUSED=0: k_combine after the backward pass always
     int tune_pair_q = 0;                         // GGP_PAIR_Q: waves per cell (2, 4; 0 = by level size)
     bool smoother_lane = false;                  // GGP_SMOOTHER_LANE=1: the lane smoother on every level
@@ -2519,6 +2538,7 @@ struct RcclApi {
     int (*all_gather)(const void *, void *, size_t, int, void *, hipStream_t) = nullptr;
     int (*comm_destroy)(void *) = nullptr;
     int (*comm_abort)(void *) = nullptr;   // ncclCommAbort (optional)
+    int (*comm_count)(const void *, int *) = nullptr;   // ncclCommCount (optional)
     const char *(*error_string)(int) = nullptr;
 };
 constexpr int kRcclUint8 = 1;   // ncclUint8 (rccl.h ncclDataType_t)
@@ -2960,7 +2980,8 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_COMBINE_FUSED")) f->combine_fused = atoi(e) != 0;
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
-    if (const char *e = getenv("GGP_AUTO_SMALL")) f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
+    if (const char *e = getenv("GGP_AUTO_SMALL"); e && !ggp::kExact)
+        f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);
     if (hipSetDevice(f->device) != hipSuccess) {
@@ -3415,6 +3436,7 @@ static int rccl_load(const char *path, RcclApi &a)
     a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(a.lib, "ncclCommDestroy"));
     a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(a.lib, "ncclGetErrorString"));
     a.comm_abort = reinterpret_cast<decltype(a.comm_abort)>(dlsym(a.lib, "ncclCommAbort"));
+    a.comm_count = reinterpret_cast<decltype(a.comm_count)>(dlsym(a.lib, "ncclCommCount"));
     if (!a.get_unique_id || !a.comm_init_rank || !a.all_gather || !a.comm_destroy) {
         g_last_err = std::string(lib) + " lacks the RCCL entry points";
         return GGP_EDEV;
@@ -3494,6 +3516,14 @@ int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t
     return GGP_OK;
 }
 
+int32_t ggp_comm_size(const ggp_forest *f)
+{
+    if (!f || !f->comm || !f->comm->nc) return 0;
+    int n = 0;
+    if (f->comm->api.comm_count && f->comm->api.comm_count(f->comm->nc, &n) == 0) return n;
+    return -1;
+}
+
 int32_t ggp_comm_nan_rank(const ggp_forest *f)
 {
     return f && f->comm ? f->comm->last_nan_rank : -1;
@@ -3546,6 +3576,10 @@ int ggp_forest_create(const ggp_forest_desc *d, ggp_forest **out)
     *out = nullptr;
     if (d->kernel < GGP_KERNEL_AUTO || d->kernel > GGP_KERNEL_PAIR) {
         g_last_err = "ggp_forest_create: unknown kernel policy";
+        return GGP_EINVAL;
+    }
+    if (ggp::kExact && d->kernel == GGP_KERNEL_WAVE) {
+        g_last_err = "ggp_forest_create: the exact-arithmetic engine (libggp_exact.so) has no wave schedule";
         return GGP_EINVAL;
     }
     std::vector<int32_t> depth, dfs;

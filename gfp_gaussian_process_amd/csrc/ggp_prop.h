@@ -21,7 +21,52 @@
 
 #include "ggp_device.h"
 
+#ifndef GGP_EXP_TABLE_DEFINED
+#define GGP_EXP_TABLE_DEFINED
+#ifdef GGP_HOST_SIM
+#define GGP_EXP_TABLE_QUALIFIER static const
+#else
+#define GGP_EXP_TABLE_QUALIFIER static __constant__ const
+#endif
+#include "exp_table.inc"
+#endif
+
 namespace ggp {
+
+// GGP_EXACT: the propagator in the oracle's arithmetic, step for step (DESIGN.md §2 "Exact
+// arithmetic"): glibc's exp (exp_glibc), every one of the 74 exponentials computed from its own
+// argument (no products), no fma contraction.  The default build keeps the fast forms.
+#ifdef GGP_EXACT
+constexpr bool kExact = true;
+#else
+constexpr bool kExact = false;
+#endif
+
+// the propagator's LDS table: the Dawson coefficients (GGP_DAWSON_NINT x NCOEF doubles), one pad
+// double, then glibc's exp table (2^(k/128), 256 64-bit words, 16-byte aligned)
+constexpr int kDawsonTabN = GGP_DAWSON_NINT * GGP_DAWSON_NCOEF;
+constexpr int kExpTabOff = (kDawsonTabN + 1) & ~1;
+constexpr int kPropTabN = kExpTabOff + GGP_EXP_TAB_N;
+static_assert(kExpTabOff % 2 == 0, "16-byte aligned exp table rows");
+GGP_DEV const uint64_t *exp_tab_of(const double *tab) { return reinterpret_cast<const uint64_t *>(tab + kExpTabOff); }
+// entry k of the combined table (a fill loop's source)
+GGP_DEV double prop_tab_entry(const int k)
+{
+    return k < kDawsonTabN ? ggp_dawson_coef[k] : k < kExpTabOff ? 0.0 : __builtin_bit_cast(double, ggp_exp_tab[k - kExpTabOff]);
+}
+#ifdef GGP_HOST_SIM
+// the combined table on the host (diagnostic builds)
+inline const double *host_prop_tab()
+{
+    static double t[kPropTabN];
+    static bool done = false;
+    if (!done) {
+        for (int k = 0; k < kPropTabN; ++k) t[k] = prop_tab_entry(k);
+        done = true;
+    }
+    return t;
+}
+#endif
 
 GGP_DEV double rdiv(double x, double d, double r)
 {
@@ -93,6 +138,101 @@ GGP_DEV double exp_lane(const double x, bool &big)
     p = __builtin_fma(t, p, 1.0);
     p = __builtin_fma(t, p, 1.0);
     return __builtin_ldexp(p, (int)dn);
+}
+
+// exp(x) as the reference's libm computes it: glibc's table-driven exp (sysdeps/ieee754/dbl-64/
+// e_exp.c), in the build an x86-64 CPU with FMA runs (the reference is built for plain x86-64,
+// src/Makefile:2, and its exp() call resolves to glibc's FMA variant at run time).  The same
+// operations in the same order, with fma exactly where that build has one (its machine code:
+// kd, both reduction steps, both polynomial halves and the last scale step), so the value is
+// glibc's bitwise (tests/test_exp_glibc.py: every double of several ranges against this
+// process's libm).  x = k ln2/128 + r; exp(x) = 2^(k/128) (1 + tail) exp(r); tab = exp_table.inc
+// (LDS on the device: one 16-byte read per call).  |x| < 2^-54, |x| >= 512, inf and NaN take
+// glibc's special paths (exp_glibc_special).
+constexpr double kGInvLn2N = 0x1.71547652b82fep0 * 128, kGShift = 0x1.8p52;
+constexpr double kGNegLn2hiN = -0x1.62e42fefa0000p-8, kGNegLn2loN = -0x1.cf79abc9e3b3ap-47;
+constexpr double kGC2 = 0x1.ffffffffffdbdp-2, kGC3 = 0x1.555555555543cp-3;
+constexpr double kGC4 = 0x1.55555cf172b91p-5, kGC5 = 0x1.1111167a4d017p-7;
+
+GGP_DEV double bits_to_double(const uint64_t u) { return __builtin_bit_cast(double, u); }
+GGP_DEV uint64_t double_to_bits(const double d) { return __builtin_bit_cast(uint64_t, d); }
+
+// the main path's reduction and polynomial: returns tmp, sets sbits and ki
+GGP_DEV double exp_glibc_core(const double x, const uint64_t *tab, uint64_t &sbits, uint64_t &ki)
+{
+    double kd = __builtin_fma(x, kGInvLn2N, kGShift);
+    ki = double_to_bits(kd);
+    kd = kd - kGShift;
+    double r = __builtin_fma(kd, kGNegLn2hiN, x);
+    r = __builtin_fma(kd, kGNegLn2loN, r);
+    const uint32_t idx = 2u * (uint32_t)(ki & 127u);
+    const double tail = bits_to_double(tab[idx]);
+    sbits = tab[idx + 1] + (ki << 45);
+    const double r2 = r * r;
+    const double p1 = __builtin_fma(r, kGC3, kGC2);
+    const double p2 = __builtin_fma(r, kGC5, kGC4);
+    const double acc = __builtin_fma(p1, r2, r + tail);
+    return __builtin_fma(r2 * r2, p2, acc);
+}
+
+// glibc's paths outside 2^-54 <= |x| < 512 (e_exp.c specialcase and the top12 checks); the lane
+// kernels reach them only through their cold paths (propagate_lane_cold, the lane-pair share loop)
+GGP_DEV double exp_glibc_special(const double x, const uint64_t *tab)
+{
+    const uint64_t ix = double_to_bits(x);
+    const uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ffu;
+    if (abstop < 0x3c9u) return x + 1.0;                       // |x| < 2^-54 (and +-0)
+    if (abstop >= 0x409u) {                                     // |x| >= 1024, inf, NaN
+        if (ix == 0xfff0000000000000ull) return 0.0;           // -inf
+        if (abstop == 0x7ffu) return x + 1.0;                  // +inf, NaN
+        return (ix >> 63) ? 0.0 : __builtin_inf();             // underflow / overflow
+    }
+    uint64_t sbits, ki;
+    const double tmp = exp_glibc_core(x, tab, sbits, ki);
+    if ((ki & 0x80000000ull) == 0) {                            // k > 0: scale may overflow
+        const double scale = bits_to_double(sbits - (1009ull << 52));
+        return 0x1p1009 * __builtin_fma(scale, tmp, scale);
+    }
+    const double scale = bits_to_double(sbits + (1022ull << 52));  // k < 0: the subnormal range
+    const double st = scale * tmp;
+    double y = scale + st;
+    if (y < 1.0) {
+        const double hi = y + 1.0;
+        double lo = (scale - y) + st;
+        lo = ((1.0 - hi) + y) + lo;
+        y = (lo + hi) - 1.0;
+        if (y == 0.0) y = 0.0;
+    }
+    return 0x1p-1022 * y;
+}
+
+// the main path only, branch-free (no special-path test per call): `big` collects whether x lies
+// outside 2^-54 <= |x| < 512, where the caller must recompute with exp_glibc.  Any x (inf, NaN
+// included) reads a table entry in range, so the unchecked value is harmless before that
+GGP_DEV double exp_glibc_main(const double x, const uint64_t *tab, bool &big)
+{
+    const uint32_t abstop = (uint32_t)(double_to_bits(x) >> 52) & 0x7ffu;
+    big = big | (abstop - 0x3c9u >= 0x3fu);
+    uint64_t sbits, ki;
+    const double tmp = exp_glibc_core(x, tab, sbits, ki);
+    const double scale = bits_to_double(sbits);
+    double y = __builtin_fma(scale, tmp, scale);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // materialised here: left to the optimiser, the polynomial sinks to the value's uses and the
+    // table words stay live instead (the lane kernels spill ~400 registers)
+    asm volatile("" : "+v"(y));
+#endif
+    return y;
+}
+
+GGP_DEV double exp_glibc(const double x, const uint64_t *tab)
+{
+    const uint32_t abstop = (uint32_t)(double_to_bits(x) >> 52) & 0x7ffu;
+    if (__builtin_expect(abstop - 0x3c9u >= 0x3fu, 0)) return exp_glibc_special(x, tab);
+    uint64_t sbits, ki;
+    const double tmp = exp_glibc_core(x, tab, sbits, ki);
+    const double scale = bits_to_double(sbits);
+    return __builtin_fma(scale, tmp, scale);
 }
 
 // 1/d for finite nonzero d as v_rcp_f64 and two Newton steps (5 instructions against the ~11 of
@@ -168,6 +308,7 @@ enum { XF_MBT = NX, XF_PGQ, NXE };   // slots of the lane schedules' X arrays (N
 constexpr XTask kXF[2] = {{KX_S, 6, 0, 0}, {KX_S, 7, 0, 0}};   // exp(-b t), exp(gq t): pickSV 6, 7
 
 struct XProd { unsigned char j, rep, fac; };   // X[j] = X[rep] * X[fac]
+// the lane schedules take the products unless GGP_EXACT (then all 74 are computed, kXCN below)
 constexpr XProd kXP[] = {
     {XC_B, XC_A, XS_gl},     {XC_J, XC_A, XS_gq},     {XC_G, XC_A, XF_MBT},    {XC_I, XC_A, XS_gq},
     {XC_D, XC_C, XS_gq},     {XC_E, XC_C, X_ONE},     {XC_F, XC_C, XF_PGQ},
@@ -177,11 +318,12 @@ constexpr XProd kXP[] = {
     {XZ_3E2, XZ_3C2, X_ONE}, {XZ_3D2, XZ_3C2, XS_gq}, {XZ_4E2, XZ_4C2, X_ONE}, {XZ_4F2, XZ_4C2, XF_PGQ},
 };
 constexpr int NXP = sizeof(kXP) / sizeof(kXP[0]);
-constexpr int NXC = NXT - NXP + 2;   // exponentials computed per step
+constexpr int NXPU = kExact ? 0 : NXP;          // products the lane schedules form
+constexpr int NXC = kExact ? NXT : NXT - NXP + 2;   // exponentials computed per step
 
 constexpr bool x_is_product(const int j)
 {
-    for (int p = 0; p < NXP; ++p)
+    for (int p = 0; p < NXPU; ++p)
         if (kXP[p].j == j) return true;
     return false;
 }
@@ -195,15 +337,17 @@ constexpr XCList make_xc()
     int n = 0;
     for (int j = 0; j < NXT; ++j)
         if (!x_is_product(j)) { L.j[n] = (unsigned char)j; L.T[n] = kXT[j]; ++n; }
-    L.j[n] = XF_MBT; L.T[n] = kXF[0]; ++n;
-    L.j[n] = XF_PGQ; L.T[n] = kXF[1]; ++n;
+    if (!kExact) {
+        L.j[n] = XF_MBT; L.T[n] = kXF[0]; ++n;
+        L.j[n] = XF_PGQ; L.T[n] = kXF[1]; ++n;
+    }
     return L;
 }
 constexpr XCList kXC = make_xc();
-static_assert(NXP == 22 && NXC == 54, "54 computed exponentials, 22 products");
+static_assert(NXP == 22 && NXC == (kExact ? 74 : 54), "54 computed exponentials, 22 products (74, none: exact)");
 constexpr bool check_products()
 {
-    for (int p = 0; p < NXP; ++p)   // every operand is a computed slot
+    for (int p = 0; p < NXPU; ++p)   // every operand is a computed slot
         if (x_is_product(kXP[p].rep) || x_is_product(kXP[p].fac)) return false;
     return true;
 }
@@ -288,6 +432,38 @@ struct OU {
     double k_xl, k_xx, k_ll, k_qq;   // the sl2 / sq2 prefactors of cov_xl, cov_xx, cov_ll, cov_qq
 };
 
+// x^3 correctly rounded (but for ties within ~2^-100 relative): the exact square and cube as
+// double-doubles (fma residuals), one rounding at the end.  pow(x, 3) in the reference
+// (mean_cov_model.h:95) is glibc's pow, itself correctly rounded but for ~1e-3 of arguments
+GGP_DEV double cube_cr(const double x)
+{
+    const double p = x * x, e1 = __builtin_fma(x, x, -p);
+    const double q = p * x, e2 = __builtin_fma(p, x, -q);
+    return q + __builtin_fma(e1, x, e2);
+}
+
+// a^k sqrt(a), k = 1..3, correctly rounded in the same sense: sqrt(a) = s + ds (s correctly
+// rounded, ds from the exact residual a - s^2), a^k as a double-double, the product's error
+// terms summed, one rounding.  GGP_EXACT's form of pow(a, k + 1/2) (mean_cov_model.h:33, 48, 66)
+GGP_DEV double pow_half_cr(const double a, const int k)
+{
+    const double s = sqrt(a);
+    const double ds = __builtin_fma(-s, s, a) * (0.5 / s);
+    double h = a, l = 0.0;
+    if (k >= 2) {
+        const double p = a * a;
+        l = __builtin_fma(a, a, -p);
+        h = p;
+    }
+    if (k >= 3) {
+        const double p = h * a;
+        l = __builtin_fma(h, a, -p) + l * a;
+        h = p;
+    }
+    const double P = h * s;
+    return P + (__builtin_fma(h, s, -P) + (l * s + h * ds));
+}
+
 GGP_DEV OU make_ou(const double ml, const double gl, const double sl2, const double mq, const double gq,
                    const double sq2, const double b)
 {
@@ -302,7 +478,7 @@ GGP_DEV OU make_ou(const double ml, const double gl, const double sl2, const dou
     P.gl2 = gl * gl;
     P.r_gl2 = 1.0 / P.gl2;
     P.k_xl = sl2 / (2 * (gl * gl));
-    P.k_xx = sl2 / (2 * pow(gl, 3));
+    P.k_xx = sl2 / (2 * cube_cr(gl));
     P.k_ll = sl2 / (2 * gl);
     P.k_qq = rdiv(sq2, 2 * gq, P.r_gq2);
     return P;
@@ -507,10 +683,29 @@ GGP_DEV double exp_arg_body(const ST &S, const XTask T)
          : T.kind == KX_E ? argE : argZ;
 }
 
-template <class ST>
-GGP_DEV double exp_body(const ST &S, const XTask T) { return exp(exp_arg_body(S, T)); }
+#ifdef GGP_HOST_SIM
+// diagnostic hooks (tools/parity_attrib.cpp): the exponential the lane bodies take (glibc's, or
+// exp_ocml's emulation), and pow(a, k + 1/2) as the reference forms it instead of a^k sqrt(a)
+extern double (*ggp_hs_exp)(double);
+extern int ggp_hs_pow_libm;
+#endif
+#if defined(GGP_EXACT)
+#define GGP_LANE_EXP(v, tab) exp_glibc((v), exp_tab_of(tab))
+#elif defined(GGP_HOST_SIM)
+#define GGP_LANE_EXP(v, tab) ggp_hs_exp(v)
+#else
+#define GGP_LANE_EXP(v, tab) exp(v)
+#endif
 
-GGP_DEV double exp_task(const Step &S, int j) { return exp_body(S, kXT[j]); }
+// tab: the propagator's table (kPropTabN doubles: the Dawson rows, then the exp table)
+template <class ST>
+GGP_DEV double exp_body(const ST &S, const XTask T, const double *tab)
+{
+    (void)tab;
+    return GGP_LANE_EXP(exp_arg_body(S, T), tab);
+}
+
+GGP_DEV double exp_task(const Step &S, int j, const double *tab) { return exp_body(S, kXT[j], tab); }
 
 template <class ST>
 GGP_DEV double dawson_body(const ST &S, const DTask T, const double *tab)
@@ -519,6 +714,24 @@ GGP_DEV double dawson_body(const ST &S, const DTask T, const double *tab)
 }
 
 GGP_DEV double dawson_task(const Step &S, int d, const double *tab) { return dawson_body(S, kDT[d], tab); }
+
+// the computed list's task descriptors, packed (pack_x's layout), for runtime-indexed loops
+struct PackedXC {
+    uint32_t w[NXC];
+};
+constexpr PackedXC make_packed_xc()
+{
+    PackedXC p{};
+    for (int k = 0; k < NXC; ++k)
+        p.w[k] = (uint32_t)kXC.T[k].kind | (uint32_t)kXC.T[k].iB << 8 | (uint32_t)kXC.T[k].ic << 16 |
+                 (uint32_t)kXC.T[k].it << 24;
+    return p;
+}
+#if defined(GGP_HOST_SIM)
+static const PackedXC kXCPacked = make_packed_xc();
+#else
+static __constant__ const PackedXC kXCPacked = make_packed_xc();
+#endif
 
 // task descriptors packed in one register word (group schedule: loaded once per kernel)
 GGP_DEV uint32_t pack_x(const XTask T) { return T.kind | T.iB << 8 | T.ic << 16 | (uint32_t)T.it << 24; }
@@ -538,6 +751,10 @@ GGP_DEV double pow_task(const ST &S, int p)
 {
     const double sa = S.two_sa * 0.5;           // sqrt(a), exact
     const double a = S.a;
+#ifdef GGP_HOST_SIM
+    if (ggp_hs_pow_libm) return p == 0 ? 4. * pow(a, 1.5) : p == 1 ? 8. * pow(a, 2.5) : 16. * pow(a, 3.5);
+#endif
+    if constexpr (kExact) return p == 0 ? 4. * pow_half_cr(a, 1) : p == 1 ? 8. * pow_half_cr(a, 2) : 16. * pow_half_cr(a, 3);
     return p == 0 ? 4. * (a * sa) : p == 1 ? 8. * ((a * a) * sa) : 16. * (((a * a) * a) * sa);
 }
 constexpr int NPW = 6;   // 3 denominators + 3 reciprocals
@@ -799,29 +1016,64 @@ GGP_DEV void cross_outputs(const Step &S, const IA &I, const XA &X, double *K)
 // constexpr template arguments, so every array index is a compile-time constant and the
 // arrays stay in registers.
 template <size_t... J>
-GGP_DEV void lane_exps(const Step &S, double *X, std::index_sequence<J...>)
+GGP_DEV void lane_exps(const Step &S, double *X, const double *tab, std::index_sequence<J...>)
 {
-    ((X[J] = exp_body(S, XTask{kXT[J].kind, kXT[J].iB, kXT[J].ic, kXT[J].it})), ...);
+    ((X[J] = exp_body(S, XTask{kXT[J].kind, kXT[J].iB, kXT[J].ic, kXT[J].it}, tab)), ...);
 }
+// GGP_EXACT's exponentials of the computed list, tasks [OFF, OFF + N): exp_glibc's main path in
+// blocks of kExpBlock behind a scheduling barrier each (left free, the scheduler issues every
+// table read of the step first and the lane kernels spill ~1300 registers), `big` collected
+#ifndef GGP_EXP_BLOCK
+#define GGP_EXP_BLOCK 8
+#endif
+constexpr int kExpBlock = GGP_EXP_BLOCK;
+template <size_t B, size_t... K>
+GGP_DEV void glibc_exp_block(const Step &S, double *Xc, const uint64_t *et, bool &big, std::index_sequence<K...>)
+{
+    ((Xc[B + K] = exp_glibc_main(exp_arg_body(S, XTask{kXC.T[B + K].kind, kXC.T[B + K].iB, kXC.T[B + K].ic,
+                                                       kXC.T[B + K].it}), et, big)), ...);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+template <size_t OFF, size_t N, size_t... Bi>
+GGP_DEV void glibc_exps(const Step &S, double *Xc, const uint64_t *et, bool &big, std::index_sequence<Bi...>)
+{
+    (glibc_exp_block<OFF + Bi * kExpBlock>(
+         S, Xc, et, big, std::make_index_sequence<(N - Bi * kExpBlock < (size_t)kExpBlock ? N - Bi * kExpBlock : kExpBlock)>{}),
+     ...);
+}
+template <size_t OFF, size_t N>
+GGP_DEV void glibc_exps_all(const Step &S, double *Xc, const double *tab, bool &big)
+{
+    glibc_exps<OFF, N>(S, Xc, exp_tab_of(tab), big, std::make_index_sequence<(N + kExpBlock - 1) / kExpBlock>{});
+}
+
 // the computed exponentials kXC, tasks K: Xc[K] (the list's order; lane_expand puts them in
 // their slots)
 template <size_t... K>
-GGP_DEV void lane_exps_c(const Step &S, double *Xc, std::index_sequence<K...>)
+GGP_DEV void lane_exps_c(const Step &S, double *Xc, const double *tab, std::index_sequence<K...>)
 {
-    ((Xc[K] = exp_body(S, XTask{kXC.T[K].kind, kXC.T[K].iB, kXC.T[K].ic, kXC.T[K].it})), ...);
+    ((Xc[K] = exp_body(S, XTask{kXC.T[K].kind, kXC.T[K].iB, kXC.T[K].ic, kXC.T[K].it}, tab)), ...);
 }
 // the same values with exp_lane (one compare per exponential instead of ocml's checks): faster
 // where registers allow (the lane-pair schedule's share of the tasks: C4 shard 0.81 -> 0.79 ms),
 // slower in the one-wave lane and smoother kernels, which keep lane_exps_c (tools/lane_ab.py)
+// GGP_EXACT: exp_glibc's main path only; `cold` is set when an argument lies outside it (the
+// caller then redoes the lane's step through propagate_lane_cold)
 template <size_t OFF, size_t... K>
-GGP_DEV void lane_exps_flagged(const Step &S, double *Xc, std::index_sequence<K...>)
+GGP_DEV void lane_exps_flagged(const Step &S, double *Xc, const double *tab, std::index_sequence<K...>, bool &cold)
 {
+    if constexpr (kExact) {
+        glibc_exps_all<OFF, sizeof...(K)>(S, Xc, tab, cold);
+        return;
+    }
     bool big = false;
     ((Xc[OFF + K] = exp_lane(exp_arg_body(S, XTask{kXC.T[OFF + K].kind, kXC.T[OFF + K].iB, kXC.T[OFF + K].ic,
                                                     kXC.T[OFF + K].it}), big)), ...);
     if (big)   // an argument beyond kExpFastMax (inf / NaN states): ocml's exp for this lane's set
         ((Xc[OFF + K] = exp_body(S, XTask{kXC.T[OFF + K].kind, kXC.T[OFF + K].iB, kXC.T[OFF + K].ic,
-                                          kXC.T[OFF + K].it})), ...);
+                                          kXC.T[OFF + K].it}, tab)), ...);
 }
 // Xc (the computed list) into the slots of X [NXE], X_ONE, then the 22 products
 template <size_t... K, size_t... P>
@@ -833,7 +1085,7 @@ GGP_DEV void lane_expand(const double *Xc, double *X, std::index_sequence<K...>,
 }
 GGP_DEV void lane_expand(const double *Xc, double *X)
 {
-    lane_expand(Xc, X, std::make_index_sequence<NXC>{}, std::make_index_sequence<NXP>{});
+    lane_expand(Xc, X, std::make_index_sequence<NXC>{}, std::make_index_sequence<NXPU>{});
 }
 template <size_t... J>
 GGP_DEV void lane_dawsons(const Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
@@ -855,16 +1107,43 @@ GGP_DEV void lane_taus(const Step &S, const XA &X, const DA &Dw, const PA &PW, d
 
 // ---- lane schedule: one lane runs every task of its own cell
 // K (optional, 16): cross_cov_model of the same step (the -j path)
-GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, const double *tab, double *K = nullptr)
+template <bool COLD>
+GGP_DEV void propagate_lane_body(double *m, double *C, const double t, const OU &P, const double *tab, double *K);
+
+// GGP_EXACT's cold step: an exponential argument outside exp_glibc's main path (|x| >= 512, inf,
+// NaN) somewhere in this lane's step -- the whole step again with every exponential through
+// exp_glibc's special paths.  Out of line on the device: the hot step keeps its registers
+#if defined(GGP_HOST_SIM)
+inline
+#else
+__device__ __attribute__((noinline))
+#endif
+void propagate_lane_cold(double *m, double *C, const double t, const OU &P, const double *tab, double *K)
+{
+    propagate_lane_body<true>(m, C, t, P, tab, K);
+}
+
+template <bool COLD>
+GGP_DEV void propagate_lane_body(double *m, double *C, const double t, const OU &P, const double *tab, double *K)
 {
     Step S;
     step_init(S, m, C, t, P);
     double Xc[NXC], X[NXE];
+    if constexpr (kExact && !COLD) {
+        bool big = false;
+        glibc_exps_all<0, NXC>(S, Xc, tab, big);
+        if (__builtin_expect(big, 0)) {   // m, C are untouched so far
+            propagate_lane_cold(m, C, t, P, tab, K);
+            return;
+        }
+    } else {
 #ifdef GGP_LANE_FLAGGED
-    lane_exps_flagged<0>(S, Xc, std::make_index_sequence<NXC>{});
+        bool cold = false;
+        lane_exps_flagged<0>(S, Xc, tab, std::make_index_sequence<NXC>{}, cold);
 #else
-    lane_exps_c(S, Xc, std::make_index_sequence<NXC>{});
+        lane_exps_c(S, Xc, tab, std::make_index_sequence<NXC>{});
 #endif
+    }
     lane_expand(Xc, X);
     double Dw[ND];
     lane_dawsons(S, Dw, tab, std::make_index_sequence<ND>{});
@@ -882,6 +1161,11 @@ GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, c
 #else
     outputs(S, I, X, m, C);
 #endif
+}
+
+GGP_DEV void propagate_lane(double *m, double *C, const double t, const OU &P, const double *tab, double *K = nullptr)
+{
+    propagate_lane_body<false>(m, C, t, P, tab, K);
 }
 
 // division map of mean_cov_after_division (predictions.h:40-60), after the propagation

@@ -74,6 +74,37 @@ def shard(hf: HostForest, rank: int, world: int) -> HostForest:
     return hf.subset_trees(roots[parts[rank]])
 
 
+def global_init_stats(hf: HostForest, group=None, device=None) -> None:
+    """Give this rank's forest the init statistics of the whole forest the ranks hold between them
+    (init_cells_f / init_cells_r, moma_input.h:675-735: mean and E[v^2] - mean^2 of the first and
+    last log_length / fp over every cell with more than one row), for ranks that generated or read
+    only their own trees: one all_reduce of 9 sums.  The sums cross ranks in another order than one
+    process adds them, so the statistics agree with the single-forest ones to the last bits, not
+    bitwise."""
+    import torch
+    import torch.distributed as dist
+    a = hf.a
+    ro = np.asarray(a["row_offset"])
+    sel = np.diff(ro) > 1
+    first, last = ro[:-1][sel], ro[1:][sel] - 1
+    cols = [a["log_length"][first], a["fp"][first], a["log_length"][last], a["fp"][last]]
+    v = [float(sel.sum())] + [float(np.sum(c)) for c in cols] + [float(np.sum(c * c)) for c in cols]
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        backend = dist.get_backend(group)
+        dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                                 if backend == "nccl" else torch.device("cpu"))
+        t = torch.tensor(v, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, group=group)
+        v = [float(x) for x in t.cpu()]
+    n = v[0]
+    mean = [x / n for x in v[1:5]]
+    var = [v[5 + k] / n - mean[k] * mean[k] for k in range(4)]
+    a["root_mean_xg"] = np.array(mean[0:2])
+    a["root_var_xg"] = np.array(var[0:2])
+    a["leaf_mean_xg"] = np.array(mean[2:4])
+    a["leaf_var_xg"] = np.array(var[2:4])
+
+
 def combine_partials(partials, nan_flags):
     """rank-order sum; first NaN = lowest rank that saw one"""
     for r, flag in enumerate(nan_flags):
@@ -160,6 +191,38 @@ class ShardedObjective:
             return self.f.total_likelihood(params), False, None
         except LikelihoodIsNan as e:
             return math.nan, True, e
+
+    def total_likelihood_chain(self, points):
+        """a known sequence of objective calls, each from the state the previous left (the -s scan,
+        the Hessian points; ggp_total_loglik_chain): every rank chains its own shard -- the carried
+        state is per tree, so the points need no exchange between them -- and ONE all_gather of the
+        per-point partials follows; the totals are the rank-order sums, as total_likelihood's.
+        Returns the totals of the points (a NaN point: NaN and every later point NaN too, as the
+        chain stops there)"""
+        pts = np.ascontiguousarray(np.atleast_2d(points), np.float64)
+        n = pts.shape[0]
+        try:
+            local = np.asarray(self.f.total_likelihood_chain(pts), np.float64)
+        except LikelihoodIsNan as e:
+            if self.world == 1 and not self.always_gather:
+                raise
+            local = np.asarray(getattr(e, "ll", []), np.float64)
+        if len(local) < n:
+            local = np.concatenate([local, np.full(n - len(local), math.nan)])
+        if self.world == 1 and not self.always_gather:
+            return local
+        torch = self.torch
+        send = torch.from_numpy(local.copy()).to(self.dev)
+        recv = torch.zeros(n * self.world, dtype=torch.float64, device=self.dev)
+        self.dist.all_gather_into_tensor(recv, send, group=self.group)
+        got = recv.cpu().numpy().reshape(self.world, n)
+        out = np.empty(n)
+        for k in range(n):
+            s = 0.0
+            for r in range(self.world):
+                s = s + float(got[r, k])
+            out[k] = s
+        return out
 
     def total_likelihood(self, params) -> float:
         if self.engine:   # the engine returns the rank-order sum (or raises, on every rank)

@@ -401,9 +401,13 @@ class Forest:
     visible device).  Results have the same bits for any device list."""
 
     def __init__(self, host_forest: HostForest, device: int = 0, kernel: str = "auto", devices=(),
-                 max_shard_rows: int = 0):
+                 max_shard_rows: int = 0, exact: bool = False):
         self.host = host_forest
-        self._lib = N.engine()
+        # exact=True: the engine built in the oracle's arithmetic (lib/libggp_exact.so, GGP_EXACT:
+        # glibc's exp, every exponential from its own argument, no fma contraction, the combine's
+        # IEEE inverses; no wave schedule), the reference's roundings step for step (DESIGN.md §2)
+        self._lib = N.engine(N.EXACT_ENGINE if exact else None)
+        self.exact = bool(exact) or N.engine_name() == N.EXACT_ENGINE
         self._poisoned = False
         d = host_forest.desc([device] if devices == () else devices, kernel, max_shard_rows)
         h = ctypes.c_void_p()
@@ -473,6 +477,11 @@ class Forest:
         self._check(self._lib.ggp_comm_attach(self._h, rccl_lib.encode() if rccl_lib else None, int(nranks),
                                               int(rank), bytes(uid)))
         self._comm_rank = int(rank)
+
+    def comm_size(self) -> int:
+        """ranks of the attached RCCL communicator as RCCL counts them (ncclCommCount); 0 if the handle
+        is not attached"""
+        return int(self._lib.ggp_comm_size(self._h))
 
     def submit(self, params) -> None:
         """enqueue one evaluation (ggp_total_loglik_async)"""

@@ -259,6 +259,9 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
 int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last call, -1 none */
+int32_t ggp_comm_size(const ggp_forest *f);       /* ranks of the attached RCCL communicator as RCCL
+                                                     counts them (ncclCommCount); 0 = not attached,
+                                                     -1 = the library lacks ncclCommCount */
 int32_t ggp_comm_local_nan(const ggp_forest *f);  /* 1: this rank's own last evaluation was bad */
 
 int ggp_device_count(int32_t *n);

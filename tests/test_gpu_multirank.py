@@ -42,7 +42,9 @@ def test_bench_two_ranks_gloo_rehearsal():
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", str(warm),
            "--trees", str(trees), "--rows", str(rows), "--no-cpu", "--large-trees", "0", "--predict-trees", "0",
-           "--hessian", "0", "--backend", "gloo", "--device", "0"]
+           "--hessian", "0", "--backend", "gloo", "--device", "0",
+           "--c4-trees", "2000", "--c4-steps", "5", "--c4-scan", "5", "--c5-trees", "2000",
+           "--c5-chunk-rows", "300000"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -74,6 +76,22 @@ def test_bench_two_ranks_gloo_rehearsal():
         vw = fw.total_likelihood(bench.P_EXAMPLE)
     fw.close()
     assert ip["total_log_likelihood"] == vw
+    # the strong-scaling legs: ONE forest split over the ranks.  C4: 2000 trees x 200 in two halves,
+    # the whole forest's init statistics on both (one all_reduce), 3 + 5 evaluations then the
+    # 5-sample chained scan; the gathered total against one handle over the whole forest (the
+    # statistics' sums cross ranks in another order: agreement to the path's conditioning, not bitwise)
+    c4 = out["c4_strong"]
+    assert c4["rows"] == 2000 * rows and c4["trees_per_rank"] == 1000 and c4["scaling"] == "strong"
+    assert c4["collective"]["ranks"] == 2 and c4["scan"]["samples"] == 5
+    h4 = g.HostForest.synthetic(2000, rows, seed=bench.SEED, first_tree=3 * 10 ** 6)
+    f4 = g.Forest(h4, device=0)
+    for _ in range(3 + 5):
+        v4 = f4.total_likelihood(bench.P_EXAMPLE)
+    f4.close()
+    assert c4["total_log_likelihood"] == pytest.approx(v4, rel=1e-9)
+    # C5 -p split: 2000 trees x 500 = 1e6 rows, 5e5 per rank smoothed in two chunks of <= 3e5 rows
+    c5 = out["c5_predict_split"]
+    assert c5["rows"] == 2000 * 500 and c5["shards_per_rank"] == 2 and c5["rows_per_s"] > 0
 
 
 def _worker(rank, world, port, q):

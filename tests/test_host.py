@@ -186,7 +186,8 @@ def _declared(header):
     return set(re.findall(r"\b(ggp_[a-z0-9_]+)\s*\(", txt))
 
 
-@pytest.mark.parametrize("lib,header", [("libggp.so", "ggp.h"), ("libggp_host.so", "ggp_host.h")])
+@pytest.mark.parametrize("lib,header", [("libggp.so", "ggp.h"), ("libggp_exact.so", "ggp.h"),
+                                        ("libggp_host.so", "ggp_host.h")])
 def test_library_exports_every_declared_symbol(lib, header):
     path = os.path.join(ROOT, "gfp_gaussian_process_amd", "lib", lib)
     out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
@@ -197,7 +198,7 @@ def test_library_exports_every_declared_symbol(lib, header):
     assert not missing, missing
     # and the python binding table covers exactly the header
     from gfp_gaussian_process_amd import _native as N
-    table = N.ENGINE_SYMBOLS if lib == "libggp.so" else N.HOST_SYMBOLS
+    table = N.HOST_SYMBOLS if lib == "libggp_host.so" else N.ENGINE_SYMBOLS
     assert set(table) == declared
 
 

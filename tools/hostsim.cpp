@@ -7,6 +7,14 @@
 #include "ggp_outtab.h"
 #include <cstring>
 
+// the diagnostic hooks of the device headers (GGP_HOST_SIM): glibc's exp, the table Dawson
+double (*ggp_hs_dawson)(double) = nullptr;
+static double glibc_exp(double x) { return ::exp(x); }
+namespace ggp {
+double (*ggp_hs_exp)(double) = glibc_exp;
+int ggp_hs_pow_libm = 0;
+}
+
 extern "C" {
 // mean_cov_model through the lane schedule's expressions (ggp::propagate_lane)
 void hs_mcm_lane(double *m, double *C, double t, const double *p)
@@ -42,7 +50,7 @@ void hs_terms(const double *m, const double *C, double t, const double *p, doubl
     Step S;
     step_init(S, m, C, t, P);
     double X[NX];
-    lane_exps(S, X, std::make_index_sequence<NXT>{});
+    lane_exps(S, X, ggp::host_prop_tab(), std::make_index_sequence<NXT>{});
     X[X_ONE] = 1.0;
     double Dw[ND];
     lane_dawsons(S, Dw, ggp_dawson_coef, std::make_index_sequence<ND>{});
@@ -123,10 +131,10 @@ void hs_mcm_lane_mask(double *m, double *C, double t, const double *p)
     Step S;
     step_init(S, m, C, t, P);
     double Xc[NXC], X[NXE];
-    lane_exps_c(S, Xc, std::make_index_sequence<NXC>{});
+    lane_exps_c(S, Xc, ggp::host_prop_tab(), std::make_index_sequence<NXC>{});
     lane_expand(Xc, X);
     for (int q = 0; q < NXP; ++q)
-        if (!((hs_xp_mask >> q) & 1)) X[kXP[q].j] = exp_body(S, kXT[kXP[q].j]);
+        if (!((hs_xp_mask >> q) & 1)) X[kXP[q].j] = exp_body(S, kXT[kXP[q].j], ggp::host_prop_tab());
     double Dw[ND];
     lane_dawsons(S, Dw, ggp_dawson_coef, std::make_index_sequence<ND>{});
     double PW[NPW];
