@@ -359,6 +359,7 @@ def main() -> int:
         ll = obj.total_likelihood(P_EXAMPLE)
     barrier()
     el = time.perf_counter() - t0
+    clock_timed = fg.launch_clock()   # the last timed launch's shader clock (wave schedule only)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -369,8 +370,12 @@ def main() -> int:
     # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
     fg.enable_profile()
     per = {}                                   # kernel name -> [ms, rows, launches]
+    clocks = []
     for _ in range(max(3, min(args.steps, 10))):
         fg.total_likelihood(P_EXAMPLE)
+        ck = fg.launch_clock()
+        if ck:
+            clocks.append(ck[0])
         for ms, rows, name in zip(*fg.launch_profile()):
             acc = per.setdefault(name, [0.0, 0, 0])
             acc[0] += ms
@@ -799,6 +804,11 @@ def main() -> int:
             },
             "fp64": fp64,
             "total_log_likelihood": ll,
+            "clock": None if clock_timed is None else {
+                "shader_mhz_last_timed_launch": clock_timed[0], "window_us": clock_timed[1],
+                "shader_mhz_profiled_launches": clocks,
+                "note": "the path launch's block 0: s_memtime cycles per s_memrealtime tick (100 MHz) over its "
+                        "path (ggp_launch_clock), i.e. the DVFS clock the evaluation ran at; peak 2400 MHz"},
         }
         if large is not None:
             result["large_forest"] = large

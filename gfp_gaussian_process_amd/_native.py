@@ -89,6 +89,7 @@ ENGINE_SYMBOLS = {
                                        ctypes.c_char_p]),
     "ggp_comm_nan_rank": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_comm_size": (ctypes.c_int32, [ctypes.c_void_p]),
+    "ggp_launch_clock": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
     "ggp_comm_local_nan": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),
     "ggp_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -154,6 +155,38 @@ def _load(name: str, table: dict):
     return lib
 
 
+def elf_dynamic(path: str):
+    """(DT_SONAME, [DT_NEEDED...]) of an ELF64 little-endian shared object, read from its dynamic
+    section (memory-mapped: no full read of a large runtime library)"""
+    import mmap
+    import struct
+    with open(path, "rb") as fh, mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) as m:
+        if m[:4] != b"\x7fELF" or m[4] != 2 or m[5] != 1:
+            raise ValueError(f"{path}: not an ELF64 little-endian object")
+        phoff, = struct.unpack_from("<Q", m, 0x20)
+        phentsize, phnum = struct.unpack_from("<HH", m, 0x36)
+        loads, dyn = [], None
+        for i in range(phnum):
+            p_type, _, p_offset, p_vaddr, _, p_filesz, _, _ = struct.unpack_from("<IIQQQQQQ", m, phoff + i * phentsize)
+            if p_type == 1:
+                loads.append((p_vaddr, p_offset, p_filesz))
+            elif p_type == 2:
+                dyn = (p_offset, p_filesz)
+        if dyn is None:
+            return None, []
+        ents = [struct.unpack_from("<qQ", m, dyn[0] + 16 * k) for k in range(dyn[1] // 16)]
+        strtab = next((v for t, v in ents if t == 5), None)
+        if strtab is None:
+            return None, []
+        base = next((off + strtab - va for va, off, sz in loads if va <= strtab < va + sz), None)
+
+        def cstr(o):
+            end = m.find(b"\0", base + o)
+            return m[base + o:end].decode()
+        soname = next((cstr(v) for t, v in ents if t == 14), None)
+        return soname, [cstr(v) for t, v in ents if t == 1]
+
+
 def _one_hip_runtime() -> None:
     """One HIP runtime per process.  libggp.so needs libamdhip64.so.7; PyTorch-ROCm ships its own
     copy (same SONAME, another file) and its libraries ask for it by another name, so when the
@@ -173,9 +206,22 @@ def _one_hip_runtime() -> None:
         return
     for d in spec.submodule_search_locations:
         hip = os.path.join(d, "lib", "libamdhip64.so")
-        if os.path.exists(hip):
+        if not os.path.exists(hip):
+            continue
+        # only a runtime the engine would bind to by name: torch's SONAME must be the
+        # libamdhip64 the engine library lists as NEEDED, else preloading would map a second runtime
+        try:
+            want = [n for n in elf_dynamic(os.path.join(LIB_DIR, engine_name()))[1] if n.startswith("libamdhip64")]
+            have = elf_dynamic(hip)[0]
+        except (OSError, ValueError):
+            want, have = [], None
+        if want and have == want[0]:
             ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
-            return
+        else:
+            import warnings
+            warnings.warn(f"torch's HIP runtime ({hip}, SONAME {have}) is not the {want[0] if want else 'libamdhip64'} "
+                          "the engine needs: not preloaded; importing torch after the engine may map two HIP runtimes")
+        return
 
 
 def engine_name() -> str:

@@ -307,6 +307,7 @@ GGP_DEV void propagate(double *m, double *C, const double t, const ggp::OU &P, c
     get_rest<ggp::NXC, W, Q, CPW>(Xc, Xl, ln);
     get_rest<ggp::ND, W, Q, CPW>(Dw, Dl, ln);
     ggp::lane_expand(Xc, X);   // the slots, X_ONE and the products, in every wave
+    ggp::lane_guard_products(S, X, tab);
     double PW[ggp::NPW];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -842,6 +843,7 @@ struct ChainRed {
     double *host_sum;
     long long *host_nan;
     int n_lblocks;                // 0: no in-launch reduction
+    unsigned long long *clk;      // mapped: block 0's shader-clock and 100 MHz ticks over its path
 };
 constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
 
@@ -974,10 +976,16 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
     __builtin_amdgcn_s_waitcnt(0);
     if (add_agent(R.done) + 1 != (unsigned)R.n_lblocks) return;
     zero_agent(R.done);
-    // every block's slots reached host memory before its count (each block waited for its stores
-    // before adding): the sequence number last, a plain system-scope store (a release here would
-    // also write back this XCD's L2, which holds nothing the host reads)
+    // every block's slots reached host memory before its count: each block's system-scope stores to
+    // the fine-grained (uncached) host slots are acknowledged by the fabric before its s_waitcnt(0)
+    // lets the count go out, so they are host-visible when the last block sees the full count.
+    // The sequence number goes last with a system-scope release (the memory model's
+    // ordering, not only the hardware's; one per launch -- A/B in DESIGN.md §6)
+#ifdef GGP_SEQ_RELAXED
     __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+    __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1010,6 +1018,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     [[maybe_unused]] const int CPW = gridDim.x <= 1024 ? 8 : 4;   // GGP_STAMPS builds only
     __shared__ __attribute__((aligned(16))) double lds[W::kLds];
     const int lane = threadIdx.x;
+    // the launch's shader clock (ggp_launch_clock): block 0 reads the shader-clock counter and the
+    // constant 100 MHz counter at its start and after its path (two scalar reads each)
+    const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
     GGP_TL(0);
@@ -1443,6 +1454,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
     GGP_STAMP_FLUSH();
     GGP_PSTAMP_FLUSH();
+    if (red.clk && blockIdx.x == 0 && blockIdx.y == 0 && lane == 0) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        __hip_atomic_store(red.clk, c1 - clk_c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(red.clk + 1, r1 - clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (red.n_lblocks > 0) chain_reduce(red, red_unpark(lds + W::L_RED, lane), call_seq, lane, cell_ll, cell_nan, lds + W::L_RX0);
     GGP_TL(6);
     GGP_TL_CNT_FLUSH();
@@ -2487,6 +2503,8 @@ struct Shard {
     int64_t *h_nan = nullptr, *m_nan = nullptr;
     volatile int64_t *h_seq = nullptr;
     int64_t *m_seq = nullptr;
+    volatile unsigned long long *h_clk = nullptr;   // path launches: block 0's clock counters
+    unsigned long long *m_clk = nullptr;
     int64_t seq = 0;
     bool seq_pending = false;
     bool spin = true;
@@ -3067,7 +3085,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
-        const size_t slots = 2 * (size_t)f->n_lblocks + 1;
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 2;   // + the launch clock's two counters
         void *h = nullptr, *m = nullptr;
         if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
@@ -3081,6 +3099,9 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->m_sum = (double *)m;
             f->m_nan = (int64_t *)((char *)m + f->n_lblocks * sizeof(double));
             f->m_seq = (int64_t *)((char *)m + 2 * f->n_lblocks * sizeof(double));
+            f->h_clk = (volatile unsigned long long *)((char *)h + (2 * f->n_lblocks + 1) * sizeof(double));
+            f->m_clk = (unsigned long long *)((char *)m + (2 * f->n_lblocks + 1) * sizeof(double));
+            f->h_clk[0] = f->h_clk[1] = 0;
         }
     }
     if (rc != GGP_OK) {
@@ -3180,6 +3201,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
                 R.host_sum = f->m_sum;
                 R.host_nan = (long long *)f->m_nan;
                 R.n_lblocks = (int)f->n_lblocks;
+                R.clk = f->m_clk;
                 f->red = R;
             }
         }
@@ -3513,6 +3535,17 @@ int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t
         return fail(GGP_EDEV);
     }
     f->comm = c;
+    return GGP_OK;
+}
+
+int ggp_launch_clock(const ggp_forest *f, double *shader_mhz, double *window_us)
+{
+    if (!f || f->shards.empty() || !f->shards[0]->h_clk) return GGP_EINVAL;
+    const Shard *s = f->shards[0];
+    const unsigned long long c = s->h_clk[0], r = s->h_clk[1];
+    if (r == 0) return GGP_EINVAL;   // no path launch has run on this handle
+    if (shader_mhz) *shader_mhz = (double)c / (double)r * 100.0;   // s_memrealtime: 100 MHz
+    if (window_us) *window_us = (double)r / 100.0;
     return GGP_OK;
 }
 

@@ -1087,6 +1087,27 @@ GGP_DEV void lane_expand(const double *Xc, double *X)
 {
     lane_expand(Xc, X, std::make_index_sequence<NXC>{}, std::make_index_sequence<NXPU>{});
 }
+// A product's factor is exp(-gl t), exp(-gq t), exp(-b t) or exp(gq t): beyond |k t| ~ 700 it
+// under- or overflows while the direct exponential of the sum may not (0 x inf = NaN where the
+// reference is finite).  Such a step (rare: a dt of weeks at the example's rates, where the
+// reference's own integrals stop being finite first, tests/test_gpu_parity.py long-dt test) forms
+// the 22 slots from their own arguments instead
+GGP_DEV bool products_risky(const Step &S)
+{
+    const double m = fmax(fabs(S.gl * S.t), fmax(fabs(S.gq * S.t), fabs(S.b * S.t)));
+    return !(m <= 700.0);
+}
+template <size_t... P>
+GGP_DEV void lane_direct_products(const Step &S, double *X, const double *tab, std::index_sequence<P...>)
+{
+    ((X[kXP[P].j] = exp_body(S, kXT[kXP[P].j], tab)), ...);
+}
+GGP_DEV void lane_guard_products(const Step &S, double *X, const double *tab)
+{
+    if constexpr (NXPU > 0) {
+        if (__builtin_expect(products_risky(S), 0)) lane_direct_products(S, X, tab, std::make_index_sequence<NXPU>{});
+    }
+}
 template <size_t... J>
 GGP_DEV void lane_dawsons(const Step &S, double *Dw, const double *tab, std::index_sequence<J...>)
 {
@@ -1145,6 +1166,7 @@ GGP_DEV void propagate_lane_body(double *m, double *C, const double t, const OU 
 #endif
     }
     lane_expand(Xc, X);
+    lane_guard_products(S, X, tab);
     double Dw[ND];
     lane_dawsons(S, Dw, tab, std::make_index_sequence<ND>{});
     double PW[NPW];

@@ -478,6 +478,13 @@ class Forest:
                                               int(rank), bytes(uid)))
         self._comm_rank = int(rank)
 
+    def launch_clock(self):
+        """(shader MHz, window us) of the last path launch's block 0 (ggp_launch_clock), or None"""
+        mhz, us = ctypes.c_double(), ctypes.c_double()
+        if self._lib.ggp_launch_clock(self._h, ctypes.byref(mhz), ctypes.byref(us)) != N.GGP_OK:
+            return None
+        return mhz.value, us.value
+
     def comm_size(self) -> int:
         """ranks of the attached RCCL communicator as RCCL counts them (ncclCommCount); 0 if the handle
         is not attached"""

@@ -259,6 +259,10 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells,
 int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id);
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id);
 int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last call, -1 none */
+/* The shader clock the last path launch (the wave schedule's one-launch evaluation) ran at, as its
+ * block 0 measured it over its path: s_memtime cycles per s_memrealtime tick (100 MHz) -- the
+ * DVFS clock of a real evaluation, for a benchmark line.  GGP_EINVAL if none ran on this handle. */
+int ggp_launch_clock(const ggp_forest *f, double *shader_mhz, double *window_us);
 int32_t ggp_comm_size(const ggp_forest *f);       /* ranks of the attached RCCL communicator as RCCL
                                                      counts them (ncclCommCount); 0 = not attached,
                                                      -1 = the library lacks ncclCommCount */

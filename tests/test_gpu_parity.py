@@ -882,38 +882,65 @@ def _row_err(a, b):
 @pytest.mark.parametrize("which", ["example", "c5_shape_2k"])
 def test_predict_every_row_within_the_oracles_own_noise(example_forests, which):
     """-p row by row against a bar calibrated on the reference algorithm itself: the oracle under
-    +-1 ulp noise on every exp() (three seeds) moves each row by some amount; every GPU row
-    (forward, backward, combined) must lie within max(FLOOR, 10 x that movement) of the oracle --
-    on the example (every one of its 22,065 rows).  On 2,000 C5-shaped trees (1e6 rows) three
-    seeds underestimate some rows' sensitivity (measured: 29 of 1e6 backward rows at 1-1.7x the
-    bar), so there every row must lie within 30 x and 99.99% within 10 x.  Everywhere the GPU's
-    median error must not exceed the oracle's own median movement.  FLOOR = 1e-10 covers the
-    combine's reciprocal pivots (<= 1.2e-11 from the exact form, test_combine_fast_form_vs_exact).
-    Beside PRED_TOL's blanket 1e-5, this shows where the GPU sits: at the reference's own rounding
-    noise, row by row."""
+    +-1 ulp noise on every exp() moves each row by some amount; EVERY GPU row (forward, backward,
+    combined) must lie within max(FLOOR, 10 x that movement) of the oracle.  On the example the
+    movement is measured here (three seeds); on 2,000 C5-shaped trees (1e6 rows) it comes from the
+    committed calibration over twelve seeds (tests/golden/smoother_noise_c5shape_2k.npz,
+    make_smoother_noise.py: three seeds had underestimated 29 rows' sensitivity by up to 1.7x, and
+    round 4's test had been relaxed to 30x for them; twelve seeds cover them, and the 10x bar holds
+    for every row again).  Everywhere the GPU's median error must not exceed the oracle's own median
+    movement.  FLOOR = 1e-10 covers the combine's reciprocal pivots (<= 1.2e-11 from the exact form,
+    test_combine_fast_form_vs_exact).  The exact-arithmetic engine holds every row at 1e-12
+    (test_gpu_exact.py)."""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     FLOOR = 1e-10
+    P = CONFIGS[0][2]
     if which == "example":
         hf = example_forests[("scaled", "binomial")]
+        ref = O.OracleForest(hf.a).predict(P)
+        noisy = [O.OracleForest(hf.a, exp_ulp_noise=s).predict(P) for s in (12345, 777, 4242)]
+        moves = [np.max([_row_err(z[k], ref[k]) for z in noisy], axis=0) for k in range(3)]
     else:
         hf = g.HostForest.synthetic(2000, 500)
-    P = CONFIGS[0][2]
+        ref = O.OracleForest(hf.a).predict(P)
+        cal = np.load(os.path.join(GOLDEN, "smoother_noise_c5shape_2k.npz"))
+        moves = [10.0 ** (cal[n].astype(np.float64) / 16.0 - 16.0) for n in ("forward", "backward", "combined")]
     got = g.Forest(hf).predict(P)
-    ref = O.OracleForest(hf.a).predict(P)
-    noisy = [O.OracleForest(hf.a, exp_ulp_noise=s).predict(P) for s in (12345, 777, 4242)]
     for k, name in enumerate(("forward", "backward", "combined")):
-        move = np.max([_row_err(z[k], ref[k]) for z in noisy], axis=0)
+        move = moves[k]
+        assert len(move) == len(ref[k])
         e = _row_err(got[k], ref[k])
         bound = np.maximum(FLOOR, 10 * move)
-        within = float(np.mean(e <= bound))
         print(f"{which} {name}: rows {len(e)}, gpu err median {np.median(e):.2e} max {e.max():.2e}; "
               f"oracle noise median {np.median(move):.2e} max {move.max():.2e}; worst err/bound "
-              f"{np.max(e / bound):.2f}; rows within 10x {within:.6f}")
+              f"{np.max(e / bound):.2f}")
         assert np.median(e) <= np.median(move), name
-        if which == "example":
-            bad = np.nonzero(~(e <= bound))[0]
-            assert len(bad) == 0, (name, bad[:5], e[bad[:5]], bound[bad[:5]])
-        else:
-            assert within >= 0.9999, (name, within)
-            assert np.all(e <= np.maximum(FLOOR, 30 * move)), (name, float(np.max(e / bound)))
+        bad = np.nonzero(~(e <= bound))[0]
+        assert len(bad) == 0, (name, len(bad), bad[:5], e[bad[:5]], bound[bad[:5]])
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_long_dt_forests_vs_oracle(kernel):
+    """time steps of 1e3-1.6e4 units (gl dt up to ~700, where exp(-gl dt) nears the underflow and
+    the lane schedules' product exponentials could meet 0 x inf; they then form the 22 products from
+    their own arguments, ggp_prop.h lane_guard_products): two chained calls against the oracle --
+    within the bar while the oracle is finite, the same first NaN cell and row where the reference
+    algorithm itself breaks down (its tauint integrals overflow first: at 1.6e4 the second call)"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    P = CONFIGS[0][2]
+    for scale in (1000.0, 5000.0, 16000.0):
+        hf = g.HostForest.synthetic(20, 40, seed=5)
+        hf.a["time"] = hf.a["time"] * scale
+        fg, of = g.Forest(hf, kernel=kernel), O.OracleForest(hf.a)
+        for call in range(2):
+            vo, nc, nr = of.total_likelihood(P)
+            if math.isnan(vo):
+                with pytest.raises(g.LikelihoodIsNan) as e:
+                    fg.total_likelihood(P)
+                assert (e.value.cell, e.value.row) == (nc, nr), (scale, call)
+                break
+            vg = fg.total_likelihood(P)
+            assert _rel(vg, vo) < REL, (scale, call, vg, vo)
+        fg.close()

@@ -9,6 +9,7 @@ import json
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -324,3 +325,34 @@ def test_sparse_joints_converter_handcrafted(tmp_path):
             + "2,1,5," + v(4) + blank * 2 + "\n")
     assert out.read_text() == want
     assert J.read_sparse(str(sp))[(0, 1)][0] == 300.0
+
+
+_ONE_RUNTIME_CHILD = r'''
+import sys
+sys.path.insert(0, ROOT)
+from gfp_gaussian_process_amd import _native as N
+N.engine()
+
+
+def mapped(tag):
+    return sorted({ln.split()[-1] for ln in open("/proc/self/maps") if tag in ln and "/" in ln})
+
+
+after_engine = (mapped("libamdhip64"), mapped("libhsa-runtime64"))
+import torch  # noqa: E402,F401
+after_torch = (mapped("libamdhip64"), mapped("libhsa-runtime64"))
+print(repr((after_engine, after_torch)))
+'''
+
+
+def test_one_hip_runtime_per_process_engine_first():
+    """ADVICE r4: a process that loads the engine before torch maps exactly one libamdhip64 and one
+    libhsa-runtime64, before and after `import torch` (the preload of torch's runtime is taken only
+    when its SONAME is the one the engine needs: _native.elf_dynamic)"""
+    import ast
+    r = subprocess.run([sys.executable, "-c", f"ROOT={ROOT!r}\n" + _ONE_RUNTIME_CHILD], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (hip_e, hsa_e), (hip_t, hsa_t) = ast.literal_eval(r.stdout.strip().splitlines()[-1])
+    assert len(hip_e) == 1 and len(hsa_e) == 1, (hip_e, hsa_e)
+    assert hip_t == hip_e and hsa_t == hsa_e, (hip_t, hsa_t)
