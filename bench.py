@@ -367,6 +367,45 @@ def main() -> int:
     total_rows = rows_rank * world * args.steps
     value = total_rows / el
 
+    # ---- N > 1: what the one collective per call costs: the same K steps without it
+    # (each rank's own evaluation only), with torch's all_gather (the headline's path) and, nccl
+    # only, with the engine's RCCL all-gather (ggp_comm_attach, its own handle; a failure is
+    # reported, not raised); microseconds per call = the difference of the max-over-ranks times ----
+    coll = None
+    if world > 1:
+        def timed_steps(fn):
+            for _ in range(3):
+                fn(P_EXAMPLE)
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                fn(P_EXAMPLE)
+            barrier()
+            tt = time.perf_counter() - t1
+            t = torch.tensor([tt], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) / args.steps
+        local_s = timed_steps(fg.total_likelihood)
+        coll = {"ranks": dist.get_world_size(), "backend": args.backend,
+                "local_only_ms_per_step": 1e3 * local_s, "torch_all_gather_ms_per_step": 1e3 * el / args.steps,
+                "torch_all_gather_us_per_call": 1e6 * (el / args.steps - local_s)}
+        if args.backend == "nccl" and args.engine_comm_leg:
+            os.environ.setdefault("GGP_COMM_TIMEOUT_S", "60")
+            try:
+                fe2 = g.Forest(hf, device=local, kernel=args.kernel)
+                oe2 = ShardedObjective(fe2, engine_comm=True)
+                if oe2.engine:
+                    eng_s = timed_steps(oe2.total_likelihood)
+                    coll.update({"engine_rccl_ms_per_step": 1e3 * eng_s,
+                                 "engine_rccl_us_per_call": 1e6 * (eng_s - local_s),
+                                 "engine_rccl_value": rows_rank * world / eng_s,
+                                 "rccl_comm_count": fe2.comm_size()})
+                else:
+                    coll["engine_rccl_error"] = "the engine's RCCL path was unavailable on some rank"
+                fe2.close()
+            except Exception as e:   # reported in the line: the headline stands either way
+                coll["engine_rccl_error"] = repr(e)[-400:]
+
     # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
     fg.enable_profile()
     per = {}                                   # kernel name -> [ms, rows, launches]
@@ -796,6 +835,10 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic_for(dom, args),
+                "traffic_source": "rocprofv3 PMC FETCH_SIZE + WRITE_SIZE per launch (profiles/traffic.json, this build): "
+                                  "bytes between L2 and the fabric, not HBM bytes -- part of the 4.8 MB forest stays "
+                                  "in L2 / the Infinity Cache from one launch to the next, so the fetch side sits "
+                                  "below the algorithmic reads",
                 "bytes_per_update": BYTES_PER_UPDATE,
                 "avg_launch_ms": avg_ms,
                 "launches_timed": d_n,
@@ -824,6 +867,8 @@ def main() -> int:
             result["joints_c5_subset"] = jc5
         if inproc is not None:
             result["inprocess"] = inproc
+        if coll is not None:
+            result["collective"] = coll
         if c4s is not None:
             result["c4_strong"] = c4s
         if c5s is not None:

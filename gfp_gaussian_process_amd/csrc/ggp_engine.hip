@@ -2505,6 +2505,11 @@ struct Shard {
     int64_t *m_seq = nullptr;
     volatile unsigned long long *h_clk = nullptr;   // path launches: block 0's clock counters
     unsigned long long *m_clk = nullptr;
+    // the largest |dt| of any propagation of the shard (in-cell steps and divisions): with the
+    // parameters it bounds |k dt| for the wave schedule's product factors exp(-gl dt), exp(-gq dt),
+    // exp(-b dt), exp(gq dt) (wave_products_risky)
+    double max_dt = 0.0;
+    bool used_path = false;                         // the last launch_levels took the path launch
     int64_t seq = 0;
     bool seq_pending = false;
     bool spin = true;
@@ -2624,6 +2629,20 @@ int level_kind(const Shard *f, int64_t n)
     return n <= f->pair_max_cells ? GGP_KERNEL_PAIR : GGP_KERNEL_LANE;
 }
 
+// The wave schedule forms 22 exponentials as products exp(c_rep + ...) exp(+-k dt).  Beyond
+// |k dt| ~ 700 a factor under- or overflows while the direct exponential may not (the lane
+// schedules guard this per step: ggp_prop.h lane_guard_products; the wave, one cell per wave, has
+// no room for a second form).  So an evaluation whose parameters reach |k| max_dt > 200 anywhere
+// on the shard runs its wave levels on the lane-pair (or lane) schedule -- the same values to the
+// bar -- and its chains call by call: a dt of days at the example's rates, where the reference's
+// own integrals overflow soon after (tests/test_gpu_parity.py long-dt test)
+constexpr double kWaveProductSafe = 200.0;
+bool wave_products_risky(const Shard *f, const double *p)
+{
+    const double k = std::max(std::fabs(p[1]), std::max(std::fabs(p[4]), std::fabs(p[6])));
+    return !(k * f->max_dt <= kWaveProductSafe);
+}
+
 int launch_levels(Shard *f, const ggp_params &P)
 {
     const int n_levels = (int)f->level_start.size() - 1;
@@ -2643,7 +2662,9 @@ int launch_levels(Shard *f, const ggp_params &P)
         }
         return hipSuccess;
     };
-    if (f->n_paths > 0) {   // every level on the wave schedule: one launch, one block per path
+    const bool risky = wave_products_risky(f, P.p);
+    f->used_path = f->n_paths > 0 && !risky;
+    if (f->used_path) {   // every level on the wave schedule: one launch, one block per path
         HIPCHK(prof_begin());
         hipLaunchKernelGGL(k_loglik_wave<false>, dim3((unsigned)f->n_paths), dim3(64), 0, f->stream, f->F, P,
                            f->d_path_cells, (int)f->n_cells, f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain,
@@ -2661,7 +2682,8 @@ int launch_levels(Shard *f, const ggp_params &P)
         if (n <= 0) continue;
         HIPCHK(prof_begin());
         const int64_t n_simd = (int64_t)f->n_cu * 4;
-        const int kind = f->level_kind[L];
+        int kind = f->level_kind[L];
+        if (kind == GGP_KERNEL_WAVE && risky) kind = n <= f->pair_max_cells ? GGP_KERNEL_PAIR : GGP_KERNEL_LANE;
         if (kind == GGP_KERNEL_WAVE) {
             hipLaunchKernelGGL(k_loglik_wave<false>, dim3(n), dim3(64), 0, f->stream, f->F, P, f->d_level_cells + a, n,
                                f->d_state, f->d_cell_ll, f->d_cell_nan, f->d_chain, f->d_cell_done, f->epoch,
@@ -2729,7 +2751,7 @@ int shard_launch(Shard *s, const ggp_params &P)
     ++s->seq;
     const int rc = launch_levels(s, P);
     if (rc != GGP_OK) return rc;
-    if (s->n_paths > 0) {   // the path launch reduced in-launch
+    if (s->used_path) {   // the path launch reduced in-launch
         s->seq_pending = true;
         return GGP_OK;
     }
@@ -3002,6 +3024,12 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
     if (nc == 0) f->row_off.assign(1, 0);
+    for (int64_t c = 0; c < nc; ++c) {
+        const int64_t a = d->row_offset[c], b = d->row_offset[c + 1];
+        for (int64_t r = a + 1; r < b; ++r) f->max_dt = std::max(f->max_dt, std::fabs(d->time[r] - d->time[r - 1]));
+        if (d->parent[c] >= 0 && b > a)
+            f->max_dt = std::max(f->max_dt, std::fabs(d->time[a] - d->time[d->row_offset[d->parent[c] + 1] - 1]));
+    }
     if (hipSetDevice(f->device) != hipSuccess) {
         g_last_err = "hipSetDevice failed";
         delete f;
@@ -4090,12 +4118,15 @@ int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, d
 // chained points on the path-launch shards: np points of params, point i's roots from the state
 // point pred[i] left (pred NULL: i - 1; -1: the carried state); per shard its block sums and
 // first-NaN codes per point, on the host once the shards are synchronised
-static bool chain_fusable(const ggp_forest *f)
+static bool chain_fusable(const ggp_forest *f, int64_t np = 0, const double *params = nullptr)
 {
     bool fused = f->comm == nullptr;
     if (const char *e = std::getenv("GGP_CHAIN_FUSED")) fused = fused && std::atoi(e) != 0;
-    for (const Shard *s : f->shards)
+    for (const Shard *s : f->shards) {
         if (s->n_cells && s->n_paths == 0) fused = false;
+        for (int64_t i = 0; fused && s->n_cells && i < np; ++i)
+            if (wave_products_risky(s, params + 11 * i)) fused = false;   // launch_levels' other schedules
+    }
     return fused;
 }
 
@@ -4197,7 +4228,7 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
     if (nan_cell) *nan_cell = -1;
     if (nan_row) *nan_row = -1;
     f->tree_pts = 0;
-    if (!chain_fusable(f) || f->n_cells == 0) {
+    if (!chain_fusable(f, n_pts, params) || f->n_cells == 0) {
         for (int32_t i = 0; i < n_pts; ++i) {
             const int rc = ggp_total_loglik(f, params + (size_t)11 * i, ll + i, nan_cell, nan_row);
             if (rc != GGP_OK) return rc;
@@ -4275,8 +4306,9 @@ int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, co
             return GGP_EINVAL;
         }
     f->tree_pts = 0;
-    if (!chain_fusable(f)) {
-        g_last_err = "ggp_total_loglik_tree: the handle has no path launch (or is attached to a communicator)";
+    if (!chain_fusable(f, n_pts, params)) {
+        g_last_err = "ggp_total_loglik_tree: the handle has no path launch (or is attached to a communicator, or "
+                     "the points' rates x dt leave the wave schedule's product range)";
         return GGP_EINVAL;
     }
     if (n_pts == 0) return GGP_OK;

