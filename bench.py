@@ -242,6 +242,25 @@ def example_parity_child() -> int:
     return 0
 
 
+def run_example_parity() -> dict:
+    """The example's parity (north star's parity config) on this process's engine and, in a child
+    process, on the exact-arithmetic engine; errors are reported in the result, not raised"""
+    import subprocess
+    try:
+        out = {"default_engine": example_parity(("auto", "lane"))}
+    except Exception as e:
+        out = {"default_engine": {"error": repr(e)[-300:]}}
+    envx = dict(os.environ, GGP_ENGINE_LIB="libggp_exact.so")
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--example-parity-child"],
+                           capture_output=True, text=True, timeout=600, env=envx)
+        out["exact_engine"] = (json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else
+                               {"error": (r.stdout + r.stderr)[-400:]})
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        out["exact_engine"] = {"error": repr(e)[-300:]}
+    return out
+
+
 def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: bool = False, note: str = ""):
     """FP64 and VALU-issue fractions of a bench leg from the PMC pass of this build
     (profiles/fp64_counts.json, tools/fp64_summary.py kind `kind`): achieved FP64 = flops per row x
@@ -874,20 +893,7 @@ def main() -> int:
         if c5s is not None:
             result["c5_predict_split"] = c5s
         if world == 1 and args.example_parity:
-            try:
-                result["example_parity"] = {"default_engine": example_parity(("auto", "lane"))}
-            except Exception as e:
-                result["example_parity"] = {"default_engine": {"error": repr(e)[-300:]}}
-            import subprocess
-            envx = dict(os.environ, GGP_ENGINE_LIB="libggp_exact.so")
-            try:
-                r = subprocess.run([sys.executable, os.path.abspath(__file__), "--example-parity-child"],
-                                   capture_output=True, text=True, timeout=600, env=envx)
-                result["example_parity"]["exact_engine"] = (json.loads(r.stdout.strip().splitlines()[-1])
-                                                            if r.returncode == 0 else
-                                                            {"error": (r.stdout + r.stderr)[-400:]})
-            except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
-                result["example_parity"]["exact_engine"] = {"error": repr(e)[-300:]}
+            result["example_parity"] = run_example_parity()
         if world == 1 and not args.no_cpu:
             fresh = g.Forest(hf, device=local, kernel=args.kernel).total_likelihood(P_EXAMPLE)
             ref, rate, n_eval, cel = cpu_baseline(hf, args.cpu_budget)

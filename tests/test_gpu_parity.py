@@ -232,7 +232,7 @@ def test_irregular_sampling_predict_vs_oracle():
     import gfp_gaussian_process_amd as g
     hf = g.HostForest.synthetic(30, 40, seed=4)
     _irregular_times(hf, 2)
-    _check_predict(hf, CONFIGS[0][2])
+    _check_predict(hf, CONFIGS[0][2], "irregular")
 
 
 def test_empty_forest():
@@ -379,8 +379,34 @@ def test_pair_schedule_c4_shard_bitwise_and_auto():
 # Tolerance: means relative to (|m| + sd), covariances relative to sqrt(Cii Cjj).  The
 # smoother inherits the latent-q sensitivity of the propagator (+-1 ulp on every exp moves
 # the normalised state by ~4e-7, see test_example_state_matches_oracle) and adds five 4x4
-# inverses per row; 1e-5 leaves an order of magnitude of margin.
+# inverses per row.  PRED_TOL is the ceiling; each case is held at twice the distance measured on
+# the MI355X for its (output, mean / covariance), capped by the ceiling (profiles/r36_pred_err.txt:
+# the engine is deterministic, so the factor 2 is room for an ulp-level change of the kernels, not
+# for run-to-run noise).  The example's const/gauss combined covariance (8.8e-6) keeps the ceiling.
 PRED_TOL = 1e-5
+PRED_MEASURED = {   # case: {output: (mean, covariance)} worst normalised distance from the oracle, r36
+    "irregular": {"forward": (1.358e-08, 9.024e-08), "backward": (3.600e-08, 4.114e-07),
+                  "combined": (3.248e-08, 3.249e-07)},
+    "example/scaled/binomial": {"forward": (8.247e-07, 8.968e-07), "backward": (1.407e-06, 3.496e-06),
+                                "combined": (2.370e-06, 3.799e-06)},
+    "example/const/gauss": {"forward": (1.023e-06, 1.398e-06), "backward": (3.339e-06, 7.092e-06),
+                            "combined": (3.598e-06, 8.794e-06)},
+    "segments": {"forward": (4.134e-09, 7.250e-08), "backward": (1.686e-08, 2.431e-07),
+                 "combined": (1.164e-08, 2.164e-07)},
+    "four_segments": {"forward": (6.272e-09, 6.180e-08), "backward": (1.251e-08, 3.304e-07),
+                      "combined": (1.215e-08, 2.871e-07)},
+    "ragged": {"forward": (1.190e-09, 2.430e-08), "backward": (1.608e-09, 6.001e-08),
+               "combined": (1.976e-09, 4.275e-08)},
+    "fixture": {"forward": (1.797e-07, 3.975e-07), "backward": (7.091e-07, 1.284e-06),
+                "combined": (2.146e-07, 1.194e-06)},
+    "c5_shard": {"combined": (1.431e-06, 1.893e-06)},
+}
+
+
+def pred_bound(case: str, output: str):
+    """(mean, covariance) bound of one case's output: 2x its measured distance, at most PRED_TOL"""
+    em, ec = PRED_MEASURED[case][output]
+    return min(PRED_TOL, 2 * em), min(PRED_TOL, 2 * ec)
 
 
 def _smoother_err(a, b):
@@ -392,7 +418,7 @@ def _smoother_err(a, b):
     return float(em), float(ec)
 
 
-def _check_predict(hf, params):
+def _check_predict(hf, params, case):
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     got = g.Forest(hf).predict(params)
@@ -401,13 +427,15 @@ def _check_predict(hf, params):
         assert np.all(np.isfinite(y)), name
         assert np.all(np.isfinite(x)), name
         em, ec = _smoother_err(x, y)
-        assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
+        bm, bc = pred_bound(case, name)
+        print(f"PRED_ERR {case} {name} mean {em:.3e} (bound {bm:.1e}) cov {ec:.3e} (bound {bc:.1e})")
+        assert em < bm and ec < bc, (case, name, em, ec)
 
 
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
 def test_predict_example_vs_oracle(example_forests, noise, div):
     params = next(p for n, d, p in CONFIGS if (n, d) == (noise, div))
-    _check_predict(example_forests[(noise, div)], params)
+    _check_predict(example_forests[(noise, div)], params, f"example/{noise}/{div}")
 
 
 def test_predict_segments_vs_oracle():
@@ -421,7 +449,7 @@ def test_predict_segments_vs_oracle():
     P1[0] *= 1.1
     P1[3] *= 0.95
     P1[7] *= 1.2
-    _check_predict(hf, np.stack([P0, P1]))
+    _check_predict(hf, np.stack([P0, P1]), "segments")
 
 
 @pytest.mark.parametrize("lane_smoother", [False, True])
@@ -439,7 +467,7 @@ def test_predict_four_segments_vs_oracle(lane_smoother, monkeypatch):
     P0 = np.array(CONFIGS[0][2])
     rng = np.random.default_rng(5)
     params = np.stack([P0 * np.exp(rng.uniform(-0.1, 0.1, 11)) if k else P0 for k in range(4)])
-    _check_predict(hf, params)
+    _check_predict(hf, params, "four_segments")
 
 
 @pytest.mark.parametrize("which", ["example", "segments", "ragged", "wide"])
@@ -503,7 +531,7 @@ def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
     """k_combine's fast form (the default: reciprocal pivots, reassociated mean) against the
     same kernel with the oracle's operations (GGP_COMBINE_EXACT=1): forward and backward rows
     bitwise (only the combine differs), combined rows within 1e-9 in the smoother check's
-    normalisation, and both within PRED_TOL of the oracle"""
+    normalisation, and both within the example's combined-row bound of the oracle (pred_bound)"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     hf = example_forests[(noise, div)]
@@ -515,13 +543,15 @@ def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
     em, ec = _smoother_err(got[2], exact[2])
     assert em < 1e-9 and ec < 1e-9, (em, ec)
     ref = O.OracleForest(hf.a).predict(params)[2]
+    bm, bc = pred_bound(f"example/{noise}/{div}", "combined")
     for x in (got[2], exact[2]):
         em, ec = _smoother_err(x, ref)
-        assert em < PRED_TOL and ec < PRED_TOL, (em, ec)
+        print(f"PRED_ERR combine_form mean {em:.3e} cov {ec:.3e}")
+        assert em < bm and ec < bc, (em, ec)
 
 
 def test_predict_ragged_and_single_rows():
-    _check_predict(_ragged_roots(), CONFIGS[0][2])
+    _check_predict(_ragged_roots(), CONFIGS[0][2], "ragged")
 
 
 def test_predict_leaves_carried_state_alone(example_forests):
@@ -706,7 +736,9 @@ def test_predict_example_vs_committed_fixture(example_forests):
     rows = gold["rows"]
     for name, x in zip(("fwd", "bwd", "comb"), got):
         em, ec = _smoother_err(x[rows], gold[name])
-        assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
+        bm, bc = pred_bound("fixture", {"fwd": "forward", "bwd": "backward", "comb": "combined"}[name])
+        print(f"PRED_ERR fixture {name} mean {em:.3e} cov {ec:.3e}")
+        assert em < bm and ec < bc, (name, em, ec)
 
 
 def test_tests_h_cell_vs_committed_fixture():
