@@ -33,5 +33,7 @@ t_batch, _ = timed(lambda: f.total_likelihood_batch(pts), 3)
 f.close()
 f = g.Forest(g.HostForest.synthetic(20000, 500))
 t_pred, _ = timed(lambda: f.predict(P, outputs=(False, False, False)), 3)
-print(f"{sys.argv[1]}: lane 40k {t_lane:.3f} ms  batch484 {t_batch:.3f} ms  predict 20k x 500 {t_pred:.3f} ms  ll={v!r}",
-      flush=True)
+import hashlib  # noqa: E402
+h = hashlib.sha1(f.predict_rows(0, 400000).tobytes()).hexdigest()[:12]   # the combined rows, bitwise
+print(f"{sys.argv[1]}: lane 40k {t_lane:.3f} ms  batch484 {t_batch:.3f} ms  predict 20k x 500 {t_pred:.3f} ms  ll={v!r}"
+      f"  rows sha1 {h}", flush=True)
