@@ -978,3 +978,37 @@ def test_long_dt_forests_vs_oracle(kernel):
             vg = fg.total_likelihood(P)
             assert _rel(vg, vo) < REL, (scale, call, vg, vo)
         fg.close()
+
+
+@pytest.mark.parametrize("kernel", ["lane", "pair", "group"])
+def test_mixed_long_dt_waves_bitwise(kernel, monkeypatch):
+    """every fourth tree's times stretched x2000 (its steps risky: |gq dt| > 700, ggp_prop.h
+    products_risky): a lane-schedule wave holding such a cell runs the step with its products
+    materialised and guarded (propagate_lane's wave-uniform branch), a wave without one forms them at
+    the integrals' reads.  The ordinary trees' carried state and -p rows (lane smoother) in the mixed
+    forest equal, bitwise, the same trees evaluated alone (every wave ordinary); the mixed total is
+    within the bar of the oracle"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    monkeypatch.setenv("GGP_SMOOTHER_LANE", "1")
+    P = CONFIGS[0][2]
+    hf = g.HostForest.synthetic(256, 40, seed=3)
+    tree = hf.tree_of_cell()
+    roots = hf.roots
+    long_roots, plain_roots = roots[::4], np.setdiff1d(roots, roots[::4])
+    ro = hf.a["row_offset"]
+    for c in np.nonzero(np.isin(tree, long_roots))[0]:
+        hf.a["time"][ro[c]:ro[c + 1]] = hf.a["time"][ro[c]:ro[c + 1]] * 2000.0
+    sub = hf.subset_trees(plain_roots)
+    fm, fs = g.Forest(hf, kernel=kernel), g.Forest(sub, kernel=kernel)
+    vm = fm.total_likelihood(P)
+    fs.total_likelihood(P)
+    vo = O.OracleForest(hf.a).total_likelihood(P)[0]
+    assert math.isfinite(vo) and _rel(vm, vo) < REL, (vm, vo)
+    keep = np.nonzero(np.isin(tree, plain_roots))[0]
+    assert np.array_equal(fm.state()[keep], fs.state())
+    rows = np.concatenate([np.arange(ro[c], ro[c + 1]) for c in keep])
+    for a, b in zip(fm.predict(P), fs.predict(P)):
+        assert np.array_equal(a[rows], b)
+    fm.close()
+    fs.close()
