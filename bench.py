@@ -15,6 +15,12 @@ largest share of the evaluation), timed with HIP events on the engine's own stre
 that launch time against the FP64 work per update counted by PMC on this same build
 (profiles/fp64_counts.json); `cpu_baseline` is the CPU oracle (oracle/, a C port of the
 reference path) timed on this host, single-threaded (as the reference) and tree-parallel.
+
+Order: the C2 forest is made resident, then the C4 strong-scaling leg runs (BASELINE configs[3],
+~0.3 s of full-chip work), then the W warm-up and the K timed C2 steps, then the other legs.  The
+C4 leg first means the headline runs at the shader clock the path sustains in a minimisation, not
+the lower clock the first tens of milliseconds after idle hold (DESIGN.md §6 "The clock"); the
+line's `clock` field reports the clock of the timed launches either way.
 """
 from __future__ import annotations
 
@@ -368,6 +374,70 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---- strong scaling, BASELINE configs[3] (C4): ONE forest of --c4-trees x --rows split over the
+    # N ranks by whole trees (contiguous blocks: every tree has the same rows, so this is the LPT
+    # split), the init statistics of the whole forest on every rank (one all_reduce at setup); one
+    # evaluation per step with one all_gather of the partials; then the chained -s scan
+    # (main.cpp:77-112) -- every rank chains its shard, one all_gather of the per-sample partials.
+    # It runs before the C2 headline: ~0.3 s of full-chip work, after which the headline's K steps
+    # run at the shader clock the path sustains in a minimisation (2.37-2.39 GHz) rather than the
+    # ~2.2 GHz the first tens of milliseconds after idle hold (DESIGN.md §6 "The clock"; the line's
+    # `clock` field records it either way; --c4-trees 0 skips it) ----
+    c4s = None
+    if args.c4_trees > 0:
+        from gfp_gaussian_process_amd.distributed import global_init_stats
+        from gfp_gaussian_process_amd.optimize import arange
+        T4 = args.c4_trees
+        lo4, hi4 = rank * T4 // world, (rank + 1) * T4 // world
+        h4 = g.HostForest.synthetic(hi4 - lo4, args.rows, seed=SEED, first_tree=3 * 10 ** 6 + lo4)
+        if world > 1:
+            global_init_stats(h4)
+        f4 = g.Forest(h4, device=local, kernel=args.kernel)
+        o4 = ShardedObjective(f4)
+        for _ in range(3):
+            o4.total_likelihood(P_EXAMPLE)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.c4_steps):
+            ll4 = o4.total_likelihood(P_EXAMPLE)
+        barrier()
+        el4 = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
+        rows4 = torch.tensor([h4.n_rows], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(rows4)
+        rows4 = int(rows4.item())
+        c4s = {"config": f"BASELINE configs[3] (C4): {T4} trees x {args.rows} tp, one forest split over "
+                         f"{world} rank(s) by whole trees; the init statistics of the whole forest",
+               "trees": T4, "rows": rows4, "trees_per_rank": hi4 - lo4, "steps": args.c4_steps,
+               "ms_per_eval": 1e3 * el4, "updates_per_s": rows4 / el4, "scaling": "strong",
+               "total_log_likelihood": ll4, "levels": f4.info()["levels"],
+               "collective": {"kind": "torch all_gather_into_tensor of 16 B per rank, rank-order sum",
+                              "backend": args.backend if world > 1 else None,
+                              "ranks": dist.get_world_size() if world > 1 else 1}}
+        if args.c4_scan > 0:
+            P4 = np.array(P_EXAMPLE)
+            samples = arange(1.0e-03, 8.0e-02, (8.0e-02 - 1.0e-03) / args.c4_scan)[: args.c4_scan]
+            pts = np.repeat(P4[None, :], len(samples), axis=0)
+            pts[:, 1] = samples
+            f4.reset_state()
+            barrier()
+            t1 = time.perf_counter()
+            scan = o4.total_likelihood_chain(pts)
+            barrier()
+            sel4 = max_over_ranks(time.perf_counter() - t1)
+            c4s["scan"] = {"parameter": "gamma_lambda", "samples": len(samples), "seconds": sel4,
+                           "updates_per_s": len(samples) * rows4 / sel4, "first": float(scan[0]),
+                           "last": float(scan[-1]),
+                           "note": "-s: each sample from the carried state the previous left; every rank "
+                                   "chains its trees (ggp_total_loglik_chain), one all_gather of the partials"}
+        f4.close()
     for _ in range(args.warmup):
         obj.total_likelihood(P_EXAMPLE)
 
@@ -424,6 +494,36 @@ def main() -> int:
                 fe2.close()
             except Exception as e:   # reported in the line: the headline stands either way
                 coll["engine_rccl_error"] = repr(e)[-400:]
+
+    if c4s is not None:
+        if world > 1 and args.backend == "nccl" and args.engine_comm_leg:
+            # the engine's own RCCL path (include/ggp.h ggp_comm_attach), after the headline and the
+            # torch leg; a wait inside it is bounded by GGP_COMM_TIMEOUT_S and reported, not raised
+            os.environ.setdefault("GGP_COMM_TIMEOUT_S", "60")
+            eng = {}
+            try:
+                fe = g.Forest(h4, device=local, kernel=args.kernel)
+                oe = ShardedObjective(fe, engine_comm=True)
+                if not oe.engine:
+                    eng["error"] = "the engine's RCCL path was unavailable on some rank (torch's path kept)"
+                else:
+                    eng["rccl_comm_count"] = fe.comm_size()
+                    for _ in range(3):
+                        oe.total_likelihood(P_EXAMPLE)
+                    barrier()
+                    t1 = time.perf_counter()
+                    for _ in range(args.c4_steps):
+                        lle = oe.total_likelihood(P_EXAMPLE)
+                    barrier()
+                    ele = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
+                    eng.update({"ms_per_eval": 1e3 * ele, "updates_per_s": rows4 / ele,
+                                "total_log_likelihood": lle, "same_total_as_torch_path": lle == ll4})
+                fe.close()
+            except Exception as e:   # reported in the line: the headline stands either way
+                eng["error"] = repr(e)[-400:]
+            eng["kind"] = "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
+            c4s["engine_rccl"] = eng
+        del h4
 
     # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
     fg.enable_profile()
@@ -694,94 +794,6 @@ def main() -> int:
                        "the GPU and copied to the host (72 doubles each), parameter tables cached per parameters"}
         fj.close()
 
-    def max_over_ranks(x: float) -> float:
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    # ---- strong scaling, BASELINE configs[3] (C4): ONE forest of --c4-trees x --rows split over the
-    # N ranks by whole trees (contiguous blocks: every tree has the same rows, so this is the LPT
-    # split), the init statistics of the whole forest on every rank (one all_reduce at setup); one
-    # evaluation per step with one all_gather of the partials; then the chained -s scan
-    # (main.cpp:77-112) -- every rank chains its shard, one all_gather of the per-sample partials ----
-    c4s = None
-    if args.c4_trees > 0:
-        from gfp_gaussian_process_amd.distributed import global_init_stats
-        from gfp_gaussian_process_amd.optimize import arange
-        T4 = args.c4_trees
-        lo4, hi4 = rank * T4 // world, (rank + 1) * T4 // world
-        h4 = g.HostForest.synthetic(hi4 - lo4, args.rows, seed=SEED, first_tree=3 * 10 ** 6 + lo4)
-        if world > 1:
-            global_init_stats(h4)
-        f4 = g.Forest(h4, device=local, kernel=args.kernel)
-        o4 = ShardedObjective(f4)
-        for _ in range(3):
-            o4.total_likelihood(P_EXAMPLE)
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.c4_steps):
-            ll4 = o4.total_likelihood(P_EXAMPLE)
-        barrier()
-        el4 = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
-        rows4 = torch.tensor([h4.n_rows], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(rows4)
-        rows4 = int(rows4.item())
-        c4s = {"config": f"BASELINE configs[3] (C4): {T4} trees x {args.rows} tp, one forest split over "
-                         f"{world} rank(s) by whole trees; the init statistics of the whole forest",
-               "trees": T4, "rows": rows4, "trees_per_rank": hi4 - lo4, "steps": args.c4_steps,
-               "ms_per_eval": 1e3 * el4, "updates_per_s": rows4 / el4, "scaling": "strong",
-               "total_log_likelihood": ll4, "levels": f4.info()["levels"],
-               "collective": {"kind": "torch all_gather_into_tensor of 16 B per rank, rank-order sum",
-                              "backend": args.backend if world > 1 else None,
-                              "ranks": dist.get_world_size() if world > 1 else 1}}
-        if args.c4_scan > 0:
-            P4 = np.array(P_EXAMPLE)
-            samples = arange(1.0e-03, 8.0e-02, (8.0e-02 - 1.0e-03) / args.c4_scan)[: args.c4_scan]
-            pts = np.repeat(P4[None, :], len(samples), axis=0)
-            pts[:, 1] = samples
-            f4.reset_state()
-            barrier()
-            t1 = time.perf_counter()
-            scan = o4.total_likelihood_chain(pts)
-            barrier()
-            sel4 = max_over_ranks(time.perf_counter() - t1)
-            c4s["scan"] = {"parameter": "gamma_lambda", "samples": len(samples), "seconds": sel4,
-                           "updates_per_s": len(samples) * rows4 / sel4, "first": float(scan[0]),
-                           "last": float(scan[-1]),
-                           "note": "-s: each sample from the carried state the previous left; every rank "
-                                   "chains its trees (ggp_total_loglik_chain), one all_gather of the partials"}
-        f4.close()
-        if world > 1 and args.backend == "nccl" and args.engine_comm_leg:
-            # the engine's own RCCL path (include/ggp.h ggp_comm_attach), after the headline and the
-            # torch leg; a wait inside it is bounded by GGP_COMM_TIMEOUT_S and reported, not raised
-            os.environ.setdefault("GGP_COMM_TIMEOUT_S", "60")
-            eng = {}
-            try:
-                fe = g.Forest(h4, device=local, kernel=args.kernel)
-                oe = ShardedObjective(fe, engine_comm=True)
-                if not oe.engine:
-                    eng["error"] = "the engine's RCCL path was unavailable on some rank (torch's path kept)"
-                else:
-                    eng["rccl_comm_count"] = fe.comm_size()
-                    for _ in range(3):
-                        oe.total_likelihood(P_EXAMPLE)
-                    barrier()
-                    t1 = time.perf_counter()
-                    for _ in range(args.c4_steps):
-                        lle = oe.total_likelihood(P_EXAMPLE)
-                    barrier()
-                    ele = max_over_ranks((time.perf_counter() - t1) / args.c4_steps)
-                    eng.update({"ms_per_eval": 1e3 * ele, "updates_per_s": rows4 / ele,
-                                "total_log_likelihood": lle, "same_total_as_torch_path": lle == ll4})
-                fe.close()
-            except Exception as e:   # reported in the line: the headline stands either way
-                eng["error"] = repr(e)[-400:]
-            eng["kind"] = "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
-            c4s["engine_rccl"] = eng
-        del h4
 
     # ---- strong scaling, BASELINE configs[4] (C5): -p over ONE forest of --c5-trees x --predict-rows
     # split over the N ranks (no collective on the data path: every rank smooths its trees, the rows
