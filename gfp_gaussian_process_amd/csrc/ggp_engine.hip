@@ -1613,9 +1613,15 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
         const double t_r = F.time[r], t_prev = r > r0 ? F.time[r - 1] : 0.0;
         const double *q_next = r > r0 ? seg_params(F, ptab, n_seg, r - 1) : pq;
         int sp = 0;
+        double mf[4], Cf[16];   // COMB: the row's forward posterior, its loads in flight across the propagation
         if constexpr (COMB) {
             sp = prior_seg[r];
             if (sp < 0 || sp >= n_seg) sp = 0;
+            const double *fr = fwd + (size_t)20 * r;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) mf[k] = fr[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) Cf[k] = fr[4 + k];
         }
         if (pend) {
             if (pq != ou_src) {
@@ -1632,12 +1638,6 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
         ggp::reverse_state(rm, rC);
         if (!COMB || out) store20(out + (size_t)20 * r, rm, rC);  // the prior, before the update
         if constexpr (COMB) {   // k_combine<true> on this row
-            double mf[4], Cf[16];
-            const double *fr = fwd + (size_t)20 * r;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) mf[k] = fr[k];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) Cf[k] = fr[4 + k];
             ggp::combine_info(mf, Cf, rm, rC, ptab + 11 * sp);
             store20(comb + (size_t)20 * r, mf, Cf);
         }
