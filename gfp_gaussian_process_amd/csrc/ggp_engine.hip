@@ -1475,6 +1475,13 @@ GGP_DEV const double *seg_params(const DevForest &F, const double *ptab, int n_s
     return ptab + 11 * s;
 }
 
+// a row's parameter row from its raw segment index, clamped as seg_params clamps it
+GGP_DEV const double *seg_row(const double *ptab, int n_seg, int s)
+{
+    if (s < 0 || s >= n_seg) s = 0;
+    return ptab + 11 * s;
+}
+
 GGP_DEV void store20(double *dst, const double *m, const double *C)
 {
 #pragma unroll
@@ -1483,14 +1490,36 @@ GGP_DEV void store20(double *dst, const double *m, const double *C)
     for (int k = 0; k < 16; ++k) dst[4 + k] = C[k];
 }
 
+// The lane smoother's row loop is pipelined one row ahead: row r - 1's (backward) or r + 1's
+// (forward) data, segment, time and forward row are loaded at the end of row r, before row r's
+// stores.  vmcnt counts loads and stores in issue order, so a wait for a load issued after a store
+// drains the store too: loaded first, the next row's operands are waited for without it, and they
+// arrive behind this row's propagation.  SL: the parameter rows staged in LDS (n_seg <= kSegLds:
+// the CLI's -b segments), so the per-row parameter reads are LDS reads, outside vmcnt altogether.
+constexpr int kSegLds = 32;
+
+template <bool SL>
+GGP_DEV const double *stage_params(double *s_par, const double *ptab, const int n_seg, const int lane)
+{
+    if constexpr (SL) {
+        for (int k = lane; k < 11 * n_seg; k += 64) s_par[k] = ptab[k];
+        return s_par;
+    } else {
+        return ptab;
+    }
+}
+
 // prediction_forward / sc_prediction_forward (predictions.h:93-173)
+template <bool SL>
 __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
                                                   const int32_t *__restrict__ cells, int n, int cpw,
                                                   double *__restrict__ pstate, double *__restrict__ out)
 {
     __shared__ double s_tab[kDawsonTab];
+    __shared__ double s_par[SL ? 11 * kSegLds : 1];
     const int lane = threadIdx.x;
     load_dawson_table(s_tab, lane);
+    const double *PT = stage_params<SL>(s_par, ptab, n_seg, lane);
     __syncthreads();
     if (lane >= cpw) return;
     const int i = blockIdx.x * cpw + lane;
@@ -1499,7 +1528,7 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
     const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
     const int par = F.parent[c];
     // root: segment of its first row; daughter: the parent's last segment (:103-108)
-    const double *pi = seg_params(F, ptab, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);
+    const double *pi = seg_params(F, PT, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);
     double m[4], C[16], dt = 0.0;
     bool pending = cell_prologue(F, pi, pstate, c, r0, m, C, dt);
     bool divide = pending;
@@ -1508,11 +1537,17 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
     const double *ou_src = nullptr;
     ggp::OU ou{};
     double t_cur = F.time[r0];
+    // row r's operands, loaded during row r - 1 (the look-ahead index is clamped to the cell's last
+    // row instead of a branch: the last row's look-ahead reads a valid row and nothing uses it)
+    const int64_t r_last = r1 - 1;
+    double y_l_n = F.logl[r0], y_f_n = F.fp[r0], t_nx_n = F.time[min(r0 + 1, r_last)];
+    int seg_n = F.seg ? F.seg[r0] : 0;
+    // the prologue's loads complete here, so the loop's waits are the look-ahead's alone
+    __builtin_amdgcn_s_waitcnt(0);
     for (int64_t r = r0; r < r1; ++r) {
-        // this row's data, parameters and the next row's time, loaded before the propagation
-        const double *p = seg_params(F, ptab, n_seg, r);
-        const double y_l = F.logl[r], y_f = F.fp[r], var_x = p[7], var_g = p[8];
-        const double t_next = r + 1 < r1 ? F.time[r + 1] : 0.0;
+        const double y_l = y_l_n, y_f = y_f_n, t_next = t_nx_n;
+        const double *p = seg_row(PT, n_seg, seg_n);
+        const double var_x = p[7], var_g = p[8];
         if (pending) {
             if (pprop != ou_src) {
                 ou = ggp::make_ou(pprop[0], pprop[1], pprop[2], pprop[3], pprop[4], pprop[5], pprop[6]);
@@ -1529,6 +1564,14 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
         ggp_innov v;
         ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
         ggp_posterior(m, C, x0, x1, v);
+        {   // row r + 1's operands, ahead of row r's store
+            const int64_t rn = min(r + 1, r_last);
+            y_l_n = F.logl[rn];
+            y_f_n = F.fp[rn];
+            t_nx_n = F.time[min(r + 2, r_last)];
+            if (F.seg) seg_n = F.seg[rn];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // the loads above issue before the store below
         store20(out + (size_t)20 * r, m, C);
         pending = r + 1 < r1;
         if (pending) dt = t_next - t_cur;
@@ -1543,7 +1586,7 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_fwd_level(DevForest F, con
 // row's backward prior is combined with its forward row as soon as it is formed, into comb; the
 // backward rows themselves are stored only when out is given.  The same operations per row as
 // k_combine<true>, so the combined rows are bitwise the separate kernel's.
-template <bool COMB>
+template <bool COMB, bool SL>
 __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, const double *__restrict__ ptab, int n_seg,
                                                   const int32_t *__restrict__ cells, int n, int cpw,
                                                   double *__restrict__ pstate, double *__restrict__ out,
@@ -1551,15 +1594,17 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
                                                   const double *__restrict__ fwd, double *__restrict__ comb)
 {
     __shared__ double s_tab[kDawsonTab];
+    __shared__ double s_par[SL ? 11 * kSegLds : 1];
     const int lane = threadIdx.x;
     load_dawson_table(s_tab, lane);
+    const double *PT = stage_params<SL>(s_par, ptab, n_seg, lane);
     __syncthreads();
     if (lane >= cpw) return;
     const int i = blockIdx.x * cpw + lane;
     if (i >= n) return;
     const int c = cells[i];
     const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
-    const double *pi = seg_params(F, ptab, n_seg, r1 - 1);          // :376-378
+    const double *pi = seg_params(F, PT, n_seg, r1 - 1);          // :376-378
     const int d1 = F.d1[c], d2 = F.d2[c];
     double m[4], C[16];
     // the propagation before row r's update (one call site: the division's and the rows' steps)
@@ -1605,24 +1650,32 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
     }
     const double *ou_src = nullptr;   // as k_fwd_level: the OU constants per segment change only
     ggp::OU ou{};
-    for (int64_t r = r1 - 1; r >= r0; --r) {
-        // this row's data and parameters, the previous row's time and parameters, and (fused) the
-        // row's prior segment, loaded before the propagation they would otherwise wait behind
-        const double *p = seg_params(F, ptab, n_seg, r);
-        const double y_l = F.logl[r], y_f = F.fp[r], var_x = p[7], var_g = p[8];
-        const double t_r = F.time[r], t_prev = r > r0 ? F.time[r - 1] : 0.0;
-        const double *q_next = r > r0 ? seg_params(F, ptab, n_seg, r - 1) : pq;
-        int sp = 0;
-        double mf[4], Cf[16];   // COMB: the row's forward posterior, its loads in flight across the propagation
+    // row r's operands, loaded during row r + 1 (k_fwd_level's pipeline, downwards; indices clamped
+    // to the cell's first row)
+    double y_l_n, y_f_n, t_r_n, t_prev_n, fw_n[20];
+    int seg_r_n, seg_p_n, sp_n = 0;
+    auto load_row = [&](const int64_t rr) {
+        const int64_t rp = max(rr - 1, r0);
+        y_l_n = F.logl[rr];
+        y_f_n = F.fp[rr];
+        t_r_n = F.time[rr];
+        t_prev_n = F.time[rp];
+        seg_p_n = F.seg ? F.seg[rp] : 0;   // row rr - 1's: the propagation after row rr
         if constexpr (COMB) {
-            sp = prior_seg[r];
-            if (sp < 0 || sp >= n_seg) sp = 0;
-            const double *fr = fwd + (size_t)20 * r;
+            sp_n = prior_seg[rr];
+            const double *fr = fwd + (size_t)20 * rr;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) mf[k] = fr[k];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) Cf[k] = fr[4 + k];
+            for (int k = 0; k < 20; ++k) fw_n[k] = fr[k];
         }
+    };
+    seg_r_n = F.seg ? F.seg[r1 - 1] : 0;
+    load_row(r1 - 1);
+    __builtin_amdgcn_s_waitcnt(0);   // the prologue's loads complete here (k_fwd_level)
+    for (int64_t r = r1 - 1; r >= r0; --r) {
+        const double y_l = y_l_n, y_f = y_f_n, t_r = t_r_n, t_prev = t_prev_n;
+        const int seg_p = seg_p_n;
+        const double *p = seg_row(PT, n_seg, seg_r_n);
+        const double var_x = p[7], var_g = p[8];
         if (pend) {
             if (pq != ou_src) {
                 ou = ggp::make_ou(-pq[0], pq[1], pq[2], -pq[3], pq[4], pq[5], -pq[6]);
@@ -1636,19 +1689,30 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_bwd_level(DevForest F, con
 #pragma unroll
         for (int k = 0; k < 16; ++k) rC[k] = C[k];
         ggp::reverse_state(rm, rC);
-        if (!COMB || out) store20(out + (size_t)20 * r, rm, rC);  // the prior, before the update
+        double mf[4], Cf[16];
+        int sp = 0;
         if constexpr (COMB) {   // k_combine<true> on this row
-            ggp::combine_info(mf, Cf, rm, rC, ptab + 11 * sp);
-            store20(comb + (size_t)20 * r, mf, Cf);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) mf[k] = fw_n[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) Cf[k] = fw_n[4 + k];
+            sp = sp_n;
+            if (sp < 0 || sp >= n_seg) sp = 0;
+            ggp::combine_info(mf, Cf, rm, rC, PT + 11 * sp);
         }
         const double x0 = y_l - m[0];
         const double x1 = y_f - m[1];
         ggp_innov v;
         ggp_innovation(m, C, var_x, var_g, F.scaled, F.fp_auto, v);
         ggp_posterior(m, C, x0, x1, v);
+        seg_r_n = seg_p;
+        load_row(max(r - 1, r0));   // row r - 1's operands, ahead of row r's stores
+        __builtin_amdgcn_sched_barrier(0);
+        if (!COMB || out) store20(out + (size_t)20 * r, rm, rC);  // the prior, before the update
+        if constexpr (COMB) store20(comb + (size_t)20 * r, mf, Cf);
         pend = r > r0;
         if (pend) {
-            pq = q_next;
+            pq = seg_row(PT, n_seg, seg_p);   // row r - 1's parameters (seg_params(r - 1))
             dtp = t_r - t_prev;
         }
     }
@@ -1730,6 +1794,17 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
     ggp::OU ou{};
     for (int k = 0; k < kmax; ++k) {
         const int64_t r = r0 + k;
+        // row r's operands and the next row's time, loaded before the propagation they would
+        // otherwise wait behind (the segment index raw: its parameter row is read after it)
+        double y_l = 0.0, y_f = 0.0, t_r = 0.0, t_nx = 0.0;
+        int seg_r = 0;
+        if (live) {
+            y_l = F.logl[r];
+            y_f = F.fp[r];
+            t_r = F.time[r];
+            if (k + 1 < nrows) t_nx = F.time[r + 1];
+            if (F.seg) seg_r = F.seg[r];
+        }
         if (__builtin_amdgcn_ballot_w64(live && pending)) {
             double mn[4], Cn[16];
 #pragma unroll
@@ -1753,15 +1828,15 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
             }
         }
         if (live) {
-            const double *p = seg_params(F, ptab, n_seg, r);
-            const double x0 = F.logl[r] - m[0];
-            const double x1 = F.fp[r] - m[1];
+            const double *p = seg_row(ptab, n_seg, seg_r);
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
             ggp_innov v;
             ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
             ggp_posterior(m, C, x0, x1, v);
             if (w == 0) store20(out + (size_t)20 * r, m, C);
             pending = k + 1 < nrows;
-            if (pending) dt = F.time[r + 1] - F.time[r];
+            if (pending) dt = t_nx - t_r;
             pprop = p;   // the step t -> t+1 uses row t's parameters (:143-146)
             live = k + 1 < nrows;
         }
@@ -1854,8 +1929,21 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
     bool live = valid && nrows > 0;
     bool pend = internal;   // the propagation before this row's update (one call site)
     for (int k = 0; k < kmax; ++k) {
-        if (__builtin_amdgcn_ballot_w64(pend)) prop(pend, dt);
         const int64_t r = r1 - 1 - k;
+        // row r's operands, the previous row's time and segment, loaded before the propagation
+        double y_l = 0.0, y_f = 0.0, t_r = 0.0, t_p = 0.0;
+        int seg_r = 0, seg_p = 0;
+        if (live) {
+            y_l = F.logl[r];
+            y_f = F.fp[r];
+            if (F.seg) seg_r = F.seg[r];
+            if (r > r0) {
+                t_r = F.time[r];
+                t_p = F.time[r - 1];
+                if (F.seg) seg_p = F.seg[r - 1];
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(pend)) prop(pend, dt);
         bool more = false;
         if (live) {
             double rm[4], rC[16];
@@ -1865,16 +1953,16 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
             for (int q = 0; q < 16; ++q) rC[q] = C[q];
             ggp::reverse_state(rm, rC);
             if (w == 0) store20(out + (size_t)20 * r, rm, rC);   // the prior, before the update
-            const double *p = seg_params(F, ptab, n_seg, r);
-            const double x0 = F.logl[r] - m[0];
-            const double x1 = F.fp[r] - m[1];
+            const double *p = seg_row(ptab, n_seg, seg_r);
+            const double x0 = y_l - m[0];
+            const double x1 = y_f - m[1];
             ggp_innov v;
             ggp_innovation(m, C, p[7], p[8], F.scaled, F.fp_auto, v);
             ggp_posterior(m, C, x0, x1, v);
             more = r > r0;
             if (more) {
-                pq = seg_params(F, ptab, n_seg, r - 1);
-                dt = F.time[r] - F.time[r - 1];
+                pq = seg_row(ptab, n_seg, seg_p);   // seg_params(r - 1)
+                dt = t_r - t_p;
             }
         }
         pend = more;
@@ -2824,16 +2912,27 @@ hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pst
             return;
         }
         const int cpw = lane_cpw(f);
-        if (fwd)
-            hipLaunchKernelGGL(k_fwd_level, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
-                               f->d_level_cells + a, n, cpw, d_pstate, d_fwd);
+        const dim3 grid((n + cpw - 1) / cpw);
+        const bool sl = n_seg <= kSegLds;   // the parameter rows in LDS
+        if (fwd && sl)
+            hipLaunchKernelGGL(k_fwd_level<true>, grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                               cpw, d_pstate, d_fwd);
+        else if (fwd)
+            hipLaunchKernelGGL(k_fwd_level<false>, grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg, f->d_level_cells + a, n,
+                               cpw, d_pstate, d_fwd);
+        else if (d_comb && sl)
+            hipLaunchKernelGGL((k_bwd_level<true, true>), grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd, f->d_prior_seg, (const double *)d_fwd, d_comb);
         else if (d_comb)
-            hipLaunchKernelGGL(k_bwd_level<true>, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab,
-                               n_seg, f->d_level_cells + a, n, cpw, d_pstate, d_bwd, f->d_prior_seg,
-                               (const double *)d_fwd, d_comb);
+            hipLaunchKernelGGL((k_bwd_level<true, false>), grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd, f->d_prior_seg, (const double *)d_fwd, d_comb);
+        else if (sl)
+            hipLaunchKernelGGL((k_bwd_level<false, true>), grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd, (const int32_t *)nullptr,
+                               (const double *)nullptr, (double *)nullptr);
         else
-            hipLaunchKernelGGL(k_bwd_level<false>, dim3((n + cpw - 1) / cpw), dim3(64), 0, f->stream, f->F, d_ptab,
-                               n_seg, f->d_level_cells + a, n, cpw, d_pstate, d_bwd, (const int32_t *)nullptr,
+            hipLaunchKernelGGL((k_bwd_level<false, false>), grid, dim3(64), 0, f->stream, f->F, d_ptab, n_seg,
+                               f->d_level_cells + a, n, cpw, d_pstate, d_bwd, (const int32_t *)nullptr,
                                (const double *)nullptr, (double *)nullptr);
     };
     hipError_t e = hipMemsetAsync(d_pstate, 0, (size_t)f->n_cells * 20 * sizeof(double), f->stream);
