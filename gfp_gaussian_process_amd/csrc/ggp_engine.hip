@@ -1768,13 +1768,17 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
                                                      double *__restrict__ out)
 {
     GGP_PAIR_LDS(CPW);
+    __shared__ double s_par[11 * kSegLds];   // the parameter rows (n_seg <= kSegLds: the launch checks)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (w == 0) load_dawson_table(s_tab, lane);
+    if (w == 1 % Q) stage_params<true>(s_par, ptab, n_seg, lane);
+    __syncthreads();
+    const double *PT = s_par;
     const int i = blockIdx.x * CPW + lane;
     const bool valid = lane < CPW && i < n;
     int c = 0, nrows = 0;
     int64_t r0 = 0;
-    const double *pi = ptab, *pprop = ptab;
+    const double *pi = PT, *pprop = PT;
     double m[4] = {0, 0, 0, 0}, C[16] = {0}, dt = 0.0;
     bool pending = false, divide = false;
     if (valid) {
@@ -1782,7 +1786,7 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
         r0 = F.row_off[c];
         nrows = (int)(F.row_off[c + 1] - r0);
         const int par = F.parent[c];
-        pi = seg_params(F, ptab, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);   // :103-108
+        pi = seg_params(F, PT, n_seg, par < 0 ? r0 : F.row_off[par + 1] - 1);   // :103-108
         pending = cell_prologue(F, pi, pstate, c, r0, m, C, dt);
         divide = pending;
         pprop = pi;
@@ -1792,19 +1796,17 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
     bool live = valid && nrows > 0;
     const double *ou_src = nullptr;   // the OU constants per segment change only (k_fwd_level)
     ggp::OU ou{};
+    // row r's operands (its data, time, the next row's time, its raw segment index) are loaded
+    // during row r - 1, after its propagation and before its store (k_fwd_level's pipeline:
+    // unconditional loads, indices clamped to the cell's rows; a lane without a cell reads row 0)
+    const int64_t r_last = r0 + max(nrows, 1) - 1;
+    double y_l_n = F.logl[r0], y_f_n = F.fp[r0], t_r_n = F.time[r0], t_nx_n = F.time[min(r0 + 1, r_last)];
+    int seg_n = F.seg ? F.seg[r0] : 0;
+    __builtin_amdgcn_s_waitcnt(0);   // the prologue's loads complete here (k_fwd_level)
     for (int k = 0; k < kmax; ++k) {
         const int64_t r = r0 + k;
-        // row r's operands and the next row's time, loaded before the propagation they would
-        // otherwise wait behind (the segment index raw: its parameter row is read after it)
-        double y_l = 0.0, y_f = 0.0, t_r = 0.0, t_nx = 0.0;
-        int seg_r = 0;
-        if (live) {
-            y_l = F.logl[r];
-            y_f = F.fp[r];
-            t_r = F.time[r];
-            if (k + 1 < nrows) t_nx = F.time[r + 1];
-            if (F.seg) seg_r = F.seg[r];
-        }
+        const double y_l = y_l_n, y_f = y_f_n, t_r = t_r_n, t_nx = t_nx_n;
+        const int seg_r = seg_n;
         if (__builtin_amdgcn_ballot_w64(live && pending)) {
             double mn[4], Cn[16];
 #pragma unroll
@@ -1827,8 +1829,17 @@ __global__ __launch_bounds__(64 * Q) void k_fwd_pair(DevForest F, const double *
                 }
             }
         }
+        {   // row r + 1's operands, ahead of row r's store
+            const int64_t rn = min(r + 1, r_last);
+            y_l_n = F.logl[rn];
+            y_f_n = F.fp[rn];
+            t_r_n = F.time[rn];
+            t_nx_n = F.time[min(r + 2, r_last)];
+            if (F.seg) seg_n = F.seg[rn];
+        }
+        __builtin_amdgcn_sched_barrier(0);
         if (live) {
-            const double *p = seg_row(ptab, n_seg, seg_r);
+            const double *p = seg_row(PT, n_seg, seg_r);
             const double x0 = y_l - m[0];
             const double x1 = y_f - m[1];
             ggp_innov v;
@@ -1851,13 +1862,17 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
                                                      double *__restrict__ out)
 {
     GGP_PAIR_LDS(CPW);
+    __shared__ double s_par[11 * kSegLds];   // the parameter rows (n_seg <= kSegLds: the launch checks)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (w == 0) load_dawson_table(s_tab, lane);
+    if (w == 1 % Q) stage_params<true>(s_par, ptab, n_seg, lane);
+    __syncthreads();
+    const double *PT = s_par;
     const int i = blockIdx.x * CPW + lane;
     const bool valid = lane < CPW && i < n;
     int c = 0, nrows = 0, d1 = -1;
     int64_t r0 = 0, r1 = 0;
-    const double *pi = ptab;
+    const double *pi = PT;
     double m[4] = {0, 0, 0, 0}, C[16] = {0}, dt = 0.0;
     bool internal = false;
     if (valid) {
@@ -1865,7 +1880,7 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
         r0 = F.row_off[c];
         r1 = F.row_off[c + 1];
         nrows = (int)(r1 - r0);
-        pi = seg_params(F, ptab, n_seg, r1 - 1);   // :376-378
+        pi = seg_params(F, PT, n_seg, r1 - 1);   // :376-378
         d1 = F.d1[c];
         const int d2 = F.d2[c];
         if (d1 < 0 && d2 < 0) {   // init_sc_distribution_r leaf branch (:317-332)
@@ -1928,22 +1943,29 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
     };
     bool live = valid && nrows > 0;
     bool pend = internal;   // the propagation before this row's update (one call site)
+    // row r's operands (its data and time, the previous row's time and raw segment index) are
+    // loaded during row r + 1, after its propagation and before its store (k_fwd_pair, downwards;
+    // indices clamped to the cell's rows, a lane without a cell reads row 0)
+    const int64_t r_first = r0, r_top = r1 > r0 ? r1 - 1 : r0;
+    auto seg_at = [&](const int64_t rr) { return F.seg ? F.seg[rr] : 0; };
+    double y_l_n = F.logl[r_top], y_f_n = F.fp[r_top], t_r_n = F.time[r_top], t_p_n = F.time[max(r_top - 1, r_first)];
+    int seg_r_n = seg_at(r_top), seg_p_n = seg_at(max(r_top - 1, r_first));
+    __builtin_amdgcn_s_waitcnt(0);   // the prologue's loads complete here (k_fwd_level)
     for (int k = 0; k < kmax; ++k) {
         const int64_t r = r1 - 1 - k;
-        // row r's operands, the previous row's time and segment, loaded before the propagation
-        double y_l = 0.0, y_f = 0.0, t_r = 0.0, t_p = 0.0;
-        int seg_r = 0, seg_p = 0;
-        if (live) {
-            y_l = F.logl[r];
-            y_f = F.fp[r];
-            if (F.seg) seg_r = F.seg[r];
-            if (r > r0) {
-                t_r = F.time[r];
-                t_p = F.time[r - 1];
-                if (F.seg) seg_p = F.seg[r - 1];
-            }
-        }
+        const double y_l = y_l_n, y_f = y_f_n, t_r = t_r_n, t_p = t_p_n;
+        const int seg_r = seg_r_n, seg_p = seg_p_n;
         if (__builtin_amdgcn_ballot_w64(pend)) prop(pend, dt);
+        {   // row r - 1's operands, ahead of row r's store
+            const int64_t rn = max(r - 1, r_first), rp = max(r - 2, r_first);
+            y_l_n = F.logl[rn];
+            y_f_n = F.fp[rn];
+            t_r_n = F.time[rn];
+            t_p_n = F.time[rp];
+            seg_r_n = seg_p;
+            seg_p_n = seg_at(rp);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         bool more = false;
         if (live) {
             double rm[4], rC[16];
@@ -1953,7 +1975,7 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
             for (int q = 0; q < 16; ++q) rC[q] = C[q];
             ggp::reverse_state(rm, rC);
             if (w == 0) store20(out + (size_t)20 * r, rm, rC);   // the prior, before the update
-            const double *p = seg_row(ptab, n_seg, seg_r);
+            const double *p = seg_row(PT, n_seg, seg_r);
             const double x0 = y_l - m[0];
             const double x1 = y_f - m[1];
             ggp_innov v;
@@ -1961,7 +1983,7 @@ __global__ __launch_bounds__(64 * Q) void k_bwd_pair(DevForest F, const double *
             ggp_posterior(m, C, x0, x1, v);
             more = r > r0;
             if (more) {
-                pq = seg_row(ptab, n_seg, seg_p);   // seg_params(r - 1)
+                pq = seg_row(PT, n_seg, seg_p);   // seg_params(r - 1)
                 dt = t_r - t_p;
             }
         }
@@ -2894,7 +2916,7 @@ hipError_t run_smoother(Shard *f, const double *d_ptab, int n_seg, double *d_pst
     // 64-cell workgroup per CU holds it, else two; bitwise the lane smoother), larger ones the
     // lane smoother (GGP_SMOOTHER_LANE=1: every level)
     auto launch = [&](const bool fwd, const int64_t a, const int n) {
-        if (!f->smoother_lane && n <= f->pair_max_cells) {
+        if (!f->smoother_lane && n <= f->pair_max_cells && n_seg <= kSegLds) {   // (the pair kernels stage <= kSegLds rows)
             const int q = n <= (int64_t)f->n_cu * 64 ? 4 : 2;
             const dim3 grid((n + 63) / 64);
             if (fwd && q == 4)

@@ -1012,3 +1012,30 @@ def test_mixed_long_dt_waves_bitwise(kernel, monkeypatch):
         assert np.array_equal(a[rows], b)
     fm.close()
     fs.close()
+
+
+def test_predict_many_segments_parameter_rows_from_global(monkeypatch):
+    """40 parameter segments (time quantiles), more than the 32 rows the lane smoother stages in LDS
+    (ggp_engine.hip kSegLds): the lane smoother reads them from global memory (k_fwd_level<false>,
+    k_bwd_level<true, false>); its rows equal the lane-pair smoother's bitwise (every level of this
+    forest fits the split) and lie within the smoother bar of the oracle"""
+    import gfp_gaussian_process_amd as g
+    from oracle import oracle as O
+    hf = g.HostForest.synthetic(30, 60, seed=21)
+    t = hf.a["time"]
+    nseg = 40
+    hf.a["segment"] = np.searchsorted(np.quantile(t, np.linspace(0, 1, nseg + 1)[1:-1]), t, side="right").astype(np.int32)
+    assert len(np.unique(hf.a["segment"])) > 32   # (the times are whole minutes: some quantiles coincide)
+    P0 = np.array(CONFIGS[0][2])
+    rng = np.random.default_rng(8)
+    params = np.stack([P0 * np.exp(rng.uniform(-0.05, 0.05, 11)) for _ in range(nseg)])
+    split = g.Forest(hf).predict(params)
+    monkeypatch.setenv("GGP_SMOOTHER_LANE", "1")
+    lane = g.Forest(hf).predict(params)
+    for name, x, y in zip(("forward", "backward", "combined"), lane, split):
+        assert np.array_equal(x, y), name
+    ref = O.OracleForest(hf.a).predict(params)
+    for name, x, y in zip(("forward", "backward", "combined"), lane, ref):
+        em, ec = _smoother_err(x, y)
+        print(f"PRED_ERR 40 segments {name} mean {em:.3e} cov {ec:.3e}")
+        assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
