@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         cell_nan += (size_t)n * pt;
         cell_done += (size_t)n * pt;
     }
-    const W::LaneC LC = W::kLaneTab.l[lane];   // this lane's row of the compile-time table
+    const W::LaneC LC = W::unpack_lane(W::kLanePTab.l[lane]);   // this lane's row of the compile-time table (packed)
     W::Lane L;
     {
         const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);

@@ -531,6 +531,119 @@ constexpr LaneTab make_lane_tab()
 }
 constexpr LaneTab kLaneTab = make_lane_tab();
 
+// The table's row in packed form: every LaneC double is a small multiple of 1/2 (stored doubled,
+// in a signed byte) or, for b_mult, one of two constants (a flag); every slot an LDS index below
+// 2^15 (a short).  100 bytes per lane instead of 400: each block's setup reads 6.4 KB of lane
+// constants instead of 25.6 KB (the launch timeline's "table" phase).
+// unpack_lane(pack_lane(row)) == row for every lane (static_assert below), so the registers the
+// step reads are bitwise the unpacked table's.
+enum { LP_ISE = 1, LP_ISA = 2, LP_ISD = 4, LP_EXMASK = 8, LP_SGN = 16, LP_FROW = 32 };
+struct LaneP {
+    signed char b_tau, b_km, b_ks, b_m1, b_m2, b_kb, b_kgl, b_kgq, b_zc;
+    signed char i_tau0, i_tau1, i_km, i_ks, i_u0, i_u1, i_u2, i_w2, i_w3, i_g, i_s0, i_s1, i_s2, i_s3, i_S1;
+    signed char u_fml, u_fmq;
+    unsigned char flags, d_bs;
+    unsigned char d_kap[kOutL];
+    short b_dst, i_d0, i_d1, i_e0r, i_e0f, i_e1r, i_e1f, i_ecr, i_ecf, i_a0, i_a1, i_dst;
+    short mo_v0, mo_v1, mo_v2, mo_dst;
+    short d_mono[kOutL], d_basis[kOutL];
+    short d_out, f_src, f_na, f_nb, f_dst, u_ub, u_wb, u_c, u_post, u_v;
+};
+constexpr signed char half2(const double v) { return (signed char)(int)(2.0 * v); }
+constexpr LaneP pack_lane(const LaneC &C)
+{
+    LaneP P{};
+    P.b_tau = half2(C.b_tau); P.b_km = half2(C.b_km); P.b_ks = half2(C.b_ks); P.b_m1 = half2(C.b_m1);
+    P.b_m2 = half2(C.b_m2); P.b_kb = half2(C.b_kb); P.b_kgl = half2(C.b_kgl); P.b_kgq = half2(C.b_kgq);
+    P.b_zc = half2(C.b_zc);
+    P.i_tau0 = half2(C.i_tau0); P.i_tau1 = half2(C.i_tau1); P.i_km = half2(C.i_km); P.i_ks = half2(C.i_ks);
+    P.i_u0 = half2(C.i_u0); P.i_u1 = half2(C.i_u1); P.i_u2 = half2(C.i_u2); P.i_w2 = half2(C.i_w2);
+    P.i_w3 = half2(C.i_w3); P.i_g = half2(C.i_g); P.i_s0 = half2(C.i_s0); P.i_s1 = half2(C.i_s1);
+    P.i_s2 = half2(C.i_s2); P.i_s3 = half2(C.i_s3); P.i_S1 = half2(C.i_S1);
+    P.u_fml = half2(C.u_fml); P.u_fmq = half2(C.u_fmq);
+    P.flags = (unsigned char)((C.b_isE ? LP_ISE : 0) | (C.b_isA ? LP_ISA : 0) | (C.b_isD ? LP_ISD : 0) |
+                              (C.b_exmask ? LP_EXMASK : 0) | (C.b_sgn ? LP_SGN : 0) | (C.f_row ? LP_FROW : 0));
+    P.d_bs = (unsigned char)C.d_bs;
+    for (int q = 0; q < kOutL; ++q) {
+        P.d_kap[q] = (unsigned char)C.d_kap[q];
+        P.d_mono[q] = (short)C.d_mono[q];
+        P.d_basis[q] = (short)C.d_basis[q];
+    }
+    P.b_dst = (short)C.b_dst; P.i_d0 = (short)C.i_d0; P.i_d1 = (short)C.i_d1; P.i_e0r = (short)C.i_e0r;
+    P.i_e0f = (short)C.i_e0f; P.i_e1r = (short)C.i_e1r; P.i_e1f = (short)C.i_e1f; P.i_ecr = (short)C.i_ecr;
+    P.i_ecf = (short)C.i_ecf; P.i_a0 = (short)C.i_a0; P.i_a1 = (short)C.i_a1; P.i_dst = (short)C.i_dst;
+    P.mo_v0 = (short)C.mo_v0; P.mo_v1 = (short)C.mo_v1; P.mo_v2 = (short)C.mo_v2; P.mo_dst = (short)C.mo_dst;
+    P.d_out = (short)C.d_out; P.f_src = (short)C.f_src; P.f_na = (short)C.f_na; P.f_nb = (short)C.f_nb;
+    P.f_dst = (short)C.f_dst; P.u_ub = (short)C.u_ub; P.u_wb = (short)C.u_wb; P.u_c = (short)C.u_c;
+    P.u_post = (short)C.u_post; P.u_v = (short)C.u_v;
+    return P;
+}
+GGP_DEV constexpr LaneC unpack_lane(const LaneP &P)
+{
+    LaneC C{};
+    C.b_tau = 0.5 * P.b_tau; C.b_km = 0.5 * P.b_km; C.b_ks = 0.5 * P.b_ks; C.b_m1 = 0.5 * P.b_m1;
+    C.b_m2 = 0.5 * P.b_m2; C.b_kb = 0.5 * P.b_kb; C.b_kgl = 0.5 * P.b_kgl; C.b_kgq = 0.5 * P.b_kgq;
+    C.b_zc = 0.5 * P.b_zc;
+    C.b_isE = (P.flags & LP_ISE) ? 1 : 0; C.b_isA = (P.flags & LP_ISA) ? 1 : 0; C.b_isD = (P.flags & LP_ISD) ? 1 : 0;
+    C.b_exmask = (P.flags & LP_EXMASK) ? -1 : 0;
+    C.b_sgn = (P.flags & LP_SGN) ? (int)0x80000000u : 0;
+    C.b_mult = C.b_isD ? GGP_SPI2 : 1.0;
+    C.b_dst = P.b_dst;
+    C.i_tau0 = 0.5 * P.i_tau0; C.i_tau1 = 0.5 * P.i_tau1; C.i_km = 0.5 * P.i_km; C.i_ks = 0.5 * P.i_ks;
+    C.i_u0 = 0.5 * P.i_u0; C.i_u1 = 0.5 * P.i_u1; C.i_u2 = 0.5 * P.i_u2; C.i_w2 = 0.5 * P.i_w2;
+    C.i_w3 = 0.5 * P.i_w3; C.i_g = 0.5 * P.i_g; C.i_s0 = 0.5 * P.i_s0; C.i_s1 = 0.5 * P.i_s1;
+    C.i_s2 = 0.5 * P.i_s2; C.i_s3 = 0.5 * P.i_s3; C.i_S1 = 0.5 * P.i_S1;
+    C.i_d0 = P.i_d0; C.i_d1 = P.i_d1; C.i_e0r = P.i_e0r; C.i_e0f = P.i_e0f; C.i_e1r = P.i_e1r; C.i_e1f = P.i_e1f;
+    C.i_ecr = P.i_ecr; C.i_ecf = P.i_ecf; C.i_a0 = P.i_a0; C.i_a1 = P.i_a1; C.i_dst = P.i_dst;
+    C.mo_v0 = P.mo_v0; C.mo_v1 = P.mo_v1; C.mo_v2 = P.mo_v2; C.mo_dst = P.mo_dst;
+    for (int q = 0; q < kOutL; ++q) {
+        C.d_mono[q] = P.d_mono[q];
+        C.d_basis[q] = P.d_basis[q];
+        C.d_kap[q] = P.d_kap[q];
+    }
+    C.d_bs = P.d_bs; C.d_out = P.d_out;
+    C.f_src = P.f_src; C.f_na = P.f_na; C.f_nb = P.f_nb; C.f_row = (P.flags & LP_FROW) ? 1 : 0; C.f_dst = P.f_dst;
+    C.u_ub = P.u_ub; C.u_wb = P.u_wb; C.u_c = P.u_c; C.u_post = P.u_post; C.u_v = P.u_v;
+    C.u_fml = 0.5 * P.u_fml; C.u_fmq = 0.5 * P.u_fmq;
+    return C;
+}
+constexpr bool same_lane(const LaneC &a, const LaneC &b)
+{
+    bool ok = a.b_tau == b.b_tau && a.b_km == b.b_km && a.b_ks == b.b_ks && a.b_m1 == b.b_m1 && a.b_m2 == b.b_m2 &&
+              a.b_kb == b.b_kb && a.b_kgl == b.b_kgl && a.b_kgq == b.b_kgq && a.b_mult == b.b_mult && a.b_zc == b.b_zc &&
+              a.b_isE == b.b_isE && a.b_isA == b.b_isA && a.b_isD == b.b_isD && a.b_exmask == b.b_exmask &&
+              a.b_sgn == b.b_sgn && a.b_dst == b.b_dst && a.i_tau0 == b.i_tau0 && a.i_tau1 == b.i_tau1 &&
+              a.i_km == b.i_km && a.i_ks == b.i_ks && a.i_u0 == b.i_u0 && a.i_u1 == b.i_u1 && a.i_u2 == b.i_u2 &&
+              a.i_w2 == b.i_w2 && a.i_w3 == b.i_w3 && a.i_g == b.i_g && a.i_s0 == b.i_s0 && a.i_s1 == b.i_s1 &&
+              a.i_s2 == b.i_s2 && a.i_s3 == b.i_s3 && a.i_S1 == b.i_S1 && a.i_d0 == b.i_d0 && a.i_d1 == b.i_d1 &&
+              a.i_e0r == b.i_e0r && a.i_e0f == b.i_e0f && a.i_e1r == b.i_e1r && a.i_e1f == b.i_e1f &&
+              a.i_ecr == b.i_ecr && a.i_ecf == b.i_ecf && a.i_a0 == b.i_a0 && a.i_a1 == b.i_a1 && a.i_dst == b.i_dst &&
+              a.mo_v0 == b.mo_v0 && a.mo_v1 == b.mo_v1 && a.mo_v2 == b.mo_v2 && a.mo_dst == b.mo_dst &&
+              a.d_bs == b.d_bs && a.d_out == b.d_out && a.f_src == b.f_src && a.f_na == b.f_na && a.f_nb == b.f_nb &&
+              a.f_row == b.f_row && a.f_dst == b.f_dst && a.u_ub == b.u_ub && a.u_wb == b.u_wb && a.u_c == b.u_c &&
+              a.u_post == b.u_post && a.u_v == b.u_v && a.u_fml == b.u_fml && a.u_fmq == b.u_fmq;
+    for (int q = 0; q < kOutL; ++q)
+        ok = ok && a.d_mono[q] == b.d_mono[q] && a.d_basis[q] == b.d_basis[q] && a.d_kap[q] == b.d_kap[q];
+    return ok;
+}
+struct LanePTab {
+    LaneP l[64];
+};
+constexpr LanePTab make_lane_ptab()
+{
+    LanePTab T{};
+    for (int l = 0; l < 64; ++l) T.l[l] = pack_lane(kLaneTab.l[l]);
+    return T;
+}
+constexpr LanePTab kLanePTab = make_lane_ptab();
+constexpr bool check_lane_ptab()
+{
+    for (int l = 0; l < 64; ++l)
+        if (!same_lane(unpack_lane(kLanePTab.l[l]), kLaneTab.l[l])) return false;
+    return true;
+}
+static_assert(check_lane_ptab(), "the packed lane table unpacks to the lane table, field for field");
+
 // the lane's registers from its row and the parameters; kap: the 33 kappas (LDS, lane_kappa)
 GGP_DEV Lane lane_from(const int lane, const LaneC &C, const OU &P, const double *kap)
 {
