@@ -378,7 +378,7 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
     int c = 0, nrows = 0;
     int64_t r0 = 0;
     double m[4] = {0, 0, 0, 0}, C[16] = {0};
-    double dt = 0.0;
+    double dt = 0.0, t_cur = 0.0;   // t_cur: this row's time, carried from the previous row's load
     bool pending = false, divide = false;
     if (valid) {
         c = cells[i];
@@ -386,6 +386,7 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
         nrows = (int)(F.row_off[c + 1] - r0);
         pending = cell_prologue(F, p, state, c, r0, m, C, dt);
         divide = pending;
+        if (nrows > 0) t_cur = F.time[r0];
     }
     // lanes without a cell propagate lane 0's state (never stored): finite operands, so they
     // take none of the Dawson's rare branches
@@ -450,7 +451,8 @@ __global__ __launch_bounds__(64 * Q) void k_loglik_pair(DevForest F, ggp_params 
             } else {
                 ggp_posterior(m, C, x0, x1, v);
                 pending = k + 1 < nrows;
-                if (pending) dt = t_next - F.time[r];
+                if (pending) dt = t_next - t_cur;   // no load on the step's chain
+                t_cur = t_next;
                 live = k + 1 < nrows;
             }
         }
