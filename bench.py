@@ -759,37 +759,41 @@ def main() -> int:
         f3.close()
 
     # ---- BASELINE configs[4]'s -j half on C5-shaped trees (the <= 10k-row subset): 20
-    # trees x 500 tp (250 + 125 + 125 rows), ggp_joints over every start row in ranges of 4,096
-    # as the CLI streams them (ggp_cli.cpp: chunk 4096), into one pair of host buffers reused
-    # from range to range as the CLI's are, the joints copied to the host ----
+    # trees x 500 tp (250 + 125 + 125 rows), ggp_joints over every start row in ranges as the CLI
+    # streams them (ggp_cli.cpp: 4,096 start rows first, then ranges sized for about 2^20 joints at
+    # the density seen), into one pair of host buffers reused from range to range as the CLI's
+    # are, the joints copied to the host ----
     jc5 = None
     if world == 1 and args.joints_trees > 0:
         hj = g.HostForest.synthetic(args.joints_trees, args.predict_rows, seed=SEED, first_tree=2 * 10 ** 6)
         fj = g.Forest(hj, device=local)
         nrj = hj.n_rows
-        jcap = 1 << 20
+        jcap = 1 << 21   # the CLI's max_cap
         jbuf = (np.empty((jcap, 2), np.int64), np.empty((jcap, 72)))
         for b_ in jbuf:
             b_.fill(0)   # paged in, as a long-running writer's buffers are
         fj.joints(P_EXAMPLE, 1e-10, 0, min(nrj, 256), out=jbuf)   # warm-up: smoother tables cached
         barrier()
         t1 = time.perf_counter()
-        nj, lo = 0, 0
+        nj, lo, chunk, n_calls = 0, 0, 4096, 0
         while lo < nrj:
-            hi = min(nrj, lo + 4096)
+            hi = min(nrj, lo + chunk)
+            n_calls += 1
             try:
                 idx_j, _ = fj.joints(P_EXAMPLE, 1e-10, lo, hi, out=jbuf)
-            except g.GGPError:
-                jcap *= 2
-                jbuf = (np.zeros((jcap, 2), np.int64), np.zeros((jcap, 72)))
+            except g.GGPError:   # more than the CLI's max_cap: split the range, as the CLI does
+                chunk = max(1, (hi - lo) // 2)
                 continue
             nj += len(idx_j)
+            if len(idx_j):
+                chunk = min(65536, max(256, (hi - lo) * (jcap // 2) // len(idx_j)))
             lo = hi
         barrier()
         jel = time.perf_counter() - t1
         jc5 = {"config": f"-j on {args.joints_trees} C5-shaped trees x {args.predict_rows} tp ({nrj} rows), "
-                         "tol 1e-10, every start row, ranges of 4,096 start rows (the CLI's), reused host buffers",
-               "rows": nrj, "joints": nj, "seconds": jel, "joints_per_s": nj / jel, "start_rows_per_s": nrj / jel,
+                         "tol 1e-10, every start row, ranges as the CLI's (4,096 start rows, then sized for ~2^20 "
+                         "joints), reused host buffers",
+               "rows": nrj, "joints": nj, "calls": n_calls, "seconds": jel, "joints_per_s": nj / jel, "start_rows_per_s": nrj / jel,
                "note": "BASELINE configs[4]'s -j leg on its tree shape (SURVEY 8(d) subset); joints computed on "
                        "the GPU and copied to the host (72 doubles each), parameter tables cached per parameters"}
         fj.close()

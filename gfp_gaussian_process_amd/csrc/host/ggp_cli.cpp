@@ -846,7 +846,7 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
     std::vector<double> val((size_t)(72 * cap));
     int64_t logged = -1;
     for (int64_t lo = 0; lo < nr;) {
-        const int64_t hi = std::min(nr, lo + chunk);
+        const int64_t hi = std::min(nr, lo + chunk), s_lo = lo;
         int64_t n_out = 0;
         const int rc = ggp_joints(F.gpu, pv.data(), (int32_t)plist.size(), tol, lo, hi, cap, idx.data(), val.data(),
                                   &n_out);
@@ -937,6 +937,18 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             }
         });
         lo = hi;
+        // the next range sized for about max_cap / 2 joints at this range's density: a launch walks
+        // its start rows side by side (one lane each) and takes as long as its longest walk, so
+        // fewer, larger ranges mean fewer launches (up to 65,536 start rows, one wave per SIMD)
+        if (n_out > 0) {
+            chunk = std::min<int64_t>(65536, std::max<int64_t>(256, (hi - s_lo) * (max_cap / 2) / n_out));
+            const int64_t want = std::min<int64_t>(max_cap, (int64_t)((double)n_out * chunk / (hi - s_lo) * 1.25) + 1);
+            if (want > cap) {
+                cap = want;
+                idx.resize((size_t)(2 * cap));
+                val.resize((size_t)(72 * cap));
+            }
+        }
     }
     if (!file) throw std::runtime_error("write failed: " + outfile);
 }
