@@ -2164,10 +2164,13 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
     int64_t cn = r - F.row_off[cur];
     bool at_div = false;
     int64_t cnt = 0;
+    // this start's slots [out_off[i], out_off[i + 1]): exact counts (two-pass) or the walk's bound
+    // (single pass); a joint past the end is counted, not stored (the host then redoes the range)
     int64_t out = out_off ? out_off[i] : 0;
+    const int64_t out_end = out_off ? out_off[i + 1] : 0;
     if (cn == rows0 - 1) {
         if (F.d1[cur] < 0) {
-            if (!out_off) counts[i] = 0;
+            counts[i] = 0;
             return;
         }
         at_div = true;
@@ -2198,7 +2201,7 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
                     stop = true;
                     break;
                 }
-                if (out_off) {
+                if (out < out_end) {
                     out_idx[2 * out] = r;
                     out_idx[2 * out + 1] = rr;
                     store_g8(out_val + (size_t)kJStart * out, comb);
@@ -2226,7 +2229,22 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
         cn = -1;
         at_div = false;
     }
-    if (!out_off) counts[i] = cnt;
+    counts[i] = cnt;
+}
+
+// single-pass -j: start i's joints from its bound slots [boff[i], ...) to the packed output at
+// coff[i] (one workgroup per start, the (start, target) pairs and the 72 values contiguous)
+__global__ __launch_bounds__(256) void k_joint_pack(int64_t n_starts, const int64_t *__restrict__ boff,
+                                                    const int64_t *__restrict__ coff, const int64_t *__restrict__ counts,
+                                                    const int64_t *__restrict__ src_idx, const double *__restrict__ src_val,
+                                                    int64_t *__restrict__ dst_idx, double *__restrict__ dst_val)
+{
+    const int64_t i = blockIdx.x;
+    if (i >= n_starts) return;
+    const int64_t n = counts[i], b = boff[i], c = coff[i];
+    for (int64_t k = threadIdx.x; k < 2 * n; k += blockDim.x) dst_idx[2 * c + k] = src_idx[2 * b + k];
+    for (int64_t k = threadIdx.x; k < (int64_t)kJStart * n; k += blockDim.x)
+        dst_val[(size_t)kJStart * c + k] = src_val[(size_t)kJStart * b + k];
 }
 
 
@@ -2657,8 +2675,12 @@ struct Shard {
     std::vector<double> j_params;      // the table the joint tables hold (empty: none)
     // -j per-call buffers, grow-only (no hipMalloc / synchronising hipFree per start-row range):
     // the walks' stacks and counts, sized by start rows x depth, and the emitted joints
-    void *d_jw_stack = nullptr, *d_jw_small = nullptr, *d_jw_out = nullptr;
-    size_t jw_stack_bytes = 0, jw_small_bytes = 0, jw_out_bytes = 0;
+    void *d_jw_stack = nullptr, *d_jw_small = nullptr, *d_jw_out = nullptr, *d_jw_bnd = nullptr;
+    size_t jw_stack_bytes = 0, jw_small_bytes = 0, jw_out_bytes = 0, jw_bnd_bytes = 0;
+    // rows below every cell (all its descendants'): with the rows after a start row in its own cell,
+    // the most joints that start's walk can emit (the single-pass emit's slots)
+    std::vector<int64_t> j_below;
+    size_t joint_slot_bytes = (size_t)2 << 30;   // GGP_JOINT_SLOT_MB: the single pass's slot budget (0: two passes)
 };
 
 // RCCL entry points, resolved at run time from the library the caller names (the one torch
@@ -2984,11 +3006,11 @@ void shard_free_joints(Shard *f)
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    for (void **p : {&f->d_jw_stack, &f->d_jw_small, &f->d_jw_out}) {
+    for (void **p : {&f->d_jw_stack, &f->d_jw_small, &f->d_jw_out, &f->d_jw_bnd}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    f->jw_stack_bytes = f->jw_small_bytes = f->jw_out_bytes = 0;
+    f->jw_stack_bytes = f->jw_small_bytes = f->jw_out_bytes = f->jw_bnd_bytes = 0;
     f->j_params.clear();
 }
 
@@ -3141,6 +3163,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_PAIR_MAX_CELLS")) f->pair_max_cells = atoll(e);
     if (const char *e = getenv("GGP_COMBINE_EXACT")) f->combine_exact = atoi(e) != 0;
     if (const char *e = getenv("GGP_COMBINE_FUSED")) f->combine_fused = atoi(e) != 0;
+    if (const char *e = getenv("GGP_JOINT_SLOT_MB")) f->joint_slot_bytes = (size_t)std::max(0, atoi(e)) << 20;
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL"); e && !ggp::kExact)
@@ -3171,6 +3194,12 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     f->level_start.assign(nc > 0 ? max_depth + 2 : 1, 0);
     for (int64_t c = 0; c < nc; ++c) f->level_start[depth[c] + 1]++;
     for (size_t L = 1; L < f->level_start.size(); ++L) f->level_start[L] += f->level_start[L - 1];
+    // rows below each cell, deepest cells first (a daughter is one generation below its parent)
+    f->j_below.assign(nc, 0);
+    for (int64_t k = nc - 1; k >= 0; --k) {
+        const int32_t c = level_cells[k], par = d->parent[c];
+        if (par >= 0) f->j_below[par] += (d->row_offset[c + 1] - d->row_offset[c]) + f->j_below[c];
+    }
     // ---- uploads ----
     check(dev_upload(&f->d_time, d->time, nr));
     check(dev_upload(&f->d_logl, d->log_length, nr));
@@ -3471,50 +3500,122 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
     const size_t b_stack_j = (size_t)ns * depth * kJStart * sizeof(double);
     const size_t b_stack_c = ((size_t)ns * depth * sizeof(int32_t) + 255) & ~(size_t)255;
     auto *stack = (char *)jw_reserve(&f->d_jw_stack, &f->jw_stack_bytes, b_stack_j + b_stack_c);
-    auto *small = (int64_t *)jw_reserve(&f->d_jw_small, &f->jw_small_bytes, (size_t)2 * ns * sizeof(int64_t));
+    // counts [ns], slot offsets [ns + 1], packed offsets [ns + 1]
+    auto *small = (int64_t *)jw_reserve(&f->d_jw_small, &f->jw_small_bytes, (size_t)(3 * ns + 2) * sizeof(int64_t));
     if (!stack || !small) { cleanup(); g_last_err = "ggp_joints: device allocation failed"; return GGP_ENOMEM; }
     auto *d_stack_c = (int32_t *)stack;
     auto *d_stack_j = (double *)(stack + b_stack_c);
-    int64_t *d_counts = small, *d_off = small + ns;
+    int64_t *d_counts = small, *d_off = small + ns, *d_coff = small + 2 * ns + 1;
     const unsigned wblocks = (unsigned)((ns + 63) / 64);
-    if (e == hipSuccess) {   // pass 1: count
+    constexpr size_t kJointBytes = 2 * sizeof(int64_t) + kJStart * sizeof(double);
+    auto walk = [&](const int64_t *offs, int64_t *o_idx, double *o_val) {
         hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, f->d_j_ptab, n_seg,
                            f->d_row_cell, f->d_j_pstate, f->d_j_back, f->d_j_cond, f->d_j_start, tol, r_lo, ns, depth,
-                           d_stack_j, d_stack_c, d_counts, (const int64_t *)nullptr, (int64_t *)nullptr,
-                           (double *)nullptr);
-        e = hipGetLastError();
-    }
-    std::vector<int64_t> counts(ns), off(ns);
-    if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
-    int64_t total = 0;
-    for (int64_t k = 0; k < ns; ++k) {
-        off[k] = total;
-        total += counts[k];
-    }
-    *n_out = total;
-    if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
+                           d_stack_j, d_stack_c, d_counts, offs, o_idx, o_val);
+        return hipGetLastError();
+    };
+    // the packed output buffer for `total` joints: (start, target) pairs, then the values
+    auto out_buf = [&](int64_t total, int64_t *&d_idx, double *&d_val) {
         const size_t b_idx = (size_t)total * 2 * sizeof(int64_t);
-        auto *out = (char *)jw_reserve(&f->d_jw_out, &f->jw_out_bytes, b_idx + (size_t)total * kJStart * sizeof(double));
-        auto *d_idx = (int64_t *)out;
-        auto *d_val = (double *)(out + b_idx);
-        if (!out) {
-            cleanup();
-            g_last_err = "ggp_joints: device allocation failed";
-            return GGP_ENOMEM;
+        auto *out = (char *)jw_reserve(&f->d_jw_out, &f->jw_out_bytes, (size_t)total * kJointBytes);
+        d_idx = (int64_t *)out;
+        d_val = out ? (double *)(out + b_idx) : nullptr;
+        return out != nullptr;
+    };
+    std::vector<int64_t> counts(ns), off(ns + 1);
+    // single pass: every start walks once into slots sized by its bound (the rows after it in its
+    // cell plus every row below the cell), then the joints are packed on the device; when the
+    // caller takes joints and the slots fit joint_slot_bytes, 2 GiB (else, or if a walk outgrew
+    // its slots, the two passes: count, then emit at the exact offsets)
+    bool single = e == hipSuccess && cap > 0 && out_idx && out_val;
+    std::vector<int64_t> boff;
+    if (single) {
+        boff.resize(ns + 1);
+        int64_t c = (int64_t)(std::upper_bound(f->row_off.begin(), f->row_off.end(), r_lo) - f->row_off.begin()) - 1;
+        int64_t acc = 0;
+        for (int64_t k = 0; k < ns; ++k) {
+            const int64_t r = r_lo + k;
+            while (f->row_off[c + 1] <= r) ++c;
+            boff[k] = acc;
+            acc += (f->row_off[c + 1] - 1 - r) + f->j_below[c];
         }
-        e = hipMemcpyAsync(d_off, off.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_joint_walk, dim3(wblocks), dim3(64), 0, f->stream, f->F, f->d_j_ptab, n_seg,
-                               f->d_row_cell, f->d_j_pstate, f->d_j_back, f->d_j_cond, f->d_j_start, tol, r_lo, ns,
-                               depth, d_stack_j, d_stack_c, d_counts, (const int64_t *)d_off, d_idx, d_val);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+        boff[ns] = acc;
+        single = (size_t)acc * kJointBytes <= f->joint_slot_bytes;
+    }
+    char *bnd = nullptr;
+    if (single) {
+        bnd = (char *)jw_reserve(&f->d_jw_bnd, &f->jw_bnd_bytes, (size_t)boff[ns] * kJointBytes);
+        single = bnd != nullptr;
+    }
+    if (single) {
+        auto *b_idx = (int64_t *)bnd;
+        auto *b_val = (double *)(bnd + (size_t)boff[ns] * 2 * sizeof(int64_t));
+        e = hipMemcpyAsync(d_off, boff.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
+        if (e == hipSuccess) e = walk(d_off, b_idx, b_val);
+        if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+        int64_t total = 0;
+        for (int64_t k = 0; k < ns && e == hipSuccess; ++k) {
+            if (counts[k] > boff[k + 1] - boff[k]) {   // not expected: the two passes redo the range
+                single = false;
+                break;
+            }
+            off[k] = total;
+            total += counts[k];
+        }
+        off[ns] = total;
+        if (e == hipSuccess && single) {
+            *n_out = total;
+            if (total > 0 && total <= cap) {
+                int64_t *d_idx = nullptr;
+                double *d_val = nullptr;
+                if (!out_buf(total, d_idx, d_val)) {
+                    cleanup();
+                    g_last_err = "ggp_joints: device allocation failed";
+                    return GGP_ENOMEM;
+                }
+                e = hipMemcpyAsync(d_coff, off.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
+                if (e == hipSuccess) {
+                    hipLaunchKernelGGL(k_joint_pack, dim3((unsigned)ns), dim3(256), 0, f->stream, ns, (const int64_t *)d_off,
+                                       (const int64_t *)d_coff, (const int64_t *)d_counts, (const int64_t *)b_idx,
+                                       (const double *)b_val, d_idx, d_val);
+                    e = hipGetLastError();
+                }
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+            }
+        }
+    }
+    if (e == hipSuccess && !single) {
+        e = walk(nullptr, nullptr, nullptr);   // pass 1: count
+        if (e == hipSuccess) e = hipMemcpyAsync(counts.data(), d_counts, ns * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+        int64_t total = 0;
+        for (int64_t k = 0; k < ns; ++k) {
+            off[k] = total;
+            total += counts[k];
+        }
+        off[ns] = total;
+        *n_out = total;
+        if (e == hipSuccess && total > 0 && total <= cap && out_idx && out_val) {   // pass 2: emit
+            int64_t *d_idx = nullptr;
+            double *d_val = nullptr;
+            if (!out_buf(total, d_idx, d_val)) {
+                cleanup();
+                g_last_err = "ggp_joints: device allocation failed";
+                return GGP_ENOMEM;
+            }
+            e = hipMemcpyAsync(d_off, off.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
+            if (e == hipSuccess) e = walk(d_off, d_idx, d_val);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+        }
     }
     cleanup();
     if (e != hipSuccess) {

@@ -336,3 +336,22 @@ def test_joints_into_reused_buffers_and_growing_workspace():
     with pytest.raises(ValueError):
         f.joints(P, 1e-10, 0, 4, out=(np.zeros((4, 2), np.int32), np.zeros((4, 72))))
     f.close()
+
+
+def test_joints_single_pass_bitwise_two_pass(monkeypatch):
+    """The single pass (each walk once into slots sized by its bound, packed on the device) gives
+    the two passes' joints bit for bit (GGP_JOINT_SLOT_MB=0 forces the count + emit passes), on
+    C5-shaped trees over ranges that start mid-cell, at a division row and at a leaf's last row"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(3, 500, seed=11)
+    nr = hf.n_rows
+    ranges = ((0, nr), (1, 250), (249, 251), (nr - 1, nr), (123, 777))
+    got = {}
+    for mb in ("2048", "0"):
+        monkeypatch.setenv("GGP_JOINT_SLOT_MB", mb)
+        f = g.Forest(hf)
+        got[mb] = [f.joints(P, 1e-10, lo, hi, cap=1 << 20) for lo, hi in ranges]
+        f.close()
+    for (lo, hi), (i1, v1), (i2, v2) in zip(ranges, got["2048"], got["0"]):
+        assert len(i1) > 0 or hi - lo == 1, (lo, hi)
+        assert np.array_equal(i1, i2) and np.array_equal(v1, v2), (lo, hi)
