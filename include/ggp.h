@@ -197,7 +197,10 @@ int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine);
  * the reference adds to its Joint_vector, in the order it adds them: out_idx[2k] = r,
  * out_idx[2k+1] = target row, out_val[72k..] = mean[8] then cov[64] row-major.  *n_out is the
  * number of joints; they are stored only when *n_out <= cap (else call again with a larger
- * cap or a smaller row range). */
+ * cap or a smaller row range).  A launch costs its longest walk (one lane per start row), so
+ * large ranges are cheap: each start is walked once into device slots sized by its bound and
+ * packed, while the range's slots fit GGP_JOINT_SLOT_MB (environment, read at creation; default
+ * 2048; 0 = count, then emit: two walks); the joints are the same either way. */
 int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo,
                int64_t r_hi, int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out);
 
