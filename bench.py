@@ -5,8 +5,10 @@ Workload (BASELINE.json configs[1], "C2"): a synthetic forest of 1,000 trees x 2
 per GPU (root 100 rows + two daughters of 50, dt = 1 min, simulated from the model SDE with
 the example parameters, Philox4x32 keyed by (seed, tree)); one step = one full
 total-log-likelihood evaluation (likelihood.h:125-174 semantics, carried root state) with
-the inputs resident in HBM, plus -- for N > 1 -- the one all_gather of the per-rank
-partial (RCCL over xGMI).  Weak scaling: rank r evaluates trees [r*T, (r+1)*T).
+the inputs resident in HBM, plus -- for N > 1 -- the one exchange of the per-rank partials
+(host shared memory for the ranks of one node, distributed.NodeExchange; torch's all_gather over
+RCCL otherwise, and timed beside it in `collective`).  Weak scaling: rank r evaluates trees
+[r*T, (r+1)*T).
 
   python bench.py [--gpus N --steps K --warmup W --trees T --rows P --kernel auto|lane|group|wave]
 
@@ -418,7 +420,7 @@ def main() -> int:
                "trees": T4, "rows": rows4, "trees_per_rank": hi4 - lo4, "steps": args.c4_steps,
                "ms_per_eval": 1e3 * el4, "updates_per_s": rows4 / el4, "scaling": "strong",
                "total_log_likelihood": ll4, "levels": f4.info()["levels"],
-               "collective": {"kind": "torch all_gather_into_tensor of 16 B per rank, rank-order sum",
+               "collective": {"kind": o4.exchange_kind if world > 1 else None,
                               "backend": args.backend if world > 1 else None,
                               "ranks": dist.get_world_size() if world > 1 else 1}}
         if args.c4_scan > 0:
@@ -437,6 +439,8 @@ def main() -> int:
                            "last": float(scan[-1]),
                            "note": "-s: each sample from the carried state the previous left; every rank "
                                    "chains its trees (ggp_total_loglik_chain), one all_gather of the partials"}
+        if world > 1:
+            o4.close()
         f4.close()
     for _ in range(args.warmup):
         obj.total_likelihood(P_EXAMPLE)
@@ -456,8 +460,9 @@ def main() -> int:
     total_rows = rows_rank * world * args.steps
     value = total_rows / el
 
-    # ---- N > 1: what the one collective per call costs: the same K steps without it
-    # (each rank's own evaluation only), with torch's all_gather (the headline's path) and, nccl
+    # ---- N > 1: what the one exchange per call costs: the same K steps without it
+    # (each rank's own evaluation only), with the headline's exchange (host shared memory when the
+    # ranks share a node, else torch's all_gather), with torch's all_gather over RCCL, and, nccl
     # only, with the engine's RCCL all-gather (ggp_comm_attach, its own handle; a failure is
     # reported, not raised); microseconds per call = the difference of the max-over-ranks times ----
     coll = None
@@ -475,9 +480,13 @@ def main() -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item()) / args.steps
         local_s = timed_steps(fg.total_likelihood)
-        coll = {"ranks": dist.get_world_size(), "backend": args.backend,
-                "local_only_ms_per_step": 1e3 * local_s, "torch_all_gather_ms_per_step": 1e3 * el / args.steps,
-                "torch_all_gather_us_per_call": 1e6 * (el / args.steps - local_s)}
+        coll = {"ranks": dist.get_world_size(), "backend": args.backend, "headline_exchange": obj.exchange_kind,
+                "local_only_ms_per_step": 1e3 * local_s, "headline_ms_per_step": 1e3 * el / args.steps,
+                "headline_us_per_call": 1e6 * (el / args.steps - local_s)}
+        ot = ShardedObjective(fg, node_exchange=False)
+        tor_s = timed_steps(ot.total_likelihood)
+        coll.update({"torch_all_gather_ms_per_step": 1e3 * tor_s,
+                     "torch_all_gather_us_per_call": 1e6 * (tor_s - local_s)})
         if args.backend == "nccl" and args.engine_comm_leg:
             os.environ.setdefault("GGP_COMM_TIMEOUT_S", "60")
             try:

@@ -6,10 +6,12 @@ row count (ties: critical-path length, then tree order).  Each rank keeps its sh
 device-resident data and carried root state; one objective call = every rank evaluates
 its shard, then ONE collective exchanges one double per rank (all_gather), and the
 partials are summed in rank order so the result is bitwise reproducible run to run.
-By default the collective is torch's all_gather_into_tensor (RCCL for an nccl group); opt-in
-(engine_comm=True / GGP_ENGINE_COMM=1) it runs inside the engine (include/ggp.h ggp_comm_attach:
-partial, RCCL all-gather and rank-order sum enqueued on the engine's stream behind the
-evaluation).  Both give the same bits.
+For ranks on one node (every rank of a one-node torchrun) the exchange goes through host shared
+memory (NodeExchange: the partials are already on the host, 16 bytes per rank is latency, not
+bandwidth); across nodes, or with GGP_NODE_EXCHANGE=0, it is torch's all_gather_into_tensor (RCCL
+for an nccl group); opt-in (engine_comm=True / GGP_ENGINE_COMM=1) it runs inside the engine
+(include/ggp.h ggp_comm_attach: partial, RCCL all-gather and rank-order sum enqueued on the
+engine's stream behind the evaluation).  All give the same bits.
 The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
 Scan samples and optimiser steps stay sequential (carried state), only the forest is
 parallel.
@@ -23,6 +25,10 @@ from __future__ import annotations
 import heapq
 import math
 import os
+import platform
+import secrets
+import socket
+import time
 
 import numpy as np
 
@@ -116,6 +122,120 @@ def combine_partials(partials, nan_flags):
     return s, -1
 
 
+class NodeExchange:
+    """An all-gather of a few doubles per rank through host shared memory, for ranks on one node.
+
+    Each call of the sharded objective exchanges 16 bytes per rank, values the ranks already hold
+    on the host (the engine returns its partial through mapped memory).  Over RCCL that is two
+    copies, a device collective and a stream synchronisation, ~36 us per call on the box
+    (DESIGN.md §5); here each rank writes its values and a sequence number into its own 128-byte
+    slot and polls the others' sequence numbers.  A slot holds two value sets used alternately: a
+    rank can run one exchange ahead of a slower one (it has published its next values) but never
+    two (it waits for every rank's number), so a set is never rewritten while being read.
+    x86-64 only: its stores are not reordered with other stores, nor its loads with other loads,
+    so the sequence number written after the values and read before them is a sufficient fence.
+    The segment (a /dev/shm file mapped by every rank) is unlinked as soon as every rank has mapped
+    it, so nothing is left behind whatever happens later.
+
+    The constructor is collective (every rank of the group calls it, in the same order); on any
+    failure every rank gets `ok == False` and the caller keeps torch's collective.
+    """
+
+    SLOT = 16   # float64 per rank: sequence number, two sets of up to 7 values
+
+    def __init__(self, dist, group=None, width: int = 2, timeout_s: float | None = None):
+        import mmap
+        import torch
+        assert 1 <= width <= (self.SLOT - 1) // 2
+        self.width = width
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.timeout = float(os.environ.get("GGP_COMM_TIMEOUT_S", "600")) if timeout_s is None else timeout_s
+        self.seq = 0
+        self.mm = None
+        self.a = None
+        size = self.world * self.SLOT * 8
+        backend = dist.get_backend(group)
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+
+        def agree(ok: bool) -> bool:
+            f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+            return int(f.item()) == 1
+
+        hosts = [None] * self.world
+        dist.all_gather_object(hosts, (socket.gethostname(), platform.machine()), group=group)
+        ok = len(set(hosts)) == 1 and hosts[0][1] in ("x86_64", "AMD64") and os.path.isdir("/dev/shm")
+        name = [None]
+        path = None
+        if ok and self.rank == 0:
+            path = f"/dev/shm/ggp_x_{os.getpid()}_{secrets.token_hex(6)}"
+            try:
+                self.mm = self._map(path, size, os.O_RDWR | os.O_CREAT | os.O_EXCL, mmap)
+                name[0] = path
+            except OSError:
+                self.mm = None
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(name, src=src, group=group)
+        ok = ok and name[0] is not None
+        if ok and self.rank != 0:
+            try:
+                self.mm = self._map(name[0], size, os.O_RDWR, mmap)
+            except OSError:
+                self.mm = None
+        self.ok = agree(ok and self.mm is not None)
+        if path is not None and name[0] is not None:
+            os.unlink(path)   # every rank has it mapped (or gave up): the name is no longer needed
+        if not self.ok:
+            self.close()
+            return
+        self.a = np.ndarray((self.world, self.SLOT), np.float64, buffer=self.mm)
+        if self.rank == 0:
+            self.a[:] = 0.0
+        agree(True)   # the slots are zeroed before any rank publishes
+
+    @staticmethod
+    def _map(path, size, flags, mmap):
+        fd = os.open(path, flags, 0o600)
+        try:
+            if flags & os.O_CREAT:
+                os.ftruncate(fd, size)
+            return mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+
+    def exchange(self, vals) -> np.ndarray:
+        """every rank's `width` values, [world, width], in rank order"""
+        s = self.seq + 1
+        lo = 1 + (s & 1) * self.width
+        hi = lo + self.width
+        mine = self.a[self.rank]
+        mine[lo:hi] = vals
+        mine[0] = s                     # published after the values
+        a, deadline = self.a, None
+        for r in range(self.world):
+            n = 0
+            while a[r, 0] < s:
+                n += 1
+                if (n & 0xFFF) == 0:
+                    now = time.monotonic()
+                    deadline = deadline or now + self.timeout
+                    if now > deadline:
+                        raise TimeoutError(f"NodeExchange: rank {r} did not publish call {s} in {self.timeout} s")
+        out = a[:, lo:hi].copy()        # read after the sequence numbers
+        self.seq = s
+        return out
+
+    def close(self) -> None:
+        self.a = None
+        if self.mm is not None:
+            try:
+                self.mm.close()
+            except BufferError:
+                pass
+            self.mm = None
+
+
 class ShardedObjective:
     """total_likelihood over a forest sharded across the ranks of a process group.
 
@@ -123,7 +243,7 @@ class ShardedObjective:
     """
 
     def __init__(self, device_forest, group=None, device=None, always_gather: bool = False,
-                 engine_comm: bool | None = None):
+                 engine_comm: bool | None = None, node_exchange: bool | None = None):
         import torch
         import torch.distributed as dist
         self.f = device_forest
@@ -146,6 +266,14 @@ class ShardedObjective:
             self._attach_engine(torch, dist, group)
         self.dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
                                                       if backend == "nccl" else torch.device("cpu"))
+        # ranks on one node: the partials' exchange through host shared memory (GGP_NODE_EXCHANGE=0:
+        # torch's collective)
+        self.xchg = None
+        if node_exchange is None:
+            node_exchange = os.environ.get("GGP_NODE_EXCHANGE", "1") != "0"
+        if not self.engine and (self.world > 1 or always_gather) and node_exchange:
+            x = NodeExchange(dist, group, width=2)
+            self.xchg = x if x.ok else None
         self._send = torch.zeros(2, dtype=torch.float64, device=self.dev)
         self._recv = torch.zeros(2 * self.world, dtype=torch.float64, device=self.dev)
         # per call, RCCL moves 16 B per rank: stage them through pinned host tensors (one async
@@ -224,6 +352,19 @@ class ShardedObjective:
             out[k] = s
         return out
 
+    @property
+    def exchange_kind(self) -> str:
+        if self.engine:
+            return "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
+        if self.xchg is not None:
+            return "host shared memory (NodeExchange): 16 B per rank, rank-order sum"
+        return "torch all_gather_into_tensor of 16 B per rank, rank-order sum"
+
+    def close(self) -> None:
+        if self.xchg is not None:
+            self.xchg.close()
+            self.xchg = None
+
     def total_likelihood(self, params) -> float:
         if self.engine:   # the engine returns the rank-order sum (or raises, on every rank)
             return self.f.total_likelihood(params)
@@ -232,6 +373,13 @@ class ShardedObjective:
             if isnan:
                 raise err
             return v
+        if self.xchg is not None:
+            got = self.xchg.exchange((v, 1.0 if isnan else 0.0))
+            total, nan_rank = combine_partials(got[:, 0], got[:, 1] != 0)
+            if nan_rank >= 0:
+                raise err if (err is not None and nan_rank == self.dist.get_rank(self.group)) else \
+                    LikelihoodIsNan(-1, -1, f"rank {nan_rank}")
+            return total
         self._h_send_np[0] = v
         self._h_send_np[1] = 1.0 if isnan else 0.0
         if self._cuda:

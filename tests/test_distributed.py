@@ -223,3 +223,84 @@ def test_strong_split_init_stats_and_sharded_chain():
     # the statistics differ from the single-process ones in the last bits, and the totals move by
     # ~5e-11 relative for that (the path's conditioning): the north star's bar
     np.testing.assert_allclose(res[0][3], want, rtol=1e-9)
+
+
+def _worker_xchg(rank, world, port, q):
+    import random
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import NodeExchange, ShardedObjective, shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        # the exchange itself: many back-to-back calls with ranks running at uneven speeds
+        x = NodeExchange(dist, None, width=2)
+        assert x.ok
+        rnd = random.Random(rank)
+        seen = []
+        for k in range(300):
+            if rnd.random() < 0.05:
+                time.sleep(0.002 * rnd.random())
+            got = x.exchange((rank * 1000.0 + k, -k))
+            seen.append(bool(np.array_equal(got[:, 0], np.arange(world) * 1000.0 + k)
+                             and np.all(got[:, 1] == -k)))
+        # a rank that never publishes: the others time out instead of waiting forever
+        y = NodeExchange(dist, None, width=1, timeout_s=0.5)
+        timed_out = False
+        if rank != world - 1:
+            try:
+                y.exchange((1.0,))
+            except TimeoutError:
+                timed_out = True
+        dist.barrier()
+        y.close()
+        # the objective: the shared-memory path and torch's give the same bits, NaN included
+        full = g.HostForest.synthetic(12, 40)
+        mine = shard(full, rank, world)
+        res = {}
+        for mode in ("1", "0"):
+            os.environ["GGP_NODE_EXCHANGE"] = mode
+            obj = ShardedObjective(_OracleShard(mine))
+            assert (obj.xchg is not None) == (mode == "1")
+            vals = [obj.total_likelihood(P0) for _ in range(2)]
+            bad = list(P0)
+            bad[2] = -1.0
+            try:
+                obj.total_likelihood(bad)
+                nan_ok = False
+            except g.LikelihoodIsNan:
+                nan_ok = True
+            res[mode] = (vals, nan_ok)
+        x.close()
+        q.put((rank, all(seen), timed_out, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_node_exchange_four_ranks():
+    """NodeExchange (host shared memory, the partials' exchange for ranks on one node): 300
+    back-to-back all-gathers at uneven rank speeds, a bounded wait when a rank never publishes, and
+    the sharded objective bitwise the same through it as through torch's all_gather, NaN included;
+    nothing left in /dev/shm"""
+    import glob
+    world = 4
+    before = set(glob.glob("/dev/shm/ggp_x_*"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_xchg, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, seen_ok, timed_out, r in res:
+        assert seen_ok, rank
+        assert timed_out == (rank != world - 1), rank
+        assert r["1"] == r["0"], rank
+        assert r["1"][1]
+    assert res[0][3]["1"][0] == res[-1][3]["1"][0]
+    assert set(glob.glob("/dev/shm/ggp_x_*")) == before

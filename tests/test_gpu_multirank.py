@@ -93,6 +93,10 @@ def test_bench_two_ranks_gloo_rehearsal():
     # the collective's cost per call, and the rank count (gloo here: torch's path only)
     co = out["collective"]
     assert co["ranks"] == 2 and co["backend"] == "gloo" and co["local_only_ms_per_step"] > 0
+    # the headline's exchange: host shared memory (both ranks on this node), cheaper than torch's
+    assert co["headline_exchange"].startswith("host shared memory"), co
+    assert c4["collective"]["kind"].startswith("host shared memory"), c4
+    assert co["headline_ms_per_step"] < co["torch_all_gather_ms_per_step"], co
     print("collective:", co)
     c5 = out["c5_predict_split"]
     assert c5["rows"] == 2000 * 500 and c5["shards_per_rank"] == 2 and c5["rows_per_s"] > 0
