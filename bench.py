@@ -778,10 +778,10 @@ def main() -> int:
         fj = g.Forest(hj, device=local)
         nrj = hj.n_rows
         jcap = 1 << 21   # the CLI's max_cap
-        jbuf = (np.empty((jcap, 2), np.int64), np.empty((jcap, 72)))
+        jbuf = (np.empty((jcap, 2), np.int64), np.empty((jcap, 44)))   # packed, as the CLI takes them
         for b_ in jbuf:
             b_.fill(0)   # paged in, as a long-running writer's buffers are
-        fj.joints(P_EXAMPLE, 1e-10, 0, min(nrj, 256), out=jbuf)   # warm-up: smoother tables cached
+        fj.joints(P_EXAMPLE, 1e-10, 0, min(nrj, 256), out=jbuf, packed=True)   # warm-up: smoother tables cached
         barrier()
         t1 = time.perf_counter()
         nj, lo, chunk, n_calls = 0, 0, 4096, 0
@@ -789,7 +789,7 @@ def main() -> int:
             hi = min(nrj, lo + chunk)
             n_calls += 1
             try:
-                idx_j, _ = fj.joints(P_EXAMPLE, 1e-10, lo, hi, out=jbuf)
+                idx_j, _ = fj.joints(P_EXAMPLE, 1e-10, lo, hi, out=jbuf, packed=True)
             except g.GGPError:   # more than the CLI's max_cap: split the range, as the CLI does
                 chunk = max(1, (hi - lo) // 2)
                 continue
@@ -804,7 +804,8 @@ def main() -> int:
                          "joints), reused host buffers",
                "rows": nrj, "joints": nj, "calls": n_calls, "seconds": jel, "joints_per_s": nj / jel, "start_rows_per_s": nrj / jel,
                "note": "BASELINE configs[4]'s -j leg on its tree shape (SURVEY 8(d) subset); joints computed on "
-                       "the GPU and copied to the host (72 doubles each), parameter tables cached per parameters"}
+                       "the GPU and copied to the host as the CLI takes them (ggp_joints_packed: 8 means and "
+                       "the covariance's upper triangle, 44 doubles each), parameter tables cached per parameters"}
         fj.close()
 
 

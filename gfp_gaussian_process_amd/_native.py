@@ -73,6 +73,9 @@ ENGINE_SYMBOLS = {
                                            ctypes.POINTER(ctypes.c_float)]),
     "ggp_joints": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, ctypes.c_double, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int64, c_int64_p, c_double_p, c_int64_p]),
+    "ggp_joints_packed": (ctypes.c_int, [ctypes.c_void_p, c_double_p, ctypes.c_int32, ctypes.c_double,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_int64_p, c_double_p,
+                                         c_int64_p]),
     "ggp_reset_state": (ctypes.c_int, [ctypes.c_void_p]),
     "ggp_get_state": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "ggp_set_state": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),

@@ -2232,8 +2232,26 @@ __global__ __launch_bounds__(64) void k_joint_walk(DevForest F, const double *__
     counts[i] = cnt;
 }
 
-// single-pass -j: start i's joints from its bound slots [boff[i], ...) to the packed output at
-// coff[i] (one workgroup per start, the (start, target) pairs and the 72 values contiguous)
+// the packed joint record (ggp_joints_packed): the 8 means, then the covariance's upper triangle
+// row by row (output_upper_triangle, predictions.h:540-551) -- the 44 values the CLI prints
+constexpr int kJPacked = 44;
+struct JUpper {
+    unsigned char off[kJPacked];   // record value -> offset in the 72-value record
+};
+constexpr JUpper make_jupper()
+{
+    JUpper u{};
+    for (int k = 0; k < 8; ++k) u.off[k] = (unsigned char)k;
+    int q = 8;
+    for (int m = 0; m < 8; ++m)
+        for (int k = m; k < 8; ++k) u.off[q++] = (unsigned char)(8 + 8 * m + k);
+    return u;
+}
+GGP_DEV constexpr JUpper kJUpper = make_jupper();
+
+// -j: start i's joints from its slots [boff[i], ...) of the 72-value records to the output at
+// coff[i] in W-value records (72: as they are; 44: packed), one workgroup per start
+template <int W>
 __global__ __launch_bounds__(256) void k_joint_pack(int64_t n_starts, const int64_t *__restrict__ boff,
                                                     const int64_t *__restrict__ coff, const int64_t *__restrict__ counts,
                                                     const int64_t *__restrict__ src_idx, const double *__restrict__ src_val,
@@ -2243,8 +2261,11 @@ __global__ __launch_bounds__(256) void k_joint_pack(int64_t n_starts, const int6
     if (i >= n_starts) return;
     const int64_t n = counts[i], b = boff[i], c = coff[i];
     for (int64_t k = threadIdx.x; k < 2 * n; k += blockDim.x) dst_idx[2 * c + k] = src_idx[2 * b + k];
-    for (int64_t k = threadIdx.x; k < (int64_t)kJStart * n; k += blockDim.x)
-        dst_val[(size_t)kJStart * c + k] = src_val[(size_t)kJStart * b + k];
+    for (int64_t k = threadIdx.x; k < (int64_t)W * n; k += blockDim.x) {
+        const int64_t q = k / W;
+        const int e = (int)(k - q * W);
+        dst_val[(size_t)W * c + k] = src_val[(size_t)kJStart * (b + q) + (W == kJStart ? e : kJUpper.off[e])];
+    }
 }
 
 
@@ -3454,7 +3475,7 @@ void scatter_rows(const ggp_forest *f, const Shard *s, const double *src, int64_
 // -j on one shard (local start rows [r_lo, r_hi)): collect_joint_distributions (correlation_tree.h
 // :464-651).  The smoother and the per-row tables are kept for the parameters they were made with.
 int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi, int64_t cap,
-                 int64_t *out_idx, double *out_val, int64_t *n_out)
+                 int64_t *out_idx, double *out_val, int64_t *n_out, int width)
 {
     const int64_t nc = f->n_cells, nr = f->n_rows;
     *n_out = 0;
@@ -3514,13 +3535,25 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
                            d_stack_j, d_stack_c, d_counts, offs, o_idx, o_val);
         return hipGetLastError();
     };
-    // the packed output buffer for `total` joints: (start, target) pairs, then the values
+    // the output buffer for `total` joints: (start, target) pairs, then width values each
     auto out_buf = [&](int64_t total, int64_t *&d_idx, double *&d_val) {
         const size_t b_idx = (size_t)total * 2 * sizeof(int64_t);
-        auto *out = (char *)jw_reserve(&f->d_jw_out, &f->jw_out_bytes, (size_t)total * kJointBytes);
+        auto *out = (char *)jw_reserve(&f->d_jw_out, &f->jw_out_bytes,
+                                       b_idx + (size_t)total * width * sizeof(double));
         d_idx = (int64_t *)out;
         d_val = out ? (double *)(out + b_idx) : nullptr;
         return out != nullptr;
+    };
+    // start i's joints from slots [from[i], ...) of 72-value records to [to[i], ...) in width-value records
+    auto pack = [&](const int64_t *from, const int64_t *to, const int64_t *s_idx, const double *s_val, int64_t *o_idx,
+                    double *o_val) {
+        if (width == kJStart)
+            hipLaunchKernelGGL(k_joint_pack<kJStart>, dim3((unsigned)ns), dim3(256), 0, f->stream, ns, from, to,
+                               (const int64_t *)d_counts, s_idx, s_val, o_idx, o_val);
+        else
+            hipLaunchKernelGGL(k_joint_pack<kJPacked>, dim3((unsigned)ns), dim3(256), 0, f->stream, ns, from, to,
+                               (const int64_t *)d_counts, s_idx, s_val, o_idx, o_val);
+        return hipGetLastError();
     };
     std::vector<int64_t> counts(ns), off(ns + 1);
     // single pass: every start walks once into slots sized by its bound (the rows after it in its
@@ -3575,16 +3608,11 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
                     return GGP_ENOMEM;
                 }
                 e = hipMemcpyAsync(d_coff, off.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
-                if (e == hipSuccess) {
-                    hipLaunchKernelGGL(k_joint_pack, dim3((unsigned)ns), dim3(256), 0, f->stream, ns, (const int64_t *)d_off,
-                                       (const int64_t *)d_coff, (const int64_t *)d_counts, (const int64_t *)b_idx,
-                                       (const double *)b_val, d_idx, d_val);
-                    e = hipGetLastError();
-                }
+                if (e == hipSuccess) e = pack(d_off, d_coff, b_idx, b_val, d_idx, d_val);
                 if (e == hipSuccess)
                     e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
                 if (e == hipSuccess)
-                    e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+                    e = hipMemcpyAsync(out_val, d_val, (size_t)total * width * sizeof(double), hipMemcpyDeviceToHost, f->stream);
                 if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
             }
         }
@@ -3609,11 +3637,24 @@ int shard_joints(Shard *f, const double *params, int32_t n_seg, double tol, int6
                 return GGP_ENOMEM;
             }
             e = hipMemcpyAsync(d_off, off.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->stream);
-            if (e == hipSuccess) e = walk(d_off, d_idx, d_val);
+            if (e == hipSuccess && width == kJStart) {
+                e = walk(d_off, d_idx, d_val);
+            } else if (e == hipSuccess) {   // packed: emit 72-value records, then pack them
+                auto *raw = (char *)jw_reserve(&f->d_jw_bnd, &f->jw_bnd_bytes, (size_t)total * kJointBytes);
+                if (!raw) {
+                    cleanup();
+                    g_last_err = "ggp_joints: device allocation failed";
+                    return GGP_ENOMEM;
+                }
+                auto *r_idx = (int64_t *)raw;
+                auto *r_val = (double *)(raw + (size_t)total * 2 * sizeof(int64_t));
+                e = walk(d_off, r_idx, r_val);
+                if (e == hipSuccess) e = pack(d_off, d_off, r_idx, r_val, d_idx, d_val);
+            }
             if (e == hipSuccess)
                 e = hipMemcpyAsync(out_idx, d_idx, (size_t)total * 2 * sizeof(int64_t), hipMemcpyDeviceToHost, f->stream);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(out_val, d_val, (size_t)total * kJStart * sizeof(double), hipMemcpyDeviceToHost, f->stream);
+                e = hipMemcpyAsync(out_val, d_val, (size_t)total * width * sizeof(double), hipMemcpyDeviceToHost, f->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
         }
     }
@@ -4796,8 +4837,8 @@ int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out)
     return GGP_OK;
 }
 
-int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
-               int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+static int joints_impl(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
+                       int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out, int width)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
@@ -4806,7 +4847,7 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
     *n_out = 0;
     if (f->n_cells == 0 || r_hi <= r_lo) return GGP_OK;
     if (f->shards.size() == 1 && f->shards[0]->cell_g.empty())
-        return shard_joints(f->shards[0], params, n_seg, tol, r_lo, r_hi, cap, out_idx, out_val, n_out);
+        return shard_joints(f->shards[0], params, n_seg, tol, r_lo, r_hi, cap, out_idx, out_val, n_out, width);
     // several shards: every start row belongs to one; count first, then each shard's joints in
     // global numbering, merged by start row (each start's joints keep their add order)
     const size_t ns = f->shards.size();
@@ -4814,7 +4855,7 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
     int64_t total = 0;
     for (size_t k = 0; k < ns; ++k) {
         local_rows(f, f->shards[k], r_lo, r_hi, lo[k], hi[k]);
-        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], 0, nullptr, nullptr, &cnt[k]);
+        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], 0, nullptr, nullptr, &cnt[k], width);
         if (rc != GGP_OK) return rc;
         total += cnt[k];
     }
@@ -4825,13 +4866,13 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
     std::vector<std::pair<int64_t, int64_t>> order;   // (global start, position in idx/val)
     order.reserve((size_t)total);
     idx.reserve((size_t)total * 2);
-    val.reserve((size_t)total * kJStart);
+    val.reserve((size_t)total * width);
     for (size_t k = 0; k < ns; ++k) {
         if (!cnt[k]) continue;
         std::vector<int64_t> li((size_t)cnt[k] * 2);
-        std::vector<double> lv((size_t)cnt[k] * kJStart);
+        std::vector<double> lv((size_t)cnt[k] * width);
         int64_t got = 0;
-        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], cnt[k], li.data(), lv.data(), &got);
+        const int rc = shard_joints(f->shards[k], params, n_seg, tol, lo[k], hi[k], cnt[k], li.data(), lv.data(), &got, width);
         if (rc != GGP_OK) return rc;
         for (int64_t q = 0; q < got; ++q) {
             const int64_t gs = g_row(f, f->shards[k], li[2 * q]), gt = g_row(f, f->shards[k], li[2 * q + 1]);
@@ -4839,7 +4880,7 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
             idx.push_back(gs);
             idx.push_back(gt);
         }
-        val.insert(val.end(), lv.begin(), lv.begin() + got * kJStart);
+        val.insert(val.end(), lv.begin(), lv.begin() + got * width);
     }
     std::stable_sort(order.begin(), order.end(),
                      [](const std::pair<int64_t, int64_t> &a, const std::pair<int64_t, int64_t> &b) { return a.first < b.first; });
@@ -4847,9 +4888,21 @@ int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, i
         const int64_t p = order[q].second;
         out_idx[2 * q] = idx[2 * p];
         out_idx[2 * q + 1] = idx[2 * p + 1];
-        std::memcpy(out_val + q * kJStart, &val[(size_t)p * kJStart], kJStart * sizeof(double));
+        std::memcpy(out_val + q * width, &val[(size_t)p * width], width * sizeof(double));
     }
     return GGP_OK;
+}
+
+int ggp_joints(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
+               int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+{
+    return joints_impl(f, params, n_seg, tol, r_lo, r_hi, cap, out_idx, out_val, n_out, kJStart);
+}
+
+int ggp_joints_packed(ggp_forest *f, const double *params, int32_t n_seg, double tol, int64_t r_lo, int64_t r_hi,
+                      int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out)
+{
+    return joints_impl(f, params, n_seg, tol, r_lo, r_hi, cap, out_idx, out_val, n_out, kJPacked);
 }
 
 // ---- test-only device math (tests/test_gpu_device_math.py) --------------------------------

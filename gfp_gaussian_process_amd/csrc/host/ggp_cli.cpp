@@ -767,7 +767,8 @@ void run_prediction(const ggp_dataset *d, std::vector<Params> &plist, std::map<s
 // P(z_column, z_start | D) as 8 means and the 36-entry upper triangle of its covariance, or
 // 44 empty fields.  Joint_vector::add stores a joint in every column whose (cell_id, time)
 // equals the target's, the last add winning.  The joints come from the GPU (ggp_joints) in
-// the reference's add order, a bounded range of start rows per call.
+// the reference's add order, a bounded range of start rows per call, packed as they are printed
+// (ggp_joints_packed: the 8 means and the covariance's upper triangle).
 void write_commas(std::ostream &file, int64_t count)
 {
     static const std::string block(44 * 1024, ',');
@@ -840,16 +841,16 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
         }
         file << "\n";
     }
-    const int64_t max_cap = (int64_t)1 << 21;        // joints per call (72 doubles each)
+    const int64_t max_cap = (int64_t)1 << 21;        // joints per call (44 doubles each: ggp_joints_packed)
     int64_t cap = (int64_t)1 << 14, chunk = 4096;
     std::vector<int64_t> idx((size_t)(2 * cap));
-    std::vector<double> val((size_t)(72 * cap));
+    std::vector<double> val((size_t)(44 * cap));
     int64_t logged = -1;
     for (int64_t lo = 0; lo < nr;) {
         const int64_t hi = std::min(nr, lo + chunk), s_lo = lo;
         int64_t n_out = 0;
-        const int rc = ggp_joints(F.gpu, pv.data(), (int32_t)plist.size(), tol, lo, hi, cap, idx.data(), val.data(),
-                                  &n_out);
+        const int rc = ggp_joints_packed(F.gpu, pv.data(), (int32_t)plist.size(), tol, lo, hi, cap, idx.data(),
+                                         val.data(), &n_out);
         if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_joints: ") + ggp_strerror(rc));
         if (n_out > cap) {   // buffers too small: split the range, or grow them
             if (n_out > max_cap && hi - lo > 1) {
@@ -857,7 +858,7 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             } else {
                 cap = n_out;
                 idx.resize((size_t)(2 * cap));
-                val.resize((size_t)(72 * cap));
+                val.resize((size_t)(44 * cap));
             }
             continue;
         }
@@ -890,15 +891,13 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
                 if (sparse) {   // every column the add reaches, in add order
                     for (int64_t k = k0; k < k1; ++k) {
                         const int64_t tgt = idx[(size_t)(2 * k + 1)];
-                        const double *j = &val[(size_t)(72 * k)];
+                        const double *j = &val[(size_t)(44 * k)];   // means, then the upper triangle
                         auto line = [&](int64_t col) {
                             out.i64(s);
                             out.ch(',');
                             out.i64(col);
                             out.ch(',');
-                            out.values(j, 8);
-                            out.ch(',');
-                            out.upper(j + 8, 8);
+                            out.values(j, 44);
                             out.ch('\n');
                         };
                         if (dup[(size_t)tgt] < 0)
@@ -925,11 +924,9 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
                 int64_t prev = 0;
                 for (const auto &e : cols) {             // Joint_vector::write
                     out.fill((size_t)(44 * (e.first - prev)), ',');
-                    const double *j = &val[(size_t)(72 * e.second)];
+                    const double *j = &val[(size_t)(44 * e.second)];   // means, then the upper triangle
                     out.ch(',');
-                    out.values(j, 8);
-                    out.ch(',');
-                    out.upper(j + 8, 8);
+                    out.values(j, 44);
                     prev = e.first + 1;
                 }
                 out.fill((size_t)(44 * (nr - prev)), ',');
@@ -946,7 +943,7 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
             if (want > cap) {
                 cap = want;
                 idx.resize((size_t)(2 * cap));
-                val.resize((size_t)(72 * cap));
+                val.resize((size_t)(44 * cap));
             }
         }
     }

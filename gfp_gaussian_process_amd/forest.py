@@ -629,28 +629,31 @@ class Forest:
         return a.value, b.value
 
     def joints(self, params_per_segment, tol: float = 1e-10, r_lo: int = 0, r_hi=None, cap: int = 1 << 22,
-               out=None):
+               out=None, packed: bool = False):
         """-j compute for start rows [r_lo, r_hi) (ggp_joints): (idx [k, 2] = (start, target) rows,
         val [k, 72] = mean[8], row-major cov[64]) in the reference's add order.
-        out=(idx, val): caller-owned int64 [cap, 2] and float64 [cap, 72] C-contiguous arrays to fill
-        (cap = their length); the results are views of them, overwritten by the next call that gets
-        the same buffers.  A caller streaming many start-row ranges (as the CLI does) reuses one pair
-        instead of paging in fresh arrays on every call."""
+        packed=True (ggp_joints_packed): val [k, 44] = mean[8], then the covariance's upper triangle
+        row by row -- the values the -j writer prints, 39% fewer bytes from the device.
+        out=(idx, val): caller-owned int64 [cap, 2] and float64 [cap, 72 or 44] C-contiguous arrays to
+        fill (cap = their length); the results are views of them, overwritten by the next call that
+        gets the same buffers.  A caller streaming many start-row ranges (as the CLI does) reuses one
+        pair instead of paging in fresh arrays on every call."""
+        w = 44 if packed else 72
         p = np.ascontiguousarray(np.atleast_2d(params_per_segment), np.float64)
         r_hi = self.n_rows if r_hi is None else r_hi
         n = ctypes.c_int64()
         if out is None:
             idx = np.zeros((cap, 2), np.int64)
-            val = np.zeros((cap, 72))
+            val = np.zeros((cap, w))
         else:
             idx, val = out
             if (idx.dtype != np.int64 or val.dtype != np.float64 or idx.ndim != 2 or idx.shape[1] != 2
-                    or val.ndim != 2 or val.shape[1] != 72 or not idx.flags.c_contiguous or not val.flags.c_contiguous):
-                raise ValueError("out must be (int64 [cap, 2], float64 [cap, 72]) C-contiguous arrays")
+                    or val.ndim != 2 or val.shape[1] != w or not idx.flags.c_contiguous or not val.flags.c_contiguous):
+                raise ValueError(f"out must be (int64 [cap, 2], float64 [cap, {w}]) C-contiguous arrays")
             cap = min(len(idx), len(val))
-        self._check(self._lib.ggp_joints(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0], tol, r_lo, r_hi, cap,
-                                         idx.ctypes.data_as(N.c_int64_p), val.ctypes.data_as(N.c_double_p),
-                                         ctypes.byref(n)))
+        fn = self._lib.ggp_joints_packed if packed else self._lib.ggp_joints
+        self._check(fn(self._h, p.ctypes.data_as(N.c_double_p), p.shape[0], tol, r_lo, r_hi, cap,
+                       idx.ctypes.data_as(N.c_int64_p), val.ctypes.data_as(N.c_double_p), ctypes.byref(n)))
         if n.value > cap:
             raise GGPError(f"{n.value} joints exceed cap {cap}: use a larger cap or a smaller row range")
         return idx[: n.value], val[: n.value]

@@ -355,3 +355,26 @@ def test_joints_single_pass_bitwise_two_pass(monkeypatch):
     for (lo, hi), (i1, v1), (i2, v2) in zip(ranges, got["2048"], got["0"]):
         assert len(i1) > 0 or hi - lo == 1, (lo, hi)
         assert np.array_equal(i1, i2) and np.array_equal(v1, v2), (lo, hi)
+
+
+def test_joints_packed_is_the_printed_values(monkeypatch):
+    """ggp_joints_packed: the same joints as ggp_joints, each as its 8 means and its covariance's
+    upper triangle row by row (what the -j writer prints), on the single pass and on the two passes"""
+    import gfp_gaussian_process_amd as g
+    hf = g.HostForest.synthetic(3, 500, seed=11)
+    iu = np.triu_indices(8)
+    for mb in ("2048", "0"):
+        monkeypatch.setenv("GGP_JOINT_SLOT_MB", mb)
+        f = g.Forest(hf)
+        for lo, hi in ((0, hf.n_rows), (123, 777)):
+            i72, v72 = f.joints(P, 1e-10, lo, hi, cap=1 << 20)
+            i44, v44 = f.joints(P, 1e-10, lo, hi, cap=1 << 20, packed=True)
+            want = np.concatenate([v72[:, :8], v72[:, 8:].reshape(-1, 8, 8)[:, iu[0], iu[1]]], axis=1)
+            assert len(i72) > 0 and v44.shape == (len(i72), 44)
+            assert np.array_equal(i44, i72) and np.array_equal(v44, want), (mb, lo, hi)
+        buf = (np.zeros((1 << 20, 2), np.int64), np.zeros((1 << 20, 44)))
+        i_b, v_b = f.joints(P, 1e-10, 0, hf.n_rows, out=buf, packed=True)
+        assert np.shares_memory(v_b, buf[1]) and len(i_b) > 0
+        with pytest.raises(ValueError):
+            f.joints(P, 1e-10, 0, 4, out=(np.zeros((4, 2), np.int64), np.zeros((4, 72))), packed=True)
+        f.close()

@@ -143,6 +143,11 @@ def test_joints_bitwise_for_any_device_list():
         ig, vg = three.joints(P, 1e-10, lo, hi)
         assert len(iw) > 0
         assert np.array_equal(iw, ig) and np.array_equal(vw, vg)
+        # the packed records (ggp_joints_packed) through the shard merge: means + upper triangle
+        ip, vp = three.joints(P, 1e-10, lo, hi, packed=True)
+        iu = np.triu_indices(8)
+        want = np.concatenate([vw[:, :8], vw[:, 8:].reshape(-1, 8, 8)[:, iu[0], iu[1]]], axis=1)
+        assert np.array_equal(ip, iw) and np.array_equal(vp, want)
 
 
 def _cli_files(tmp_path, csv, cfg, pf, tag, extra):
