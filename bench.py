@@ -269,6 +269,32 @@ def run_example_parity() -> dict:
     return out
 
 
+def host_split(step_t, trace) -> dict:
+    """the timed steps' wall times and, per step, the engine's host split (ggp_call_trace: enqueue,
+    wait for the completion, result; the path launch's own device time and clock), so the line shows
+    where a step's time goes beyond the kernel: min / median / max over the steps and the first step
+    on its own"""
+    wall = np.diff(np.asarray(step_t)) * 1e6
+
+    def stats(x):
+        x = np.asarray(x, float)
+        return {"min": float(x.min()), "median": float(np.median(x)), "max": float(x.max()), "first": float(x[0]),
+                "mean": float(x.mean())}
+    out = {"wall_us": stats(wall)}
+    if trace is not None and len(trace) == len(wall):
+        enq, wait, res, kern, mhz = (trace[:, k] for k in range(5))
+        out.update({"enqueue_us": stats(enq), "wait_us": stats(wait), "result_us": stats(res)})
+        if np.all(kern > 0):
+            out.update({"kernel_us": stats(kern), "shader_mhz": stats(mhz),
+                        "host_us": stats(wall - kern),
+                        "dispatch_and_completion_us": stats(wait - kern),
+                        "python_us": stats(wall - enq - wait - res)})
+        out["note"] = ("per timed step: wall = python + enqueue + wait + result; wait = dispatch + kernel + the "
+                       "completion's trip to the host (kernel: the path launch's first block start to its publishing "
+                       "block's end on the device's 100 MHz counter, ggp_call_trace)")
+    return out
+
+
 def leg_fp64(cnt, kind: str, rows_per_s: float, n_simd: int, per_row_useful: bool = False, note: str = ""):
     """FP64 and VALU-issue fractions of a bench leg from the PMC pass of this build
     (profiles/fp64_counts.json, tools/fp64_summary.py kind `kind`): achieved FP64 = flops per row x
@@ -439,20 +465,31 @@ def main() -> int:
                            "last": float(scan[-1]),
                            "note": "-s: each sample from the carried state the previous left; every rank "
                                    "chains its trees (ggp_total_loglik_chain), one all_gather of the partials"}
-        if world > 1:
-            o4.close()
-        f4.close()
+        # the C4 handle is released after the headline: freeing its device memory here would put
+        # an idle gap between the leg's full-chip work and the headline's steps
     for _ in range(args.warmup):
         obj.total_likelihood(P_EXAMPLE)
 
-    # ---- timed region: exactly K steps ----
+    # ---- timed region: exactly K steps (each step's wall time kept: the line's `steps_us`; the
+    # collector paused so no collection lands inside a step) ----
+    import gc
+    gc.disable()
+    step_t = [0.0] * (args.steps + 1)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    step_t[0] = t0
+    for k in range(args.steps):
         ll = obj.total_likelihood(P_EXAMPLE)
+        step_t[k + 1] = time.perf_counter()
     barrier()
     el = time.perf_counter() - t0
+    gc.enable()
     clock_timed = fg.launch_clock()   # the last timed launch's shader clock (wave schedule only)
+    steps_us = host_split(step_t, fg.call_trace(args.steps) if hasattr(fg, "call_trace") else None)
+    if c4s is not None:
+        if world > 1:
+            o4.close()
+        f4.close()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -892,6 +929,7 @@ def main() -> int:
             },
             "fp64": fp64,
             "total_log_likelihood": ll,
+            "steps_us": steps_us,
             "clock": None if clock_timed is None else {
                 "shader_mhz_last_timed_launch": clock_timed[0], "window_us": clock_timed[1],
                 "shader_mhz_profiled_launches": clocks,

@@ -60,19 +60,26 @@ def build(verbose: bool = False, force: bool = False) -> dict:
         if os.path.exists(p):
             eng_deps.append(p)
     eng = os.path.join(LIB, "libggp.so")
-    if force or not _newer(eng, eng_deps):
-        # -cuid: a fixed offload compilation-unit id (clang derives it from the source path by
-        # default), so the same sources give the same bytes in any checkout -- the PMC stamps in
-        # profiles/ are keyed on this library's sha256 (bench.py)
-        _run([HIPCC, *HIP_FLAGS, "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src, "-ldl"],
-             verbose)
-    out["libggp"] = eng
-    # the same engine in the oracle's arithmetic (-DGGP_EXACT: glibc's exp, no products, no fma
-    # contraction; DESIGN.md §2 "Exact arithmetic"), selected with GGP_ENGINE_LIB=libggp_exact.so
     eng_x = os.path.join(LIB, "libggp_exact.so")
+    # -cuid: a fixed offload compilation-unit id (clang derives it from the source path by
+    # default), so the same sources give the same bytes in any checkout -- the PMC stamps in
+    # profiles/ are keyed on this library's sha256 (bench.py).  The second library is the same
+    # engine in the oracle's arithmetic (-DGGP_EXACT: glibc's exp, no products, no fma
+    # contraction; DESIGN.md §2 "Exact arithmetic"), selected with GGP_ENGINE_LIB=libggp_exact.so.
+    # The two compile concurrently (one hipcc each).
+    jobs = []
+    if force or not _newer(eng, eng_deps):
+        jobs.append([HIPCC, *HIP_FLAGS, "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng, eng_src,
+                     "-ldl"])
     if force or not _newer(eng_x, eng_deps):
-        _run([HIPCC, *HIP_FLAGS, "-DGGP_EXACT", "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o", eng_x,
-              eng_src, "-ldl"], verbose)
+        jobs.append([HIPCC, *HIP_FLAGS, "-DGGP_EXACT", "-cuid=ggp_engine", "-shared", f"-I{INC}", f"-I{CSRC}", "-o",
+                     eng_x, eng_src, "-ldl"])
+    if jobs:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(len(jobs)) as ex:
+            for fut in [ex.submit(_run, j, verbose) for j in jobs]:
+                fut.result()
+    out["libggp"] = eng
     out["libggp_exact"] = eng_x
     # --- host ingest ---
     host_src = os.path.join(CSRC, "host", "ggp_host.cpp")

@@ -845,7 +845,8 @@ struct ChainRed {
     double *host_sum;
     long long *host_nan;
     int n_lblocks;                // 0: no in-launch reduction
-    unsigned long long *clk;      // mapped: block 0's shader-clock and 100 MHz ticks over its path
+    unsigned long long *clk;      // mapped: block 0's shader-clock and 100 MHz ticks over its path, its
+                                  // start (100 MHz counter), the publishing block's end (ggp_call_trace)
 };
 constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
 
@@ -978,6 +979,9 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
     __builtin_amdgcn_s_waitcnt(0);
     if (add_agent(R.done) + 1 != (unsigned)R.n_lblocks) return;
     zero_agent(R.done);
+    if (R.clk)   // the launch's end on the 100 MHz counter (ggp_call_trace), before the sequence number
+        __hip_atomic_store(R.clk + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     // every block's slots reached host memory before its count: each block's system-scope stores to
     // the fine-grained (uncached) host slots are acknowledged by the fabric before its s_waitcnt(0)
     // lets the count go out, so they are host-visible when the last block sees the full count.
@@ -1460,6 +1464,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(red.clk, c1 - clk_c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(red.clk + 1, r1 - clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(red.clk + 2, clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (red.n_lblocks > 0) chain_reduce(red, red_unpark(lds + W::L_RED, lane), call_seq, lane, cell_ll, cell_nan, lds + W::L_RX0);
     GGP_TL(6);
@@ -2655,6 +2660,7 @@ struct Shard {
     volatile int64_t *h_seq = nullptr;
     int64_t *m_seq = nullptr;
     volatile unsigned long long *h_clk = nullptr;   // path launches: block 0's clock counters
+    unsigned long long clk_snap[4] = {0, 0, 0, 0}; // h_clk as the last completed launch left it
     unsigned long long *m_clk = nullptr;
     // the largest |dt| of any propagation of the shard (in-cell steps and divisions): with the
     // parameters it bounds |k dt| for the wave schedule's product factors exp(-gl dt), exp(-gq dt),
@@ -2752,8 +2758,18 @@ static void comm_fail(Comm *c)
     }
 }
 
+// one objective call's host split (ggp_call_trace)
+struct CallRec {
+    double enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call;
+};
+constexpr int kCallRing = 512;
+
 struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0, n_trees = 0, blk_trees = 1, n_blocks = 0;
+    std::chrono::steady_clock::time_point tr_t0, tr_t1, tr_t2;   // the pending call's entry, enqueue end, wait end
+    bool tr_pending = false;
+    int64_t tr_n = 0;                  // calls recorded
+    CallRec tr_ring[kCallRing];
     std::vector<DeviceCtx *> devs;
     std::vector<Shard *> shards;
     std::vector<int32_t> dfs_order;    // global DFS position -> global cell
@@ -2928,6 +2944,8 @@ int shard_wait(Shard *s)
             if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        if (seen && s->used_path && s->h_clk)   // the launch's counters, complete before its sequence number
+            for (int k = 0; k < 4; ++k) s->clk_snap[k] = s->h_clk[k];
     }
     s->seq_pending = false;
     if (!seen || s->profile) {
@@ -3286,7 +3304,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
-        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 2;   // + the launch clock's two counters
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 4;   // + the launch clock's four counters
         void *h = nullptr, *m = nullptr;
         if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
@@ -3302,7 +3320,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->m_seq = (int64_t *)((char *)m + 2 * f->n_lblocks * sizeof(double));
             f->h_clk = (volatile unsigned long long *)((char *)h + (2 * f->n_lblocks + 1) * sizeof(double));
             f->m_clk = (unsigned long long *)((char *)m + (2 * f->n_lblocks + 1) * sizeof(double));
-            f->h_clk[0] = f->h_clk[1] = 0;
+            f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = 0;
         }
     }
     if (rc != GGP_OK) {
@@ -3835,8 +3853,10 @@ int ggp_launch_clock(const ggp_forest *f, double *shader_mhz, double *window_us)
 {
     if (!f || f->shards.empty() || !f->shards[0]->h_clk) return GGP_EINVAL;
     const Shard *s = f->shards[0];
-    const unsigned long long c = s->h_clk[0], r = s->h_clk[1];
-    if (r == 0) return GGP_EINVAL;   // no path launch has run on this handle
+    // the last COMPLETED launch's counters (snapshotted when its sequence number was seen), never a
+    // launch still in flight
+    const unsigned long long c = s->clk_snap[0], r = s->clk_snap[1];
+    if (r == 0) return GGP_EINVAL;   // no path launch has completed on this handle
     if (shader_mhz) *shader_mhz = (double)c / (double)r * 100.0;   // s_memrealtime: 100 MHz
     if (window_us) *window_us = (double)r / 100.0;
     return GGP_OK;
@@ -4100,6 +4120,7 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
         g_last_err = "the handle's communicator was aborted after a failed collective evaluation; re-create the group";
         return GGP_EDEV;
     }
+    f->tr_t0 = std::chrono::steady_clock::now();
     ggp_params P;
     std::memcpy(P.p, params, sizeof P.p);
     for (Shard *s : f->shards) {   // every device enqueued before any is waited for
@@ -4135,6 +4156,8 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
             return GGP_EDEV;
         }
     }
+    f->tr_t1 = std::chrono::steady_clock::now();
+    f->tr_pending = true;
     return GGP_OK;
 }
 
@@ -4169,6 +4192,9 @@ static int comm_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *na
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     s->seq_pending = false;
+    f->tr_t2 = std::chrono::steady_clock::now();
+    if (seen && s->used_path && s->h_clk)   // the path launch completed before k_rank_sum (stream order)
+        for (int k = 0; k < 4; ++k) s->clk_snap[k] = s->h_clk[k];
     if (timed_out) {
         g_last_err = "multi-process evaluation did not complete within GGP_COMM_TIMEOUT_S (a peer rank never reached the collective); communicator aborted";
         comm_fail(c);
@@ -4211,16 +4237,17 @@ static int comm_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *na
     return GGP_ENAN;
 }
 
-int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
+static int loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
-    DeviceGuard device_guard_;   // the caller's current device is restored on return
-    if (!f) return GGP_EINVAL;
     if (f->comm) return comm_result(f, ll, nan_cell, nan_row);
     std::vector<double> blocks((size_t)f->n_blocks, 0.0);
     long long code = kNoNan;
     for (Shard *s : f->shards) {
         const int rc = shard_wait(s);
         if (rc != GGP_OK) return rc;
+    }
+    f->tr_t2 = std::chrono::steady_clock::now();
+    for (Shard *s : f->shards) {
         for (int64_t j = 0; j < s->n_lblocks; ++j) {
             blocks[(size_t)s->blk_global[j]] = s->h_sum[j];
             code = std::min<long long>(code, s->h_nan[j]);
@@ -4242,6 +4269,47 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
         return GGP_ENAN;
     }
     if (std::isnan(v)) return GGP_ENAN;   // NaN from +inf + -inf across cells (see include/ggp.h)
+    return GGP_OK;
+}
+
+int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
+{
+    DeviceGuard device_guard_;   // the caller's current device is restored on return
+    if (!f) return GGP_EINVAL;
+    f->tr_t2 = {};
+    const int rc = loglik_result(f, ll, nan_cell, nan_row);
+    if (f->tr_pending) {   // the call's host split (ggp_call_trace)
+        f->tr_pending = false;
+        const auto t3 = std::chrono::steady_clock::now();
+        const auto t2 = f->tr_t2 == std::chrono::steady_clock::time_point{} ? t3 : f->tr_t2;
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        CallRec &r = f->tr_ring[f->tr_n % kCallRing];
+        r.enqueue_us = us(f->tr_t0, f->tr_t1);
+        r.wait_us = us(f->tr_t1, t2);
+        r.result_us = us(t2, t3);
+        r.kernel_us = r.shader_mhz = 0.0;
+        const Shard *s0 = f->shards.empty() ? nullptr : f->shards[0];
+        if (s0 && s0->used_path && s0->clk_snap[3] > s0->clk_snap[2] && s0->clk_snap[1] > 0) {
+            r.kernel_us = (double)(s0->clk_snap[3] - s0->clk_snap[2]) / 100.0;   // s_memrealtime: 100 MHz
+            r.shader_mhz = (double)s0->clk_snap[0] / (double)s0->clk_snap[1] * 100.0;
+        }
+        r.call = (double)f->tr_n;
+        ++f->tr_n;
+    }
+    return rc;
+}
+
+int ggp_call_trace(const ggp_forest *f, int32_t cap, double *out, int32_t *n)
+{
+    if (!f || cap < 0 || (cap > 0 && !out)) return GGP_EINVAL;
+    const int64_t have = std::min<int64_t>(f->tr_n, kCallRing);
+    const int32_t k = (int32_t)std::min<int64_t>(have, cap);
+    for (int32_t i = 0; i < k; ++i) {   // the last k calls, oldest first
+        const CallRec &r = f->tr_ring[(f->tr_n - k + i) % kCallRing];
+        const double v[6] = {r.enqueue_us, r.wait_us, r.result_us, r.kernel_us, r.shader_mhz, r.call};
+        std::memcpy(out + 6 * (size_t)i, v, sizeof v);
+    }
+    if (n) *n = k;
     return GGP_OK;
 }
 

@@ -12,7 +12,9 @@ bandwidth); across nodes, or with GGP_NODE_EXCHANGE=0, it is torch's all_gather_
 for an nccl group); opt-in (engine_comm=True / GGP_ENGINE_COMM=1) it runs inside the engine
 (include/ggp.h ggp_comm_attach: partial, RCCL all-gather and rank-order sum enqueued on the
 engine's stream behind the evaluation).  All give the same bits.
-The first NaN is resolved the same way (lowest rank with a NaN, its first cell/row).
+The first NaN is resolved as the reference finds it: each rank sends the place of its own first NaN
+in the whole forest's order (root input position, DFS rank, row; NanOrder) with its partial, and
+every rank raises the smallest one's (cell, row).
 Scan samples and optimiser steps stay sequential (carried state), only the forest is
 parallel.
 
@@ -111,15 +113,86 @@ def global_init_stats(hf: HostForest, group=None, device=None) -> None:
     a["leaf_var_xg"] = np.array(var[2:4])
 
 
-def combine_partials(partials, nan_flags):
-    """rank-order sum; first NaN = lowest rank that saw one"""
-    for r, flag in enumerate(nan_flags):
-        if flag:
-            return math.nan, r
+def combine_partials(partials, nan_flags, keys=None):
+    """rank-order sum of the partials.  The first NaN: the rank whose first NaN comes first in the
+    reference's order -- roots in input order, DFS pre-order within a tree, row (likelihood.h:71-93,
+    125-159) -- by each rank's order key (NanOrder.key); without keys, the lowest
+    rank that saw one.  Returns (total, first NaN rank or -1)."""
+    bad = [r for r, flag in enumerate(nan_flags) if flag]
+    if bad:
+        if keys is None:
+            return math.nan, bad[0]
+        return math.nan, min(bad, key=lambda r: (tuple(float(k) for k in keys[r]), r))
     s = 0.0
     for v in partials:
         s = s + float(v)
     return s, -1
+
+
+class NanOrder:
+    """Where a rank's first NaN stands in the whole forest's reference order.
+
+    The reference stops at the first row whose running total is NaN, walking the roots in input
+    order, each tree in DFS pre-order (cell, daughter1's subtree, daughter2's subtree), each cell's
+    rows in order (likelihood_recr, likelihood.h:110-122; sc_likelihood :71-93).  A rank holds
+    whole trees of that forest, so its first NaN's place is the key (global position of its tree's
+    root, DFS rank of the cell within the tree, row); the smallest key over the ranks is the
+    reference's first NaN.  The global position of a root is its input-order cell index in the
+    whole forest (HostForest.cells, kept by subset_trees); a shard without that mapping (each rank
+    generated or read only its own trees, contiguous blocks in rank order) orders by rank first.
+    key() returns four floats (exact integers below 2^53): the three key parts and the cell's index
+    in the whole forest (its local index without the mapping), the cell the error reports."""
+
+    def __init__(self, hf, rank: int = 0):
+        self.rank = rank
+        self.hf = hf
+        self._root_pos = self._dfs = None
+
+    def _build(self):
+        a = self.hf.a
+        d1, d2 = np.asarray(a["daughter1"]), np.asarray(a["daughter2"])
+        n = len(d1)
+        root_of = np.full(n, -1, np.int64)
+        dfs = np.zeros(n, np.int64)
+        for r in self.hf.roots:
+            k, stack = 0, [int(r)]
+            while stack:
+                c = stack.pop()
+                root_of[c], dfs[c] = r, k
+                k += 1
+                if d2[c] >= 0:
+                    stack.append(int(d2[c]))
+                if d1[c] >= 0:
+                    stack.append(int(d1[c]))
+        cells = self.hf.cells
+        if cells is not None:
+            pos = np.asarray(cells, np.int64)[root_of]
+        else:
+            pos = self.rank * (1 << 40) + root_of
+        self._root_pos, self._dfs = pos, dfs
+
+    def key(self, cell: int, row: int):
+        if cell is None or cell < 0:          # no location (a peer's report, a stall): last in order
+            return (math.inf, math.inf, math.inf, -1.0)
+        if self.hf is None:
+            return (float(self.rank * (1 << 40) + cell), 0.0, float(row), float(cell))
+        if self._root_pos is None:
+            self._build()
+        gcell = cell if self.hf.cells is None else int(self.hf.cells[cell])
+        return (float(self._root_pos[cell]), float(self._dfs[cell]), float(row), float(gcell))
+
+    def error(self, owner: int, key, local_err):
+        """the LikelihoodIsNan every rank raises: the whole forest's first NaN (cell, row), owned by
+        rank `owner` (its cell id where this rank is the owner and knows it)"""
+        mine = owner == self.rank and local_err is not None
+        cid = getattr(local_err, "cell_id", None) if mine else None
+        if mine and self.hf is not None and self.hf.ids and local_err.local_cell >= 0:
+            cid = self.hf.ids[local_err.local_cell]
+        e = LikelihoodIsNan(int(key[3]), int(key[2]), cid)
+        e.rank = owner
+        e.local_cell = getattr(local_err, "local_cell", -1) if local_err is not None else -1
+        e.local_row = getattr(local_err, "local_row", -1) if local_err is not None else -1
+        return e
 
 
 class NodeExchange:
@@ -205,23 +278,35 @@ class NodeExchange:
             os.close(fd)
 
     def exchange(self, vals) -> np.ndarray:
-        """every rank's `width` values, [world, width], in rank order"""
+        """every rank's `width` values, [world, width], in rank order.  A waiting rank polls flat
+        out for ~1 ms (an evaluation's skew between ranks), then yields its core between polls
+        (sched_yield, then 50 us sleeps after ~0.1 s), so a rank waiting on a slower one's host work
+        neither burns a core nor holds the GIL.  After a timeout the exchange is unusable: the
+        ranks' sequence numbers are out of step, so every later call raises at once."""
+        if self.a is None:
+            raise RuntimeError("NodeExchange: unusable (closed, or a peer timed out earlier)")
         s = self.seq + 1
         lo = 1 + (s & 1) * self.width
         hi = lo + self.width
         mine = self.a[self.rank]
         mine[lo:hi] = vals
         mine[0] = s                     # published after the values
-        a, deadline = self.a, None
+        a, deadline, t_wait = self.a, None, None
         for r in range(self.world):
             n = 0
             while a[r, 0] < s:
                 n += 1
                 if (n & 0xFFF) == 0:
                     now = time.monotonic()
-                    deadline = deadline or now + self.timeout
+                    if deadline is None:
+                        deadline, t_wait = now + self.timeout, now
                     if now > deadline:
+                        self.a = None
                         raise TimeoutError(f"NodeExchange: rank {r} did not publish call {s} in {self.timeout} s")
+                    if now - t_wait > 0.1:
+                        time.sleep(50e-6)
+                    elif now - t_wait > 1e-3:
+                        time.sleep(0)
         out = a[:, lo:hi].copy()        # read after the sequence numbers
         self.seq = s
         return out
@@ -240,10 +325,15 @@ class ShardedObjective:
     """total_likelihood over a forest sharded across the ranks of a process group.
 
     device_forest: this rank's Forest (or any object with .total_likelihood(params)).
+    host_forest: this rank's HostForest, where device_forest does not carry it as .host (the first
+    NaN's place in the whole forest, NanOrder).
     """
 
+    # per rank and call: the partial, the NaN flag, and the first NaN's order key (NanOrder)
+    WIDTH = 6
+
     def __init__(self, device_forest, group=None, device=None, always_gather: bool = False,
-                 engine_comm: bool | None = None, node_exchange: bool | None = None):
+                 engine_comm: bool | None = None, node_exchange: bool | None = None, host_forest=None):
         import torch
         import torch.distributed as dist
         self.f = device_forest
@@ -252,6 +342,9 @@ class ShardedObjective:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.always_gather = always_gather          # tests: the collective path at world size 1
+        # this rank's trees (the first NaN's place in the whole forest): the Forest's own by default
+        self.order = NanOrder(host_forest if host_forest is not None else getattr(device_forest, "host", None),
+                              dist.get_rank(group) if dist.is_initialized() else 0)
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         # RCCL inside the engine (include/ggp.h ggp_comm_attach): the all-gather is enqueued on the
         # engine's stream behind the evaluation, no host round trip in between.  Opt-in
@@ -272,17 +365,17 @@ class ShardedObjective:
         if node_exchange is None:
             node_exchange = os.environ.get("GGP_NODE_EXCHANGE", "1") != "0"
         if not self.engine and (self.world > 1 or always_gather) and node_exchange:
-            x = NodeExchange(dist, group, width=2)
+            x = NodeExchange(dist, group, width=self.WIDTH)
             self.xchg = x if x.ok else None
-        self._send = torch.zeros(2, dtype=torch.float64, device=self.dev)
-        self._recv = torch.zeros(2 * self.world, dtype=torch.float64, device=self.dev)
+        self._send = torch.zeros(self.WIDTH, dtype=torch.float64, device=self.dev)
+        self._recv = torch.zeros(self.WIDTH * self.world, dtype=torch.float64, device=self.dev)
         # per call, RCCL moves 16 B per rank: stage them through pinned host tensors (one async
         # copy each way, numpy views for the element writes) instead of two element-fill
         # launches and a blocking .cpu()
         self._cuda = self.dev.type == "cuda"
         pin = self._cuda
-        self._h_send = torch.zeros(2, dtype=torch.float64, pin_memory=pin)
-        self._h_recv = torch.zeros(2 * self.world, dtype=torch.float64, pin_memory=pin)
+        self._h_send = torch.zeros(self.WIDTH, dtype=torch.float64, pin_memory=pin)
+        self._h_recv = torch.zeros(self.WIDTH * self.world, dtype=torch.float64, pin_memory=pin)
         self._h_send_np = self._h_send.numpy()
         self._h_recv_np = self._h_recv.numpy()
 
@@ -320,36 +413,78 @@ class ShardedObjective:
         except LikelihoodIsNan as e:
             return math.nan, True, e
 
+    def _allgather(self, vec) -> np.ndarray:
+        """every rank's float64 vector (the same length on every rank), [world, len], through torch's
+        collective (the NaN resolution and the chained partials: once per chain or per failure)"""
+        torch = self.torch
+        v = np.ascontiguousarray(vec, np.float64)
+        send = torch.from_numpy(v.copy()).to(self.dev)
+        recv = torch.zeros(len(v) * self.world, dtype=torch.float64, device=self.dev)
+        self.dist.all_gather_into_tensor(recv, send, group=self.group)
+        return recv.cpu().numpy().reshape(self.world, len(v))
+
+    def _key(self, err):
+        if err is None:
+            return (math.inf, math.inf, math.inf, -1.0)
+        return self.order.key(getattr(err, "local_cell", err.cell), getattr(err, "local_row", err.row))
+
+    def _engine_nan(self, err):
+        """the engine's collective reported a NaN on every rank: one exchange of each rank's own
+        first NaN (its order key) names the whole forest's first one, the same on every rank"""
+        own = err if getattr(err, "local_cell", -1) is not None and getattr(err, "local_cell", -1) >= 0 else None
+        got = self._allgather((1.0 if own is not None else 0.0,) + self._key(own))
+        _, owner = combine_partials(np.zeros(self.world), got[:, 0] != 0, got[:, 1:4])
+        if owner < 0:   # no rank located it (cannot happen with a NaN on some rank): the engine's report
+            return err
+        e = self.order.error(owner, got[owner, 1:5], own)
+        for k in ("point", "ll"):
+            if hasattr(err, k):
+                setattr(e, k, getattr(err, k))
+        return e
+
     def total_likelihood_chain(self, points):
         """a known sequence of objective calls, each from the state the previous left (the -s scan,
         the Hessian points; ggp_total_loglik_chain): every rank chains its own shard -- the carried
         state is per tree, so the points need no exchange between them -- and ONE all_gather of the
         per-point partials follows; the totals are the rank-order sums, as total_likelihood's.
-        Returns the totals of the points (a NaN point: NaN and every later point NaN too, as the
-        chain stops there)"""
+        A NaN raises, on every rank, what the one-process chain raises: LikelihoodIsNan at the
+        first point any rank failed (.point, .ll = the totals before it), located at the whole
+        forest's first NaN of that point (NanOrder).  With the engine's collective every chained
+        call already returns the total over the ranks (ggp_comm_attach), so its results are the
+        totals as they are."""
         pts = np.ascontiguousarray(np.atleast_2d(points), np.float64)
         n = pts.shape[0]
+        if self.engine:
+            try:
+                return np.asarray(self.f.total_likelihood_chain(pts), np.float64)
+            except LikelihoodIsNan as e:
+                raise self._engine_nan(e) from None
+        err = None
         try:
             local = np.asarray(self.f.total_likelihood_chain(pts), np.float64)
         except LikelihoodIsNan as e:
             if self.world == 1 and not self.always_gather:
                 raise
+            err = e
             local = np.asarray(getattr(e, "ll", []), np.float64)
+        fail = len(local) if err is not None else n   # this rank's first failing point (n: none)
         if len(local) < n:
             local = np.concatenate([local, np.full(n - len(local), math.nan)])
         if self.world == 1 and not self.always_gather:
             return local
-        torch = self.torch
-        send = torch.from_numpy(local.copy()).to(self.dev)
-        recv = torch.zeros(n * self.world, dtype=torch.float64, device=self.dev)
-        self.dist.all_gather_into_tensor(recv, send, group=self.group)
-        got = recv.cpu().numpy().reshape(self.world, n)
+        got = self._allgather(np.concatenate([local, [float(fail)], self._key(err)]))
         out = np.empty(n)
         for k in range(n):
             s = 0.0
             for r in range(self.world):
                 s = s + float(got[r, k])
             out[k] = s
+        p = int(got[:, n].min())
+        if p < n:
+            _, owner = combine_partials(np.zeros(self.world), got[:, n] == p, got[:, n + 1:n + 4])
+            e = self.order.error(owner, got[owner, n + 1:n + 5], err if err is not None and fail == p else None)
+            e.point, e.ll = p, out[:p].copy()
+            raise e
         return out
 
     @property
@@ -357,8 +492,8 @@ class ShardedObjective:
         if self.engine:
             return "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
         if self.xchg is not None:
-            return "host shared memory (NodeExchange): 16 B per rank, rank-order sum"
-        return "torch all_gather_into_tensor of 16 B per rank, rank-order sum"
+            return "host shared memory (NodeExchange): 48 B per rank, rank-order sum"
+        return "torch all_gather_into_tensor of 48 B per rank, rank-order sum"
 
     def close(self) -> None:
         if self.xchg is not None:
@@ -366,34 +501,32 @@ class ShardedObjective:
             self.xchg = None
 
     def total_likelihood(self, params) -> float:
-        if self.engine:   # the engine returns the rank-order sum (or raises, on every rank)
-            return self.f.total_likelihood(params)
+        if self.engine:   # the engine returns the rank-order sum (or a NaN on every rank)
+            try:
+                return self.f.total_likelihood(params)
+            except LikelihoodIsNan as e:
+                raise self._engine_nan(e) from None
         v, isnan, err = self.local(params)
         if self.world == 1 and not self.always_gather:
             if isnan:
                 raise err
             return v
+        mine = (v, 1.0 if isnan else 0.0) + self._key(err)
         if self.xchg is not None:
-            got = self.xchg.exchange((v, 1.0 if isnan else 0.0))
-            total, nan_rank = combine_partials(got[:, 0], got[:, 1] != 0)
-            if nan_rank >= 0:
-                raise err if (err is not None and nan_rank == self.dist.get_rank(self.group)) else \
-                    LikelihoodIsNan(-1, -1, f"rank {nan_rank}")
-            return total
-        self._h_send_np[0] = v
-        self._h_send_np[1] = 1.0 if isnan else 0.0
-        if self._cuda:
-            self._send.copy_(self._h_send, non_blocking=True)
-            self.dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
-            self._h_recv.copy_(self._recv, non_blocking=True)
-            self.torch.cuda.current_stream(self.dev).synchronize()
+            got = self.xchg.exchange(mine)
         else:
-            self.dist.all_gather_into_tensor(self._h_recv, self._h_send, group=self.group)
-        got = self._h_recv_np.reshape(self.world, 2)
-        total, nan_rank = combine_partials(got[:, 0], got[:, 1] != 0)
+            self._h_send_np[:] = mine
+            if self._cuda:
+                self._send.copy_(self._h_send, non_blocking=True)
+                self.dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+                self._h_recv.copy_(self._recv, non_blocking=True)
+                self.torch.cuda.current_stream(self.dev).synchronize()
+            else:
+                self.dist.all_gather_into_tensor(self._h_recv, self._h_send, group=self.group)
+            got = self._h_recv_np.reshape(self.world, self.WIDTH)
+        total, nan_rank = combine_partials(got[:, 0], got[:, 1] != 0, got[:, 2:5])
         if nan_rank >= 0:
-            raise err if (err is not None and nan_rank == self.dist.get_rank(self.group)) else \
-                LikelihoodIsNan(-1, -1, f"rank {nan_rank}")
+            raise self.order.error(nan_rank, got[nan_rank, 2:6], err)
         return total
 
 

@@ -40,6 +40,9 @@ class LikelihoodIsNan(GGPError):
 
     def __init__(self, cell: int, row: int, cell_id: str | None = None):
         self.cell, self.row, self.cell_id = cell, row, cell_id
+        # this process's own first NaN (its handle's cell index and row; -1 if its own evaluation
+        # was clean): what distributed.ShardedObjective exchanges to find the reference's first NaN
+        self.local_cell, self.local_row = cell, row
         super().__init__(f"Likelihood is Nan (cell {cell_id or cell}, row {row})")
 
 
@@ -200,11 +203,12 @@ class HostForest:
     """A flattened forest: the reference's std::vector<MOMAdata> after genealogy + init_cells,
     as structure-of-arrays (cells in input order, rows cell-major)."""
 
-    def __init__(self, arrays: dict, ids=None, parent_ids=None, rows=None):
+    def __init__(self, arrays: dict, ids=None, parent_ids=None, rows=None, cells=None):
         self.a = arrays
         self.ids = ids
         self.parent_ids = parent_ids
         self.rows = rows          # subset_trees: each row's index in the full forest
+        self.cells = cells        # subset_trees: each cell's index in the full forest (input order)
 
     # -- constructors --
     @classmethod
@@ -268,6 +272,8 @@ class HostForest:
             out["_parent_ids"] = np.array(self.parent_ids, dtype=np.str_)
         if self.rows is not None:
             out["_rows"] = np.asarray(self.rows, np.int64)
+        if self.cells is not None:
+            out["_cells"] = np.asarray(self.cells, np.int64)
         np.savez(path, **out)
 
     @classmethod
@@ -280,7 +286,8 @@ class HostForest:
             ids = [str(x) for x in z["_ids"]] if "_ids" in z.files else None
             pids = [str(x) for x in z["_parent_ids"]] if "_parent_ids" in z.files else None
             rows = z["_rows"] if "_rows" in z.files else None
-        return cls(a, ids, pids, rows)
+            cells = z["_cells"] if "_cells" in z.files else None
+        return cls(a, ids, pids, rows, cells)
 
     # -- properties --
     @property
@@ -328,7 +335,9 @@ class HostForest:
             a[k] = self.a[k][rows]
         ids = [self.ids[i] for i in idx] if self.ids else None
         pids = [self.parent_ids[i] for i in idx] if self.parent_ids else None
-        return HostForest(a, ids, pids, rows=np.asarray(rows, np.int64))
+        grows = np.asarray(rows, np.int64) if self.rows is None else np.asarray(self.rows, np.int64)[rows]
+        gcells = idx.astype(np.int64) if self.cells is None else np.asarray(self.cells, np.int64)[idx]
+        return HostForest(a, ids, pids, rows=grows, cells=gcells)
 
     def desc(self, devices=(0,), kernel: str = "auto", max_shard_rows: int = 0) -> N.ForestDesc:
         """ggp_forest_desc; devices: HIP ordinals to shard over (repeats = logical shards on one
@@ -437,7 +446,9 @@ class Forest:
             if self._lib.ggp_comm_local_nan(self._h):
                 self._poisoned = True
             if r >= 0 and r != self._comm_rank:
-                return LikelihoodIsNan(-1, -1, f"rank {r}")
+                e = LikelihoodIsNan(-1, -1, f"rank {r}")
+                e.local_cell, e.local_row = nc, nr
+                return e
         self._poisoned = True
         cid = self.host.ids[nc] if (self.host.ids and nc >= 0) else None
         return LikelihoodIsNan(nc, nr, cid)
@@ -484,6 +495,14 @@ class Forest:
         if self._lib.ggp_launch_clock(self._h, ctypes.byref(mhz), ctypes.byref(us)) != N.GGP_OK:
             return None
         return mhz.value, us.value
+
+    def call_trace(self, last: int = 512) -> np.ndarray:
+        """the host split of the last `last` objective calls (ggp_call_trace), oldest first: [k, 6] =
+        (enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call index)"""
+        out = np.zeros((max(1, last), 6))
+        n = ctypes.c_int32()
+        self._check(self._lib.ggp_call_trace(self._h, int(last), out.ctypes.data_as(N.c_double_p), ctypes.byref(n)))
+        return out[: n.value]
 
     def comm_size(self) -> int:
         """ranks of the attached RCCL communicator as RCCL counts them (ncclCommCount); 0 if the handle

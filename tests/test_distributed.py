@@ -304,3 +304,88 @@ def test_node_exchange_four_ranks():
         assert r["1"][1]
     assert res[0][3]["1"][0] == res[-1][3]["1"][0]
     assert set(glob.glob("/dev/shm/ggp_x_*")) == before
+
+
+def _nan_forest():
+    """12 trees x 40 rows (tree k: cells 3k, 3k+1, 3k+2); LPT deals the even trees to rank 0 and the
+    odd ones to rank 1.  NaN data in tree 4's root (rank 0) and in tree 1's second daughter (rank 1):
+    the reference's first NaN is tree 1's (roots in input order), on the HIGHER rank"""
+    import gfp_gaussian_process_amd as g
+    full = g.HostForest.synthetic(12, 40, with_ids=True)
+    ro = full.a["row_offset"]
+    full.a["fp"] = np.array(full.a["fp"])
+    full.a["fp"][ro[12] + 5] = np.nan     # tree 4, root, row 5
+    full.a["fp"][ro[5] + 3] = np.nan      # tree 1, daughter2, row 3
+    full.a["fp"][ro[4] + 7] = np.nan      # tree 1, daughter1, row 7: before daughter2 in DFS order
+    return full
+
+
+def _worker_nan(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedObjective, shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        mine = shard(_nan_forest(), rank, world)
+        out = {}
+        for mode in ("1", "0"):
+            os.environ["GGP_NODE_EXCHANGE"] = mode
+            obj = ShardedObjective(_OracleChainShard(mine), host_forest=mine)
+            try:
+                obj.total_likelihood(P0)
+                out[mode] = None
+            except g.LikelihoodIsNan as e:
+                out[mode] = (e.cell, e.row, e.rank)
+            obj.close()
+        # the chain: the first point already fails (the data are NaN)
+        obj = ShardedObjective(_OracleChainShard(mine), host_forest=mine)
+        pts = np.repeat(np.array(P0)[None, :], 3, axis=0)
+        try:
+            obj.total_likelihood_chain(pts)
+            out["chain"] = None
+        except g.LikelihoodIsNan as e:
+            out["chain"] = (e.cell, e.row, e.rank, e.point, len(e.ll))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_first_nan_across_ranks_is_the_references():
+    """the reference's first NaN (roots in input order, DFS pre-order, row; likelihood.h:71-93,
+    110-122) when both ranks hit NaN and the HIGHER rank holds the earlier root: every rank raises
+    the whole-forest oracle's (cell, row), through the shared-memory exchange, torch's all_gather
+    and the chained path"""
+    from oracle import oracle as O
+    world = 2
+    full = _nan_forest()
+    v, c, r = O.OracleForest(full.a).total_likelihood(P0)
+    assert math.isnan(v) and (c, r) == (4, 7)          # tree 1's daughter1 (rank 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_nan, args=(rk, world, port, q)) for rk in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        assert out["1"] == (c, r, 1), (rank, out)
+        assert out["0"] == (c, r, 1), (rank, out)
+        assert out["chain"] == (c, r, 1, 0, 0), (rank, out)
+
+
+def test_nan_order_keys():
+    """NanOrder: DFS pre-order ranks within a tree and the root's input position in the whole forest"""
+    from gfp_gaussian_process_amd.distributed import NanOrder, shard
+    full = _nan_forest()
+    sub = shard(full, 1, 2)                  # trees 1, 3, 5, ...: cells 3, 4, 5, 9, 10, 11, ...
+    o = NanOrder(sub, rank=1)
+    assert o.key(0, 2) == (3.0, 0.0, 2.0, 3.0)
+    assert o.key(1, 7) == (3.0, 1.0, 7.0, 4.0)
+    assert o.key(2, 3) == (3.0, 2.0, 3.0, 5.0)
+    assert o.key(3, 0) == (9.0, 0.0, 0.0, 9.0)
+    assert o.key(-1, -1)[0] == math.inf

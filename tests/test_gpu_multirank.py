@@ -158,3 +158,123 @@ def test_sharded_objective_hip_engine_two_ranks():
             assert abs(v - w) <= 1e-12 * abs(w)    # another partition of the same sum
             assert abs(v - o) <= 1e-9 * abs(o)     # the parity bar against the oracle
     assert res[0][1] == res[1][1]                  # every rank holds the same total
+
+
+def _worker_nan(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import gfp_gaussian_process_amd as g
+    from gfp_gaussian_process_amd.distributed import ShardedObjective, shard
+    from test_distributed import _nan_forest
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        mine = shard(_nan_forest(), rank, world)
+        out = {}
+        for mode in ("1", "0"):
+            os.environ["GGP_NODE_EXCHANGE"] = mode
+            obj = ShardedObjective(g.Forest(mine, device=0))
+            try:
+                obj.total_likelihood(P0)
+                out[mode] = None
+            except g.LikelihoodIsNan as e:
+                out[mode] = (e.cell, e.row, e.rank)
+            obj.close()
+        obj = ShardedObjective(g.Forest(mine, device=0))
+        pts = np.repeat(np.array(P0)[None, :], 3, axis=0)
+        try:
+            obj.total_likelihood_chain(pts)
+            out["chain"] = None
+        except g.LikelihoodIsNan as e:
+            out["chain"] = (e.cell, e.row, e.rank, e.point)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_first_nan_across_ranks_hip_engine():
+    """the whole forest's first NaN in the reference's order (likelihood.h:71-93, 110-122) from two
+    ranks' HIP evaluations when the HIGHER rank holds the earlier root (tests/test_distributed.py's
+    forest): every rank raises the oracle's (cell, row) through the shared-memory exchange, torch's
+    all_gather and the chained path"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+    from test_distributed import _nan_forest
+    world = 2
+    v, c, r = O.OracleForest(_nan_forest().a).total_likelihood(P0)
+    assert math.isnan(v)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_nan, args=(rk, world, port, q)) for rk in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        assert out["1"] == (c, r, 1) and out["0"] == (c, r, 1), (rank, out)
+        assert out["chain"] == (c, r, 1, 0), (rank, out)
+
+
+_NCCL_CHILD = r'''
+import os, sys, json, math
+sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np, torch, torch.distributed as dist
+import gfp_gaussian_process_amd as g
+from gfp_gaussian_process_amd.distributed import ShardedObjective, shard
+from test_distributed import _nan_forest
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(rank)
+dist.init_process_group("nccl", device_id=torch.device("cuda", rank))
+P = PARAMS
+full = g.HostForest.synthetic(301, 120)
+mine = shard(full, rank, world)
+res = {}
+for name, ec in (("engine", True), ("node", False)):
+    o = ShardedObjective(g.Forest(mine, device=rank), engine_comm=ec)
+    res[name] = {"engine": o.engine, "comm": o.f.comm_size() if ec else 0,
+                 "vals": [o.total_likelihood(P) for _ in range(3)]}
+    pts = np.repeat(np.array(P)[None, :], 3, axis=0); pts[:, 1] = [0.02, 0.03, 0.04]
+    res[name]["chain"] = [float(x) for x in o.total_likelihood_chain(pts)]
+    bad = shard(_nan_forest(), rank, world)
+    ob = ShardedObjective(g.Forest(bad, device=rank), engine_comm=ec)
+    try:
+        ob.total_likelihood(P); res[name]["nan"] = None
+    except g.LikelihoodIsNan as e:
+        res[name]["nan"] = [e.cell, e.row, e.rank]
+dist.destroy_process_group()
+print(json.dumps({"rank": rank, "res": res}), flush=True)
+'''
+
+
+def test_engine_rccl_two_devices():
+    """the engine's own RCCL collective (ggp_comm_attach) across two ranks on two distinct GPUs, one
+    process each (nccl): totals and chained totals bitwise the host exchange's, the communicator
+    holding both ranks, and the reference's first NaN on every rank.  Needs two visible devices
+    (skipped on a one-GPU box; the driver's multi-GPU node runs it unchanged)"""
+    import subprocess
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible devices")
+    from oracle import oracle as O
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_distributed import _nan_forest
+    code = f"ROOT={ROOT!r}\nPARAMS={P0!r}\n" + _NCCL_CHILD
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, (so[-2000:], se[-3000:])
+    res = [json.loads(so.strip().splitlines()[-1])["res"] for so, _ in outs]
+    _, c, r = O.OracleForest(_nan_forest().a).total_likelihood(P0)
+    for rr in res:
+        assert rr["engine"]["engine"] and rr["engine"]["comm"] == 2
+        assert rr["engine"]["vals"] == rr["node"]["vals"] == res[0]["node"]["vals"]
+        assert rr["engine"]["chain"] == rr["node"]["chain"]
+        assert rr["engine"]["nan"] == [c, r, 1] and rr["node"]["nan"] == [c, r, 1]

@@ -777,6 +777,12 @@ for name, ec in (("engine", True), ("torch", False)):   # RCCL inside the engine
         a2, b2 = g.Forest(hf), g.Forest(hf)
         same = same and ShardedObjective(a2, always_gather=True, engine_comm=ec).total_likelihood(P) == b2.total_likelihood(P)
         if ec and len(keep) < 3: keep.append(a2)
+    # the chain (-s scan): with the engine's collective each chained call already returns the total
+    pts = np.repeat(np.array(P)[None, :], 3, axis=0); pts[:, 1] = [0.02, 0.03, 0.04]
+    a3, b3 = g.Forest(hf), g.Forest(hf)
+    o3 = ShardedObjective(a3, always_gather=True, engine_comm=ec)
+    if ec: keep.append(a3)
+    same = same and np.array_equal(o3.total_likelihood_chain(pts), b3.total_likelihood_chain(pts))
     bad = list(P); bad[2] = -1.0
     try:   # on its own forest: a NaN evaluation leaves NaN in the carried state, as in the reference
         ShardedObjective(g.Forest(hf), always_gather=True, engine_comm=ec).total_likelihood(bad); nan_ok = False

@@ -257,3 +257,48 @@ def test_descriptor_device_sets():
     d.n_devices, d.devices = 1, bad.ctypes.data_as(N.c_int32_p)
     h = ctypes.c_void_p()
     assert lib.ggp_forest_create(ctypes.byref(d), ctypes.byref(h)) != 0
+
+
+def test_distinct_devices_bitwise():
+    """the device list over DISTINCT ordinals [0..n-1] (and each twice) -- what `-g all` runs on a
+    multi-GPU node: the chain, carried state, NaN location, batch points, -p rows and joints bitwise
+    one device's.  Skipped on a one-GPU box (the repeated-ordinal lists above run the same code)."""
+    import torch
+    import gfp_gaussian_process_amd as g
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs two visible devices")
+    hf = _forest(300, 60)
+    lists = [list(range(n)), [k % n for k in range(2 * n)]]
+    one = g.Forest(hf)
+    many = [g.Forest(hf, devices=d) for d in lists]
+    assert sorted({dv for dv, _, _ in many[0].shards()}) == list(range(n))
+    for call in range(3):
+        want = one.total_likelihood(INIT)
+        for f in many:
+            assert f.total_likelihood(INIT) == want, call
+    for f in many:
+        assert np.array_equal(f.state(), one.state())
+    bad = list(INIT)
+    bad[2] = -1.0
+    got = []
+    for d in [[0]] + lists:
+        with pytest.raises(g.LikelihoodIsNan) as e:
+            g.Forest(hf, devices=d).total_likelihood(bad)
+        got.append((e.value.cell, e.value.row))
+    assert all(x == got[0] for x in got)
+    rng = np.random.default_rng(7)
+    pts = np.stack([np.asarray(INIT) * (1 + 0.02 * rng.standard_normal(11)) for _ in range(5)])
+    want, _ = g.Forest(hf, kernel="lane").total_likelihood_batch(pts)
+    for d in lists:
+        assert np.array_equal(g.Forest(hf, devices=d).total_likelihood_batch(pts)[0], want)
+    pw = g.Forest(hf).predict(INIT)
+    P8 = list(INIT)
+    P8[8] = 2.6e4
+    iw, vw = g.Forest(hf).joints(P8, 1e-10, 0, 500)
+    for d in lists:
+        f = g.Forest(hf, devices=d)
+        for w, x in zip(pw, f.predict(INIT)):
+            assert np.array_equal(w, x)
+        ig, vg = f.joints(P8, 1e-10, 0, 500)
+        assert np.array_equal(iw, ig) and np.array_equal(vw, vg)
