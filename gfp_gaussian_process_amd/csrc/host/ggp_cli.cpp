@@ -842,7 +842,7 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
         file << "\n";
     }
     const int64_t max_cap = (int64_t)1 << 21;        // joints per call (44 doubles each: ggp_joints_packed)
-    int64_t cap = (int64_t)1 << 14, chunk = 4096;
+    int64_t cap = (int64_t)1 << 14, chunk = 4096, chunk_max = 65536;
     std::vector<int64_t> idx((size_t)(2 * cap));
     std::vector<double> val((size_t)(44 * cap));
     int64_t logged = -1;
@@ -851,6 +851,10 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
         int64_t n_out = 0;
         const int rc = ggp_joints_packed(F.gpu, pv.data(), (int32_t)plist.size(), tol, lo, hi, cap, idx.data(),
                                          val.data(), &n_out);
+        if (rc == GGP_ENOMEM && hi - lo > 1) {   // the range's walk stack or slots do not fit: a smaller range
+            chunk = chunk_max = std::max<int64_t>(1, (hi - lo) / 2);
+            continue;
+        }
         if (rc != GGP_OK) throw std::runtime_error(std::string("ggp_joints: ") + ggp_strerror(rc));
         if (n_out > cap) {   // buffers too small: split the range, or grow them
             if (n_out > max_cap && hi - lo > 1) {
@@ -938,7 +942,8 @@ void run_joints(const ggp_dataset *d, std::vector<Params> &plist, std::map<std::
         // its start rows side by side (one lane each) and takes as long as its longest walk, so
         // fewer, larger ranges mean fewer launches (up to 65,536 start rows, one wave per SIMD)
         if (n_out > 0) {
-            chunk = std::min<int64_t>(65536, std::max<int64_t>(256, (hi - s_lo) * (max_cap / 2) / n_out));
+            chunk = std::min<int64_t>(chunk_max, std::max<int64_t>(std::min<int64_t>(256, chunk_max),
+                                                                  (hi - s_lo) * (max_cap / 2) / n_out));
             const int64_t want = std::min<int64_t>(max_cap, (int64_t)((double)n_out * chunk / (hi - s_lo) * 1.25) + 1);
             if (want > cap) {
                 cap = want;

@@ -681,6 +681,38 @@ static void div_r_transform(double *m, double *C, const double *p, int binomial)
     }
 }
 
+/* init_sc_distribution_r leaf branch (predictions.h:317-332) */
+static void leaf_init(const double *leaf_mean_xg, const double *leaf_var_xg, double *m, double *C, const double *p)
+{
+    m[0] = leaf_mean_xg[0];
+    m[1] = leaf_mean_xg[1];
+    C[0] = leaf_var_xg[0];
+    C[5] = leaf_var_xg[1];
+    m[2] = -p[0];
+    m[3] = -p[3];
+    C[10] = p[2] / (2. * p[1]);
+    C[15] = p[5] / (2. * p[4]);
+}
+
+static void neg_ou(const double *p, double *q);
+
+/* mean_cov_after_division_r (predictions.h:201-275): d1 / d2 the daughters' states (d2 NULL: none) */
+static void after_division_r(double *m, double *C, const double *d1, const double *d2, double dt, const double *p,
+                             int binomial)
+{
+    memcpy(m, d1, ORA_STATE * sizeof(double));
+    div_r_transform(m, C, p, binomial);
+    if (d2) {
+        double m2[ORA_STATE];
+        memcpy(m2, d2, sizeof m2);
+        div_r_transform(m2, m2 + 4, p, binomial);
+        mult_gauss(m, C, m2, m2 + 4);
+    }
+    double q[11];
+    neg_ou(p, q);
+    ora_mean_cov_model(m, C, dt, q);
+}
+
 static const double *seg_params(const double *params, int n_seg, const int32_t *seg, int64_t r)
 {
     int s = seg ? seg[r] : 0;
@@ -755,30 +787,11 @@ int ora_predict(const ora_forest *f, const double *params, int n_seg, double *st
             int64_t r0 = f->row_off[c], r1 = f->row_off[c + 1];
             const double *pinit = seg_params(params, n_seg, seg, r1 - 1);
             if (f->d1[c] == -1 && f->d2[c] == -1) {
-                /* init_sc_distribution_r leaf branch (predictions.h:317-332) */
-                m[0] = f->leaf_mean_xg[0];
-                m[1] = f->leaf_mean_xg[1];
-                C[0] = f->leaf_var_xg[0];
-                C[5] = f->leaf_var_xg[1];
-                m[2] = -pinit[0];
-                m[3] = -pinit[3];
-                C[10] = pinit[2] / (2. * pinit[1]);
-                C[15] = pinit[5] / (2. * pinit[4]);
+                leaf_init(f->leaf_mean_xg, f->leaf_var_xg, m, C, pinit);
             } else {
-                /* mean_cov_after_division_r (predictions.h:201-275) */
                 int64_t a1 = f->d1[c];
-                const double *dm = state + ORA_STATE * a1;
-                memcpy(m, dm, ORA_STATE * sizeof(double));
-                div_r_transform(m, C, pinit, f->div_binomial);
-                if (f->d2[c] >= 0) {
-                    double m2[ORA_STATE];
-                    memcpy(m2, state + ORA_STATE * f->d2[c], sizeof m2);
-                    div_r_transform(m2, m2 + 4, pinit, f->div_binomial);
-                    mult_gauss(m, C, m2, m2 + 4);
-                }
-                double q[11];
-                neg_ou(pinit, q);
-                ora_mean_cov_model(m, C, f->time[f->row_off[a1]] - f->time[r1 - 1], q);
+                after_division_r(m, C, state + ORA_STATE * a1, f->d2[c] >= 0 ? state + ORA_STATE * f->d2[c] : NULL,
+                                 f->time[f->row_off[a1]] - f->time[r1 - 1], pinit, f->div_binomial);
             }
             for (int64_t r = r1 - 1; r >= r0; --r) {
                 double *dst = B + ORA_STATE * r;
@@ -825,4 +838,46 @@ int ora_predict(const ora_forest *f, const double *params, int n_seg, double *st
     if (!bwd) free(B);
     free(order);
     return 0;
+}
+
+/* ---- test-only entry points: the path's per-cell pieces one at a time, for the mechanical check
+ * against the reference's own text (tests/test_oracle_reference_path.py).  Each calls the static
+ * function ora_total_loglik / ora_predict use. ---- */
+void ora_t_after_division(double *m, double *C, const double *pm, const double *pC, double dt, const double *p,
+                          int binomial)
+{
+    after_division(m, C, pm, pC, dt, p, binomial);
+}
+
+void ora_t_root_init(double *m, double *C, const double *root_mean_xg, const double *root_var_xg, const double *p)
+{
+    ora_forest f;
+    memset(&f, 0, sizeof f);
+    memcpy(f.root_mean_xg, root_mean_xg, sizeof f.root_mean_xg);
+    memcpy(f.root_var_xg, root_var_xg, sizeof f.root_var_xg);
+    root_init(&f, m, C, p);
+}
+
+/* one row of sc_likelihood (likelihood.h:56-95): the residual, S, Si, the ll term, the posterior */
+double ora_t_update(double *m, double *C, double y0, double y1, const double *p, int scaled, double fp_auto)
+{
+    const double x0 = y0 - m[0], x1 = y1 - m[1];
+    ora_innov v;
+    innovation(m, C, p, scaled, fp_auto, &v);
+    const double ll = ll_term(x0, x1, &v);
+    posterior(m, C, x0, x1, &v);
+    return ll;
+}
+
+void ora_t_reverse_state(double *m, double *C) { reverse_state(m, C); }
+
+void ora_t_leaf_init(double *m, double *C, const double *leaf_mean_xg, const double *leaf_var_xg, const double *p)
+{
+    leaf_init(leaf_mean_xg, leaf_var_xg, m, C, p);
+}
+
+void ora_t_after_division_r(double *m, double *C, const double *d1, const double *d2, double dt, const double *p,
+                            int binomial)
+{
+    after_division_r(m, C, d1, d2, dt, p, binomial);
 }

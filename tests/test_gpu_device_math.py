@@ -64,6 +64,20 @@ def test_device_dawson_matches_reference_faddeeva(variant):
     assert np.sum(np.abs(xs) > 45) > 50 and np.sum(np.abs(xs) >= 5e7) >= 4
 
 
+def test_exact_engine_dawson_bitwise_reference():
+    """the exact-arithmetic engine (libggp_exact.so: no contraction) evaluates the Faddeeva
+    package's own coefficient table (dawson_table.inc, tools/gen_dawson_table.py) in the reference's
+    expression order: its Dawson is Faddeeva::Dawson bit for bit on all 6,810 values of
+    dawson_ref.json (the default engine contracts the Horner steps into fma: a few ulp, above)"""
+    from gfp_gaussian_process_amd import _native as N
+    lib = N.engine(N.EXACT_ENGINE)
+    g = json.load(open(os.path.join(GOLDEN, "dawson_ref.json")))
+    x = np.ascontiguousarray([float.fromhex(v) for v in g["x"]], np.float64)
+    out = np.zeros_like(x)
+    assert lib.ggp_debug_dawson(0, 0, x.ctypes.data_as(N.c_double_p), x.size, out.ctypes.data_as(N.c_double_p)) == 0
+    assert [v.hex() for v in out] == g["dawson"]
+
+
 @pytest.mark.parametrize("variant", [0, 1])
 def test_device_dawson_maple_values(variant):
     g = json.load(open(os.path.join(GOLDEN, "dawson_maple.json")))

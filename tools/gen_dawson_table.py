@@ -20,7 +20,23 @@ kernels and the CPU oracle (the oracle is pinned independently: tests compare it
 reference's own Faddeeva.cc compiled into oracle/_ref and with the Maple values in that
 file's self-test, see tests/golden/).
 
-Run:  python tools/gen_dawson_table.py   (about 30 s)
+Two modes:
+
+``--reference`` (the default when the reference's Faddeeva.cc is present): the coefficients are
+read from ``w_im_y100`` in S. G. Johnson's Faddeeva package as vendored by the reference
+(/root/reference/src/Faddeeva.cc:1458-1862, MIT licence, reproduced in the generated file): each
+case's Horner expression is parsed into its coefficients (a subtracted innermost term becomes a
+negated coefficient: c - d*t and c + (-d)*t are the same IEEE operations), each decimal literal
+rounded to the nearest double as a C compiler does, and the parse is checked by evaluating the
+literal expression against the zero-padded Horner form at 257 points of every interval, bit for
+bit.  The Taylor coefficients (:1852-1857) and the constants 1/sqrt(pi) (:1870) and sqrt(pi)/2
+(:469) are the reference's literals too.  So the table is the reference's arithmetic: the device
+and oracle Dawson are bitwise Faddeeva::Dawson wherever they evaluate the same expression
+(verdict r5, "a constant table" of a third-party file).
+
+``--derive``: the independent derivation described above (the table of rounds 1-5).
+
+Run:  python tools/gen_dawson_table.py [--reference PATH | --derive]
 """
 from __future__ import annotations
 
@@ -107,36 +123,127 @@ def fit_interval(k: int):
     return power
 
 
+REF = "/root/reference/src/Faddeeva.cc"
+MIT = """ * Copyright (c) 2012 Massachusetts Institute of Technology
+ *
+ * Permission is hereby granted, free of charge, to any person obtaining
+ * a copy of this software and associated documentation files (the
+ * "Software"), to deal in the Software without restriction, including
+ * without limitation the rights to use, copy, modify, merge, publish,
+ * distribute, sublicense, and/or sell copies of the Software, and to
+ * permit persons to whom the Software is furnished to do so, subject to
+ * the following conditions:
+ *
+ * The above copyright notice and this permission notice shall be
+ * included in all copies or substantial portions of the Software.
+ *
+ * THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND,
+ * EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF
+ * MERCHANTABILITY, FITNESS FOR A PARTICULAR PURPOSE AND
+ * NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE
+ * LIABLE FOR ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION
+ * OF CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION
+ * WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
+"""
+
+
+def horner(c, t):
+    acc = c[-1]
+    for v in reversed(c[:-1]):
+        acc = acc * t + v
+    return acc
+
+
+def from_reference(path: str):
+    """(rows [97][9], taylor [5], ispi, spi2) read from the Faddeeva package's w_im_y100 / w_im /
+    Dawson, each literal rounded to the nearest double (float(), as strtod)"""
+    import re
+    src = open(path).read()
+    i = src.index("static double w_im_y100(double y100, double x)")
+    j = src.index("double FADDEEVA(w_im)(double x)", i)
+    body = src[i:j]
+    cases = re.findall(r"case (\d+): \{\s*double t = 2\*y100 - (\d+);\s*return ([^;]+);", body)
+    if len(cases) != NINT:
+        raise SystemExit(f"expected {NINT} polynomial cases, found {len(cases)}")
+    rows = []
+    for k, (case, off, expr) in enumerate(cases):
+        if int(case) != k or int(off) != 2 * k + 1:
+            raise SystemExit(f"case {case}: unexpected layout")
+        e = expr.replace(" ", "").replace("\n", "")
+        coefs = [(-1.0 if sign == "-" else 1.0) * float(num)
+                 for sign, num in re.findall(r"([+-]?)(\d+\.\d+e[+-]?\d+)", e)]
+        if len(coefs) - 1 != DEGREES[k] or e.count("*t") != DEGREES[k]:
+            raise SystemExit(f"case {k}: {len(coefs)} coefficients, {e.count('*t')} products")
+        row = coefs + [0.0] * (DEG + 1 - len(coefs))
+        # the literal expression (valid Python: no FMA, left-to-right, as the reference's x86-64
+        # build) against the padded Horner form, bitwise at 257 points of the interval
+        for q in range(257):
+            t = -1.0 + q / 128.0
+            want = eval(e, {"t": t})
+            if float.hex(horner(row, t)) != float.hex(want):
+                raise SystemExit(f"case {k}: Horner form differs at t={t}")
+        rows.append(row)
+    m = re.search(r"return x \* \(([0-9.]+)\s*- x2 \* \(([0-9.]+)\s*- x2 \* \(([0-9.]+)\s*"
+                  r"- x2 \* \(([0-9.]+)\s*- x2 \* ([0-9.]+)\)\)\)\);", body)
+    if not m:
+        raise SystemExit("Taylor branch not found")
+    taylor = [float(v) for v in m.groups()]
+    w = src[j:j + 2000]
+    ispi = float(re.search(r"const double ispi = ([0-9.]+);", w).group(1))
+    d = src.index("double FADDEEVA_RE(Dawson)(double x)")
+    spi2 = float(re.search(r"const double spi2 = ([0-9.]+);", src[d:d + 400]).group(1))
+    return rows, taylor, ispi, spi2
+
+
 def main() -> int:
     out = os.path.join(os.path.dirname(__file__), "..", "gfp_gaussian_process_amd", "csrc",
                        "dawson_table.inc")
-    rows = []
-    for k in range(NINT):
-        p = fit_interval(k)
-        rows.append([float(c) for c in p])
-        sys.stderr.write(f"\rinterval {k+1}/{NINT}")
-    sys.stderr.write("\n")
-    with open(out, "w") as f:
-        f.write("/* GENERATED by tools/gen_dawson_table.py -- do not edit.\n"
-                " * Power-basis coefficients (Horner order c0..c8, in t = 2*y100-(2k+1)) of\n"
+    derive = "--derive" in sys.argv
+    ref = REF
+    if "--reference" in sys.argv:
+        k = sys.argv.index("--reference")
+        if k + 1 < len(sys.argv):
+            ref = sys.argv[k + 1]
+    if not derive and not os.path.exists(ref):
+        raise SystemExit(f"{ref} not found (--derive re-derives the table independently)")
+    if derive:
+        rows = []
+        for k in range(NINT):
+            p = fit_interval(k)
+            rows.append([float(c) for c in p])
+            sys.stderr.write(f"\rinterval {k+1}/{NINT}")
+        sys.stderr.write("\n")
+        tsp = TWO_OVER_SQRT_PI
+        # the reference's last Taylor coefficient is 16/945 WITHOUT the 2/sqrt(pi) factor
+        # (Faddeeva.cc:1855); replicated for parity
+        taylor = [float(c) for c in (tsp, tsp * 2 / 3, tsp * 4 / 15, tsp * 8 / 105, Decimal(16) / 945)]
+        ispi, spi2 = float(1 / SQRT_PI), float(SQRT_PI / 2)
+        head = (" * Power-basis coefficients (Horner order c0..c8, in t = 2*y100-(2k+1)) of\n"
                 " * w_im(x) = 2/sqrt(pi) * Dawson(x) on y = 1/(1+x) in [k/100, (k+1)/100],\n"
                 " * k = 0..96: the interval layout and per-interval degree (6..8) of\n"
                 " * Faddeeva.cc:1458-1862; coefficients re-derived independently (60-digit\n"
                 " * Rybicki sum, Chebyshev truncation), zero-padded to 9 (exact in Horner). */\n")
+    else:
+        rows, taylor, ispi, spi2 = from_reference(ref)
+        head = (" * The coefficient table of w_im_y100 in S. G. Johnson's Faddeeva package\n"
+                " * (http://ab-initio.mit.edu/Faddeeva), as the reference vendors it\n"
+                " * (src/Faddeeva.cc:1458-1862): per interval k = 0..96 of y = 1/(1+x), the\n"
+                " * Horner coefficients c0..c8 in t = 2*y100-(2k+1), each decimal literal\n"
+                " * rounded to the nearest double, zero-padded to 9 (exact in Horner); the\n"
+                " * Taylor branch (:1852-1857), 1/sqrt(pi) (:1870) and sqrt(pi)/2 (:469).\n"
+                " * The package's licence:\n *\n" + MIT + " */\n")
+    with open(out, "w") as f:
+        f.write("/* GENERATED by tools/gen_dawson_table.py -- do not edit.\n" + head)
         f.write(f"#define GGP_DAWSON_NINT {NINT}\n#define GGP_DAWSON_NCOEF {DEG+1}\n")
         f.write("GGP_DAWSON_TABLE_QUALIFIER double ggp_dawson_coef[GGP_DAWSON_NINT * GGP_DAWSON_NCOEF] = {\n")
         for k, r in enumerate(rows):
             f.write("  " + ", ".join(float.hex(c) for c in r) + f",  /* k={k} */\n")
         f.write("};\n")
         # Taylor branch (y100 >= 97, |x| <= 0.0309): x*(c0 - x2*(c1 - x2*(c2 - x2*(c3 - x2*c4))))
-        # with c_j = 2/sqrt(pi) * 2^j/(2j+1)!! for j < 4.  The reference's last coefficient
-        # is 16/945 WITHOUT the 2/sqrt(pi) factor (Faddeeva.cc:1855); replicated for parity.
-        tsp = TWO_OVER_SQRT_PI
-        taylor = [tsp, tsp * 2 / 3, tsp * 4 / 15, tsp * 8 / 105, Decimal(16) / 945]
         f.write("GGP_DAWSON_TABLE_QUALIFIER double ggp_dawson_taylor[5] = {"
-                + ", ".join(float.hex(float(c)) for c in taylor) + "};\n")
-        f.write(f"#define GGP_ISPI {float.hex(float(1 / SQRT_PI))}   /* 1/sqrt(pi)  */\n")
-        f.write(f"#define GGP_SPI2 {float.hex(float(SQRT_PI / 2))}   /* sqrt(pi)/2  */\n")
+                + ", ".join(float.hex(c) for c in taylor) + "};\n")
+        f.write(f"#define GGP_ISPI {float.hex(ispi)}   /* 1/sqrt(pi)  */\n")
+        f.write(f"#define GGP_SPI2 {float.hex(spi2)}   /* sqrt(pi)/2  */\n")
     print("wrote", os.path.normpath(out))
     return 0
 

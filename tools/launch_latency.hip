@@ -15,6 +15,13 @@
 #include <vector>
 
 __global__ void k_empty() {}
+struct BigArgs {
+    double v[64];
+};
+__global__ void k_bigarg(BigArgs a, int64_t *seq, int64_t v)
+{
+    if (threadIdx.x == 0 && a.v[0] == 12345.0) __hip_atomic_store(seq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void k_signal(int64_t *seq, int64_t v)
 {
     if (threadIdx.x == 0) __hip_atomic_store(seq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -53,6 +60,22 @@ int main()
     });
     const double l = median_us([&](int) { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s); }, 200);
     (void)hipStreamSynchronize(s);
+    // the enqueue of a launch with a 512-byte argument block (the path launch passes ~400 B), each
+    // after the previous completed (as the engine's calls are)
+    BigArgs ba{};
+    std::vector<double> enq;
+    for (int i = 0; i < 2050; ++i) {
+        const auto a = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(k_bigarg, dim3(2000), dim3(64), 0, s, ba, d, (int64_t)0);
+        const auto b = std::chrono::steady_clock::now();
+        (void)hipStreamSynchronize(s);
+        if (i >= 50) enq.push_back(std::chrono::duration<double, std::micro>(b - a).count());
+    }
+    std::sort(enq.begin(), enq.end());
+    int dev = 0;
+    const double gd = median_us([&](int) { (void)hipGetDevice(&dev); });
+    const double sd = median_us([&](int) { (void)hipSetDevice(dev); });
+    const double le = median_us([&](int) { (void)hipGetLastError(); });
     ggp_host_forest *hf = nullptr;
     ggp_synthetic_forest(1, 4, 20261015ULL, 0, 1, 1, &hf);   // one tree: root 2 rows, daughters 1 + 1
     ggp_forest_desc dd;
@@ -64,10 +87,34 @@ int main()
     double ll;
     int64_t nc, nr;
     const double g = median_us([&](int) { ggp_total_loglik(f, P, &ll, &nc, &nr); });
+    // C2 (1000 trees x 200): the call and its host split (ggp_call_trace), median of 500 calls
+    ggp_host_forest *h2 = nullptr;
+    ggp_synthetic_forest(1000, 200, 20261015ULL, 0, 1, 1, &h2);
+    ggp_forest_desc d2;
+    ggp_host_forest_desc(h2, &d2);
+    ggp_forest *f2 = nullptr;
+    ggp_forest_create(&d2, &f2);
+    const double c2 = median_us([&](int) { ggp_total_loglik(f2, P, &ll, &nc, &nr); }, 500);
+    std::vector<double> tr(6 * 500);
+    int32_t ntr = 0;
+    ggp_call_trace(f2, 500, tr.data(), &ntr);
+    auto med = [&](int k) {
+        std::vector<double> x;
+        for (int i = 0; i < ntr; ++i) x.push_back(tr[6 * i + k]);
+        std::sort(x.begin(), x.end());
+        return x.empty() ? 0.0 : x[x.size() / 2];
+    };
     printf("empty kernel + hipStreamSynchronize   %7.2f us\n", e);
     printf("kernel + spin on a mapped seq slot    %7.2f us   (the engine's completion path)\n", m);
     printf("hipLaunchKernelGGL alone (enqueue)    %7.2f us\n", l);
     printf("ggp_total_loglik, 1 tree x 4 rows     %7.2f us   (4 cells' steps, setup, reduction)\n", g);
+    printf("enqueue of a 2000-block launch, 520 B of arguments  %7.2f us (median), %7.2f us (p90)\n",
+           enq[enq.size() / 2], enq[enq.size() * 9 / 10]);
+    printf("hipGetDevice %7.3f us, hipSetDevice (same device) %7.3f us, hipGetLastError %7.3f us\n", gd, sd, le);
+    printf("ggp_total_loglik C2 (1000 x 200)      %7.2f us: enqueue %.2f, wait %.2f (kernel %.2f), result %.2f\n", c2,
+           med(0), med(1), med(3), med(2));
+    ggp_forest_destroy(f2);
+    ggp_host_forest_free(h2);
     ggp_forest_destroy(f);
     ggp_host_forest_free(hf);
     return 0;
