@@ -284,14 +284,18 @@ def host_split(step_t, trace) -> dict:
     if trace is not None and len(trace) == len(wall):
         enq, wait, res, kern, mhz = (trace[:, k] for k in range(5))
         out.update({"enqueue_us": stats(enq), "wait_us": stats(wait), "result_us": stats(res)})
+        disp = trace[:, 6]
+        out["python_us"] = stats(wall - enq - wait - res)
         if np.all(kern > 0):
             out.update({"kernel_us": stats(kern), "shader_mhz": stats(mhz),
                         "host_us": stats(wall - kern),
-                        "dispatch_and_completion_us": stats(wait - kern),
-                        "python_us": stats(wall - enq - wait - res)})
-        out["note"] = ("per timed step: wall = python + enqueue + wait + result; wait = dispatch + kernel + the "
-                       "completion's trip to the host (kernel: the path launch's first block start to its publishing "
-                       "block's end on the device's 100 MHz counter, ggp_call_trace)")
+                        "dispatch_and_completion_us": stats(wait - kern)})
+            if np.all(disp >= 0):
+                out.update({"dispatch_us": stats(disp), "completion_us": stats(wait - disp - kern)})
+        out["note"] = ("per timed step: wall = python + enqueue + wait + result; wait = dispatch (enqueued to the "
+                       "launch's start flag seen by the waiting host) + kernel (its first block start to its publishing "
+                       "block's end on the device's 100 MHz counter) + completion (the sequence number's trip to the "
+                       "host); ggp_call_trace")
     return out
 
 
@@ -565,7 +569,6 @@ def main() -> int:
                 eng["error"] = repr(e)[-400:]
             eng["kind"] = "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
             c4s["engine_rccl"] = eng
-        del h4
 
     # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
     fg.enable_profile()
@@ -581,10 +584,13 @@ def main() -> int:
             acc[0] += ms
             acc[1] += rows
             acc[2] += 1
-    if c4s is not None:   # released only now: the profiled launches run at the headline's clock too
+    if c4s is not None:   # released only now: freeing a 2e7-row forest (host and device) idles the GPU
+        # long enough for its clock to fall, so neither the headline's steps nor its profiled launches
+        # may follow it (DESIGN.md §6 "The clock")
         if world > 1:
             o4.close()
         f4.close()
+        del h4
     dom = max(per, key=lambda k: per[k][0])
     d_ms, d_rows, d_n = per[dom]
     avg_ms = d_ms / d_n

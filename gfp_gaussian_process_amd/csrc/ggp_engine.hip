@@ -835,7 +835,17 @@ constexpr unsigned kChainQuietPerRow = 1100;    // s_memtime units (~0.5 us) of 
 // each path's block, its path count and tree bounds are loaded at the launch's start
 // (RedPre): the reduction's only round trips are the block count, the cells' results (all
 // lanes at once), the host slots and the done count.
+// A path launch's block b: what its setup reads before its first row loads, in one place (one
+// scalar load) instead of a chain of four dependent loads (path_seq -> path_cells -> row_off ->
+// rows; path_blk -> block tables -> tree_dfs)
+struct PathDesc {
+    int32_t i_lo, i_hi, c0, j;    // the path's cells [i_lo, i_hi) of path_cells, its first cell, its block
+    int32_t npaths, nb, t0, pad;  // the block's path count, tree count and first tree
+    int64_t r0, r1;               // the first cell's rows
+};
+
 struct ChainRed {
+    const PathDesc *pdesc;        // per path (nullptr: the tables below / the level launch's cells)
     const int32_t *path_blk;      // local block of each path
     const int32_t *blk_npaths;    // paths per local block
     const int64_t *tree_dfs;      // DFS start of each local tree, then the end
@@ -878,10 +888,19 @@ GGP_DEV RedPre red_load(const ChainRed &R, const int b, const int lane)
 {
     RedPre q{0, 0, 0, 0};
     if (R.n_lblocks <= 0) return q;
-    q.j = R.path_blk[b];
-    q.npaths = R.blk_npaths[q.j];
-    q.nb = R.blk_nt[q.j];
-    const int t0 = R.blk_t0[q.j];
+    int t0;
+    if (R.pdesc) {
+        const PathDesc &pd = R.pdesc[b];
+        q.j = pd.j;
+        q.npaths = pd.npaths;
+        q.nb = pd.nb;
+        t0 = pd.t0;
+    } else {
+        q.j = R.path_blk[b];
+        q.npaths = R.blk_npaths[q.j];
+        q.nb = R.blk_nt[q.j];
+        t0 = R.blk_t0[q.j];
+    }
     q.tb = lane <= q.nb ? R.tree_dfs[t0 + lane] : 0;
     return q;
 }
@@ -1027,6 +1046,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // the launch's shader clock (ggp_launch_clock): block 0 reads the shader-clock counter and the
     // constant 100 MHz counter at its start and after its path (two scalar reads each)
     const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+    // the call's start, seen by the host as it waits (ggp_call_trace: dispatch vs completion)
+    if (red.clk && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        __hip_atomic_store(red.clk + 4, (unsigned long long)call_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
     GGP_TL(0);
@@ -1036,16 +1058,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // block tables, the Dawson/exp table, this lane's row of the lane constants and the first
     // cell's first 64 rows; make_ou runs while they are in flight
     const RedPre rq0 = red_load(red, blockIdx.x, lane);
-    constexpr int kTabN = W::kTabRows * W::kTabRow, kTabR = (kTabN + 63) / 64;
-    double tab_v[kTabR];
+    constexpr int kTabN2 = W::kTabRows * W::kTabRow / 2, kTabR = (kTabN2 + 63) / 64;   // 16-byte pieces
+    double2 tab_v[kTabR];
+    const double2 *tab_img = reinterpret_cast<const double2 *>(W::kTabImg.v);
 #pragma unroll
-    for (int j = 0; j < kTabR; ++j) tab_v[j] = W::tab_entry(min(lane + 64 * j, kTabN - 1));
-    const int i_lo = seq ? seq[blockIdx.x] : (int)blockIdx.x;
-    const int i_hi = seq ? seq[blockIdx.x + 1] : i_lo + 1;
+    for (int j = 0; j < kTabR; ++j) tab_v[j] = tab_img[min(lane + 64 * j, kTabN2 - 1)];
+    const PathDesc *pd = red.pdesc ? red.pdesc + blockIdx.x : nullptr;
+    const int i_lo = pd ? pd->i_lo : seq ? seq[blockIdx.x] : (int)blockIdx.x;
+    const int i_hi = pd ? pd->i_hi : seq ? seq[blockIdx.x + 1] : i_lo + 1;
     double pre_l = 0.0, pre_f = 0.0, pre_t = 0.0, pre_t64 = 0.0;   // the first cell's chunk [r0, r0 + 64)
     {
-        const int c = cells[i_lo];
-        const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1], rr = r0 + lane;
+        const int c = pd ? pd->c0 : cells[i_lo];
+        const int64_t r0 = pd ? pd->r0 : F.row_off[c], r1 = pd ? pd->r1 : F.row_off[c + 1], rr = r0 + lane;
         if (rr < r1) {
             pre_l = F.logl[rr];
             pre_f = F.fp[rr];
@@ -1073,7 +1097,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const double kap = W::lane_kappa(lane, ou);
 #pragma unroll
         for (int j = 0; j < kTabR; ++j)
-            if (lane + 64 * j < kTabN) lds[W::L_TAB + lane + 64 * j] = tab_v[j];
+            if (lane + 64 * j < kTabN2) reinterpret_cast<double2 *>(lds + W::L_TAB)[lane + 64 * j] = tab_v[j];
         if (red.n_lblocks > 0) red_park(rq0, lds + W::L_RED, lane);
         lds[W::L_ROWL + lane] = pre_l;   // the first cell's chunk (its loop iteration loads no rows)
         lds[W::L_ROWF + lane] = pre_f;
@@ -2580,6 +2604,15 @@ double top_sum(std::vector<double> v)
     return v.empty() ? 0.0 : v[0];
 }
 
+// top_sum in place on a buffer already zero-padded to a power of two (n_pow2 entries): the same
+// tree, no allocation (the objective's result path, once per call)
+double top_sum_inplace(double *v, size_t n_pow2)
+{
+    for (size_t n = n_pow2; n > 1; n /= 2)
+        for (size_t i = 0; i < n / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+    return n_pow2 ? v[0] : 0.0;
+}
+
 }  // namespace
 
 // One device (HIP ordinal) used by the handle: its stream, and the -p workspace its shards
@@ -2660,7 +2693,10 @@ struct Shard {
     volatile int64_t *h_seq = nullptr;
     int64_t *m_seq = nullptr;
     volatile unsigned long long *h_clk = nullptr;   // path launches: block 0's clock counters
+    PathDesc *d_pdesc = nullptr;                    // path launches: per path (PathDesc)
     unsigned long long clk_snap[4] = {0, 0, 0, 0}; // h_clk as the last completed launch left it
+    std::chrono::steady_clock::time_point t_started;  // when the wait saw the path launch's start flag
+    bool started_seen = false;
     unsigned long long *m_clk = nullptr;
     // the largest |dt| of any propagation of the shard (in-cell steps and divisions): with the
     // parameters it bounds |k dt| for the wave schedule's product factors exp(-gl dt), exp(-gq dt),
@@ -2760,7 +2796,7 @@ static void comm_fail(Comm *c)
 
 // one objective call's host split (ggp_call_trace)
 struct CallRec {
-    double enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call;
+    double enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call, dispatch_us;
 };
 constexpr int kCallRing = 512;
 
@@ -2773,6 +2809,7 @@ struct ggp_forest {
     std::vector<DeviceCtx *> devs;
     std::vector<Shard *> shards;
     std::vector<int32_t> dfs_order;    // global DFS position -> global cell
+    std::vector<double> res_blocks;    // the result path's block sums, padded to a power of two
     std::vector<int64_t> row_off;      // global row_offset
     Comm *comm = nullptr;              // multi-process mode (ggp_comm_attach)
     int32_t tree_pts = 0;              // points of the last ggp_total_loglik_tree (ggp_keep_point_state)
@@ -2914,6 +2951,14 @@ int launch_levels(Shard *f, const ggp_params &P)
     return GGP_OK;
 }
 
+// a chained / tree launch's ChainRed: no in-launch reduction, only the per-path setup descriptors
+ChainRed chain_red_setup(const Shard *s)
+{
+    ChainRed R{};
+    R.pdesc = s->d_pdesc;
+    return R;
+}
+
 // one evaluation on a shard: the levels, then the block sums straight into mapped host memory
 int shard_launch(Shard *s, const ggp_params &P)
 {
@@ -2938,8 +2983,16 @@ int shard_wait(Shard *s)
 {
     if (s->n_cells == 0) return GGP_OK;
     bool seen = false;
+    s->started_seen = false;
     if (s->spin && s->seq_pending) {
+        // a path launch's block 0 raises its start flag (h_clk[4] = the call's number) as it
+        // begins: the wait notes when it sees it (ggp_call_trace), a few loads per poll
+        const bool flag = s->used_path && s->h_clk != nullptr;
         for (uint32_t it = 1;; ++it) {
+            if (flag && !s->started_seen && s->h_clk[4] == (unsigned long long)s->seq) {
+                s->t_started = std::chrono::steady_clock::now();
+                s->started_seen = true;
+            }
             if (*s->h_seq == s->seq) { seen = true; break; }
             if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
         }
@@ -3095,7 +3148,7 @@ void shard_destroy(Shard *f)
                     (void *)f->d_blk_t0, (void *)f->d_blk_nt, (void *)f->d_gdfs, (void *)f->d_done,
                     (void *)f->d_blk_sum, (void *)f->d_blk_nan, (void *)f->d_chain, (void *)f->d_cell_done,
                     (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_blk,
-                    (void *)f->d_blk_npaths, (void *)f->d_cnt_blk,
+                    (void *)f->d_blk_npaths, (void *)f->d_cnt_blk, (void *)f->d_pdesc,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -3304,7 +3357,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
-        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 4;   // + the launch clock's four counters
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 5;   // + the launch clock's four counters, the start flag
         void *h = nullptr, *m = nullptr;
         if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
@@ -3320,7 +3373,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->m_seq = (int64_t *)((char *)m + 2 * f->n_lblocks * sizeof(double));
             f->h_clk = (volatile unsigned long long *)((char *)h + (2 * f->n_lblocks + 1) * sizeof(double));
             f->m_clk = (unsigned long long *)((char *)m + (2 * f->n_lblocks + 1) * sizeof(double));
-            f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = 0;
+            f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = f->h_clk[4] = 0;
         }
     }
     if (rc != GGP_OK) {
@@ -3404,10 +3457,30 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             }
             check(dev_upload(&f->d_path_blk, pblk.data(), pblk.size()));
             check(dev_upload(&f->d_blk_npaths, bnp.data(), bnp.size()));
+            {
+                std::vector<int32_t> bt0(blk_ntrees.size() + 1, 0);   // each block's first tree (blk_t0)
+                for (size_t jj = 0; jj < blk_ntrees.size(); ++jj) bt0[jj + 1] = bt0[jj] + blk_ntrees[jj];
+                std::vector<PathDesc> pdv(heads.size());
+                for (size_t q = 0; q < heads.size(); ++q) {
+                    PathDesc &P = pdv[q];
+                    P.i_lo = pseq[q];
+                    P.i_hi = pseq[q + 1];
+                    P.c0 = pcells[(size_t)pseq[q]];
+                    P.j = pblk[q];
+                    P.npaths = bnp[(size_t)pblk[q]];
+                    P.nb = blk_ntrees[(size_t)pblk[q]];
+                    P.t0 = bt0[(size_t)pblk[q]];
+                    P.pad = 0;
+                    P.r0 = d->row_offset[P.c0];
+                    P.r1 = d->row_offset[P.c0 + 1];
+                }
+                check(dev_upload(&f->d_pdesc, pdv.data(), pdv.size()));
+            }
             check(dev_upload<unsigned>(&f->d_cnt_blk, nullptr, bnp.size()));
             if (rc == GGP_OK && hipMemset(f->d_cnt_blk, 0, bnp.size() * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
             if (rc == GGP_OK) {
                 ChainRed R{};
+                R.pdesc = f->d_pdesc;
                 R.path_blk = f->d_path_blk;
                 R.blk_npaths = f->d_blk_npaths;
                 R.tree_dfs = f->d_tree_dfs;
@@ -4240,20 +4313,25 @@ static int comm_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *na
 static int loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan_row)
 {
     if (f->comm) return comm_result(f, ll, nan_cell, nan_row);
-    std::vector<double> blocks((size_t)f->n_blocks, 0.0);
     long long code = kNoNan;
     for (Shard *s : f->shards) {
         const int rc = shard_wait(s);
         if (rc != GGP_OK) return rc;
     }
     f->tr_t2 = std::chrono::steady_clock::now();
+    size_t np2 = 1;
+    while (np2 < (size_t)f->n_blocks) np2 *= 2;
+    if (f->res_blocks.size() != np2) f->res_blocks.assign(np2, 0.0);
+    double *blocks = f->res_blocks.data();
+    std::fill(blocks + f->n_blocks, blocks + np2, 0.0);   // the pad (the tree overwrites the low slots)
     for (Shard *s : f->shards) {
+        const int64_t *gj = s->blk_global.data();
         for (int64_t j = 0; j < s->n_lblocks; ++j) {
-            blocks[(size_t)s->blk_global[j]] = s->h_sum[j];
+            blocks[(size_t)gj[j]] = s->h_sum[j];
             code = std::min<long long>(code, s->h_nan[j]);
         }
     }
-    const double v = top_sum(std::move(blocks));
+    const double v = f->n_blocks ? top_sum_inplace(blocks, np2) : 0.0;
     if (ll) *ll = v;
     if (nan_cell) *nan_cell = -1;
     if (nan_row) *nan_row = -1;
@@ -4288,7 +4366,9 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
         r.wait_us = us(f->tr_t1, t2);
         r.result_us = us(t2, t3);
         r.kernel_us = r.shader_mhz = 0.0;
+        r.dispatch_us = -1.0;
         const Shard *s0 = f->shards.empty() ? nullptr : f->shards[0];
+        if (s0 && s0->started_seen) r.dispatch_us = us(f->tr_t1, s0->t_started);
         if (s0 && s0->used_path && s0->clk_snap[3] > s0->clk_snap[2] && s0->clk_snap[1] > 0) {
             r.kernel_us = (double)(s0->clk_snap[3] - s0->clk_snap[2]) / 100.0;   // s_memrealtime: 100 MHz
             r.shader_mhz = (double)s0->clk_snap[0] / (double)s0->clk_snap[1] * 100.0;
@@ -4306,8 +4386,8 @@ int ggp_call_trace(const ggp_forest *f, int32_t cap, double *out, int32_t *n)
     const int32_t k = (int32_t)std::min<int64_t>(have, cap);
     for (int32_t i = 0; i < k; ++i) {   // the last k calls, oldest first
         const CallRec &r = f->tr_ring[(f->tr_n - k + i) % kCallRing];
-        const double v[6] = {r.enqueue_us, r.wait_us, r.result_us, r.kernel_us, r.shader_mhz, r.call};
-        std::memcpy(out + 6 * (size_t)i, v, sizeof v);
+        const double v[7] = {r.enqueue_us, r.wait_us, r.result_us, r.kernel_us, r.shader_mhz, r.call, r.dispatch_us};
+        std::memcpy(out + 7 * (size_t)i, v, sizeof v);
     }
     if (n) *n = k;
     return GGP_OK;
@@ -4481,7 +4561,7 @@ static int run_points(ggp_forest *f, int64_t np, const double *params, const int
         ++s->epoch;
         hipLaunchKernelGGL(k_loglik_wave<true>, dim3((unsigned)s->n_paths, (unsigned)np), dim3(64), 0, s->stream, s->F, P0,
                            s->d_path_cells, (int)nc, s->d_b_state, s->d_b_ll, s->d_b_nan, s->d_chain, s->d_b_done, s->epoch,
-                           s->d_path_seq, ChainRed{}, (int64_t)0, s->spin_max, (const double *)s->d_b_ptab,
+                           s->d_path_seq, chain_red_setup(s), (int64_t)0, s->spin_max, (const double *)s->d_b_ptab,
                            (const double *)s->d_state, pred ? (const int32_t *)s->d_b_pred : (const int32_t *)nullptr);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_reduce_blocks, dim3((unsigned)s->n_lblocks, (unsigned)np), dim3(s->red_threads), 0,

@@ -326,6 +326,34 @@ GGP_DEV double tab_entry(const int k)
     return i < 3 ? 0.0 : ggp_dawson_coef[GGP_DAWSON_NCOEF * r + (kTabRow - 1 - i)];
 }
 
+#if !defined(GGP_HOST_SIM)
+// The LDS image of the table (tab_entry for k = 0 .. kTabRows * kTabRow - 1), laid out in global
+// memory exactly as the launch copies it: each lane moves contiguous 16-byte pieces (10 coalesced
+// loads per lane instead of 19 gathers through tab_entry's row / column arithmetic).  The
+// coefficients come from a constexpr copy of the same dawson_table.inc.
+namespace cx {
+#pragma push_macro("GGP_DAWSON_TABLE_QUALIFIER")
+#undef GGP_DAWSON_TABLE_QUALIFIER
+#define GGP_DAWSON_TABLE_QUALIFIER constexpr
+#include "dawson_table.inc"
+#pragma pop_macro("GGP_DAWSON_TABLE_QUALIFIER")
+}  // namespace cx
+struct TabImg {
+    double v[kTabRows * kTabRow];
+};
+constexpr TabImg make_tab_img()
+{
+    TabImg T{};
+    for (int k = 0; k < kTabRows * kTabRow; ++k) {
+        const int r = k / kTabRow, i = k % kTabRow;
+        T.v[k] = r == kExpRow ? kExpCoef[i] : i < 3 ? 0.0 : cx::ggp_dawson_coef[GGP_DAWSON_NCOEF * r + (kTabRow - 1 - i)];
+    }
+    return T;
+}
+static_assert((kTabRows * kTabRow) % 2 == 0, "the image moves in 16-byte pieces");
+__constant__ __attribute__((aligned(16))) const TabImg kTabImg = make_tab_img();
+#endif
+
 // ---- lane constants -------------------------------------------------------------------------
 // LaneC: everything that does not depend on the parameters, a compile-time table (kLaneTab, one
 // row per lane, loaded once per launch); Lane: the registers the step reads, completed from

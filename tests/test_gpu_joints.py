@@ -9,8 +9,9 @@ oracle's, start row by start row:
     tol (crosscovariance_is_small, correlation_tree.h:484-493).  Every walk must emit exactly the
     oracle's pairs, in the same order, except after a threshold event: the first pair where the
     two walks part must have a cross ratio below BAND x tol on the side that emitted it (the
-    ratio of tiny cross-covariances is rounding-dominated there), and the walks may differ only
-    until they meet again (the next sibling subtree).  No blanket slack.
+    ratio of tiny cross-covariances is rounding-dominated there) -- or the common pair just before
+    it must, where the other walk stopped at that pair -- and the walks may differ only until they
+    meet again (the next sibling subtree).  No blanket slack.
   * values: every common pair whose cross ratio is above the margin (10 x tol) is compared,
     normalised by the oracle's standard deviations: at 1e-6, or -- where the reference algorithm
     itself is ill-conditioned -- at 10 x the oracle's own movement under +-1 ulp noise on exp()
@@ -45,19 +46,27 @@ def _unexplained(ix, vx, other, tol, band):
     starts = ix[:, 0]
     for s in np.unique(starts):
         boundary = False
+        prev = np.inf   # cross ratio / tol of this walk's previous pair
         for n in np.nonzero(starts == s)[0]:
             key = (int(ix[n, 0]), int(ix[n, 1]))
+            d = _ratio(vx[n]) / tol
             if key in other:
                 boundary = False
+                prev = d
                 continue
             if boundary:
+                prev = d
                 continue
-            d = _ratio(vx[n]) / tol
-            worst = max(worst, d)
-            if d < band:
+            # the event is this pair (the other walk stopped short of it) or the common pair before
+            # it (the other walk stopped AT it: its stop test saw a ratio below tol where this one
+            # saw one above -- the ratio along a walk need not fall monotonically)
+            ev = min(d, prev)
+            worst = max(worst, ev)
+            if ev < band:
                 boundary = True
             else:
                 bad.append((key, d))
+            prev = d
     return bad, worst
 
 

@@ -418,16 +418,27 @@ def _smoother_err(a, b):
     return float(em), float(ec)
 
 
-def _check_predict(hf, params, case):
+def _check_predict(hf, params, case, noise_seeds=()):
+    """the device's -p rows against the oracle's: each output within its case's bound, or -- with
+    noise_seeds -- within 3x the ORACLE's own movement under +-1 ulp random noise on every exp()
+    (those seeds) where that is larger: the reference's filter on the example is conditioned so that
+    an ulp anywhere moves the smoothed covariances by ~1e-5 of a standard deviation (measured
+    2026-10: the oracle moves by up to 8.4e-6 by itself), so the device's distance is held against
+    the reference algorithm's own rounding sensitivity rather than a fixed number"""
     import gfp_gaussian_process_amd as g
     from oracle import oracle as O
     got = g.Forest(hf).predict(params)
     ref = O.OracleForest(hf.a).predict(params)
-    for name, x, y in zip(("forward", "backward", "combined"), got, ref):
+    moves = [O.OracleForest(hf.a, exp_ulp_noise=sd).predict(params) for sd in noise_seeds]
+    for k, (name, x, y) in enumerate(zip(("forward", "backward", "combined"), got, ref)):
         assert np.all(np.isfinite(y)), name
         assert np.all(np.isfinite(x)), name
         em, ec = _smoother_err(x, y)
         bm, bc = pred_bound(case, name)
+        if moves:
+            nm = max(_smoother_err(mv[k], y)[0] for mv in moves)
+            nc = max(_smoother_err(mv[k], y)[1] for mv in moves)
+            bm, bc = max(bm, 3 * nm), max(bc, 3 * nc)
         print(f"PRED_ERR {case} {name} mean {em:.3e} (bound {bm:.1e}) cov {ec:.3e} (bound {bc:.1e})")
         assert em < bm and ec < bc, (case, name, em, ec)
 
@@ -435,7 +446,7 @@ def _check_predict(hf, params, case):
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
 def test_predict_example_vs_oracle(example_forests, noise, div):
     params = next(p for n, d, p in CONFIGS if (n, d) == (noise, div))
-    _check_predict(example_forests[(noise, div)], params, f"example/{noise}/{div}")
+    _check_predict(example_forests[(noise, div)], params, f"example/{noise}/{div}", noise_seeds=(12345, 777, 4242))
 
 
 def test_predict_segments_vs_oracle():

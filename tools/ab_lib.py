@@ -44,5 +44,15 @@ for _ in range(5):
     lv.append(f.launch_profile()[0])
 import numpy as np
 ms = np.median(np.array(lv), axis=0)
+kus = ""
+try:   # the path launch's own device time (ggp_call_trace; builds from round 6 on)
+    f2 = g.Forest(hf, kernel=kern)
+    for _ in range(3 + reps):
+        f2.total_likelihood(P)
+    tr = f2.call_trace(reps)
+    if len(tr) and np.all(tr[:, 3] > 0):
+        kus = f"  kernel_us {np.median(tr[:, 3]):.2f} enqueue_us {np.median(tr[:, 0]):.2f} mhz {np.median(tr[:, 4]):.0f}"
+except Exception:
+    pass
 print(f"{sys.argv[1]} {kern} trees={trees}: {1e3 * dt:.4f} ms/eval  levels " + " ".join(f"{m:.4f}" for m in ms)
-      + f"  ll={v!r}", flush=True)
+      + f"  ll={v!r}" + kus, flush=True)

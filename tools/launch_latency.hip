@@ -18,6 +18,30 @@ __global__ void k_empty() {}
 struct BigArgs {
     double v[64];
 };
+template <int N>
+struct Args {
+    double v[N];
+};
+template <int N>
+__global__ void k_args(Args<N> a, int64_t *seq, int64_t v)
+{
+    if (threadIdx.x == 0 && a.v[0] == 12345.0) __hip_atomic_store(seq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <int N>
+static double enqueue_after_sync(hipStream_t s, int64_t *d)
+{
+    Args<N> a{};
+    std::vector<double> t;
+    for (int i = 0; i < 1050; ++i) {
+        const auto x = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(k_args<N>, dim3(2000), dim3(64), 0, s, a, d, (int64_t)0);
+        const auto y = std::chrono::steady_clock::now();
+        (void)hipStreamSynchronize(s);
+        if (i >= 50) t.push_back(std::chrono::duration<double, std::micro>(y - x).count());
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
 __global__ void k_bigarg(BigArgs a, int64_t *seq, int64_t v)
 {
     if (threadIdx.x == 0 && a.v[0] == 12345.0) __hip_atomic_store(seq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -72,6 +96,16 @@ int main()
         if (i >= 50) enq.push_back(std::chrono::duration<double, std::micro>(b - a).count());
     }
     std::sort(enq.begin(), enq.end());
+    // the same with no arguments: does the argument block's size show in the enqueue?
+    std::vector<double> enq0;
+    for (int i = 0; i < 2050; ++i) {
+        const auto a = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(k_empty, dim3(2000), dim3(64), 0, s);
+        const auto b = std::chrono::steady_clock::now();
+        (void)hipStreamSynchronize(s);
+        if (i >= 50) enq0.push_back(std::chrono::duration<double, std::micro>(b - a).count());
+    }
+    std::sort(enq0.begin(), enq0.end());
     int dev = 0;
     const double gd = median_us([&](int) { (void)hipGetDevice(&dev); });
     const double sd = median_us([&](int) { (void)hipSetDevice(dev); });
@@ -95,12 +129,12 @@ int main()
     ggp_forest *f2 = nullptr;
     ggp_forest_create(&d2, &f2);
     const double c2 = median_us([&](int) { ggp_total_loglik(f2, P, &ll, &nc, &nr); }, 500);
-    std::vector<double> tr(6 * 500);
+    std::vector<double> tr(7 * 500);
     int32_t ntr = 0;
     ggp_call_trace(f2, 500, tr.data(), &ntr);
     auto med = [&](int k) {
         std::vector<double> x;
-        for (int i = 0; i < ntr; ++i) x.push_back(tr[6 * i + k]);
+        for (int i = 0; i < ntr; ++i) x.push_back(tr[7 * i + k]);
         std::sort(x.begin(), x.end());
         return x.empty() ? 0.0 : x[x.size() / 2];
     };
@@ -110,9 +144,13 @@ int main()
     printf("ggp_total_loglik, 1 tree x 4 rows     %7.2f us   (4 cells' steps, setup, reduction)\n", g);
     printf("enqueue of a 2000-block launch, 520 B of arguments  %7.2f us (median), %7.2f us (p90)\n",
            enq[enq.size() / 2], enq[enq.size() * 9 / 10]);
+    printf("enqueue of a 2000-block launch, no arguments        %7.2f us (median)\n", enq0[enq0.size() / 2]);
+    printf("enqueue by argument bytes (+16): 64 %.2f, 128 %.2f, 192 %.2f, 256 %.2f, 320 %.2f, 384 %.2f us\n",
+           enqueue_after_sync<8>(s, d), enqueue_after_sync<16>(s, d), enqueue_after_sync<24>(s, d),
+           enqueue_after_sync<32>(s, d), enqueue_after_sync<40>(s, d), enqueue_after_sync<48>(s, d));
     printf("hipGetDevice %7.3f us, hipSetDevice (same device) %7.3f us, hipGetLastError %7.3f us\n", gd, sd, le);
-    printf("ggp_total_loglik C2 (1000 x 200)      %7.2f us: enqueue %.2f, wait %.2f (kernel %.2f), result %.2f\n", c2,
-           med(0), med(1), med(3), med(2));
+    printf("ggp_total_loglik C2 (1000 x 200)      %7.2f us: enqueue %.2f, wait %.2f (dispatch %.2f, kernel %.2f), result %.2f\n",
+           c2, med(0), med(1), med(6), med(3), med(2));
     ggp_forest_destroy(f2);
     ggp_host_forest_free(h2);
     ggp_forest_destroy(f);
