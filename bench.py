@@ -284,18 +284,14 @@ def host_split(step_t, trace) -> dict:
     if trace is not None and len(trace) == len(wall):
         enq, wait, res, kern, mhz = (trace[:, k] for k in range(5))
         out.update({"enqueue_us": stats(enq), "wait_us": stats(wait), "result_us": stats(res)})
-        disp = trace[:, 6]
         out["python_us"] = stats(wall - enq - wait - res)
         if np.all(kern > 0):
             out.update({"kernel_us": stats(kern), "shader_mhz": stats(mhz),
                         "host_us": stats(wall - kern),
                         "dispatch_and_completion_us": stats(wait - kern)})
-            if np.all(disp >= 0):
-                out.update({"dispatch_us": stats(disp), "completion_us": stats(wait - disp - kern)})
-        out["note"] = ("per timed step: wall = python + enqueue + wait + result; wait = dispatch (enqueued to the "
-                       "launch's start flag seen by the waiting host) + kernel (its first block start to its publishing "
-                       "block's end on the device's 100 MHz counter) + completion (the sequence number's trip to the "
-                       "host); ggp_call_trace")
+        out["note"] = ("per timed step: wall = python + enqueue + wait + result; wait = the launch's dispatch + kernel "
+                       "(its first block start to its publishing block's end on the device's 100 MHz counter) + the "
+                       "completion's trip to the host; ggp_call_trace")
     return out
 
 

@@ -998,9 +998,7 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
     __builtin_amdgcn_s_waitcnt(0);
     if (add_agent(R.done) + 1 != (unsigned)R.n_lblocks) return;
     zero_agent(R.done);
-    if (R.clk)   // the launch's end on the 100 MHz counter (ggp_call_trace), before the sequence number
-        __hip_atomic_store(R.clk + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     // every block's slots reached host memory before its count: each block's system-scope stores to
     // the fine-grained (uncached) host slots are acknowledged by the fabric before its s_waitcnt(0)
     // lets the count go out, so they are host-visible when the last block sees the full count.
@@ -1011,6 +1009,9 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
 #else
     __hip_atomic_store(R.out_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
+    // the launch's end on the 100 MHz counter (ggp_call_trace), AFTER the sequence number: nothing
+    // waits for it (the host reads it when it next enters the handle, long after it landed)
+    if (R.clk) __hip_atomic_store(R.clk + 3, t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1046,9 +1047,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // the launch's shader clock (ggp_launch_clock): block 0 reads the shader-clock counter and the
     // constant 100 MHz counter at its start and after its path (two scalar reads each)
     const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-    // the call's start, seen by the host as it waits (ggp_call_trace: dispatch vs completion)
-    if (red.clk && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
-        __hip_atomic_store(red.clk + 4, (unsigned long long)call_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
     GGP_TL(0);
@@ -2695,8 +2693,6 @@ struct Shard {
     volatile unsigned long long *h_clk = nullptr;   // path launches: block 0's clock counters
     PathDesc *d_pdesc = nullptr;                    // path launches: per path (PathDesc)
     unsigned long long clk_snap[4] = {0, 0, 0, 0}; // h_clk as the last completed launch left it
-    std::chrono::steady_clock::time_point t_started;  // when the wait saw the path launch's start flag
-    bool started_seen = false;
     unsigned long long *m_clk = nullptr;
     // the largest |dt| of any propagation of the shard (in-cell steps and divisions): with the
     // parameters it bounds |k dt| for the wave schedule's product factors exp(-gl dt), exp(-gq dt),
@@ -2796,7 +2792,7 @@ static void comm_fail(Comm *c)
 
 // one objective call's host split (ggp_call_trace)
 struct CallRec {
-    double enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call, dispatch_us;
+    double enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call;
 };
 constexpr int kCallRing = 512;
 
@@ -2804,6 +2800,7 @@ struct ggp_forest {
     int64_t n_cells = 0, n_rows = 0, n_trees = 0, blk_trees = 1, n_blocks = 0;
     std::chrono::steady_clock::time_point tr_t0, tr_t1, tr_t2;   // the pending call's entry, enqueue end, wait end
     bool tr_pending = false;
+    int64_t tr_open = -1;              // ring entry whose kernel end stamp is still to be read
     int64_t tr_n = 0;                  // calls recorded
     CallRec tr_ring[kCallRing];
     std::vector<DeviceCtx *> devs;
@@ -2983,16 +2980,8 @@ int shard_wait(Shard *s)
 {
     if (s->n_cells == 0) return GGP_OK;
     bool seen = false;
-    s->started_seen = false;
     if (s->spin && s->seq_pending) {
-        // a path launch's block 0 raises its start flag (h_clk[4] = the call's number) as it
-        // begins: the wait notes when it sees it (ggp_call_trace), a few loads per poll
-        const bool flag = s->used_path && s->h_clk != nullptr;
         for (uint32_t it = 1;; ++it) {
-            if (flag && !s->started_seen && s->h_clk[4] == (unsigned long long)s->seq) {
-                s->t_started = std::chrono::steady_clock::now();
-                s->started_seen = true;
-            }
             if (*s->h_seq == s->seq) { seen = true; break; }
             if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
         }
@@ -3357,7 +3346,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
-        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 5;   // + the launch clock's four counters, the start flag
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 4;   // + the launch clock's four counters
         void *h = nullptr, *m = nullptr;
         if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
@@ -3373,7 +3362,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->m_seq = (int64_t *)((char *)m + 2 * f->n_lblocks * sizeof(double));
             f->h_clk = (volatile unsigned long long *)((char *)h + (2 * f->n_lblocks + 1) * sizeof(double));
             f->m_clk = (unsigned long long *)((char *)m + (2 * f->n_lblocks + 1) * sizeof(double));
-            f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = f->h_clk[4] = 0;
+            f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = 0;
         }
     }
     if (rc != GGP_OK) {
@@ -4185,6 +4174,20 @@ int ggp_set_state(ggp_forest *f, const double *in)
     return GGP_OK;
 }
 
+// the last path launch's device time into its ring entry: its first block's start (written before
+// the sequence number) and its publishing block's end (written just after it; a stamp older than
+// the start is one that has not landed: the entry keeps kernel_us = 0)
+static void trace_finalize(ggp_forest *f)
+{
+    if (f->tr_open < 0 || f->shards.empty()) return;
+    const Shard *s0 = f->shards[0];
+    CallRec &r = f->tr_ring[f->tr_open];
+    f->tr_open = -1;
+    if (!s0->h_clk) return;
+    const unsigned long long t0 = s0->clk_snap[2], t1 = s0->h_clk[3];
+    if (t1 > t0) r.kernel_us = (double)(t1 - t0) / 100.0;   // s_memrealtime: 100 MHz
+}
+
 int ggp_total_loglik_async(ggp_forest *f, const double *params)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
@@ -4194,6 +4197,7 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
         return GGP_EDEV;
     }
     f->tr_t0 = std::chrono::steady_clock::now();
+    trace_finalize(f);   // before the next launch can overwrite the stamps
     ggp_params P;
     std::memcpy(P.p, params, sizeof P.p);
     for (Shard *s : f->shards) {   // every device enqueued before any is waited for
@@ -4366,13 +4370,12 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
         r.wait_us = us(f->tr_t1, t2);
         r.result_us = us(t2, t3);
         r.kernel_us = r.shader_mhz = 0.0;
-        r.dispatch_us = -1.0;
         const Shard *s0 = f->shards.empty() ? nullptr : f->shards[0];
-        if (s0 && s0->started_seen) r.dispatch_us = us(f->tr_t1, s0->t_started);
-        if (s0 && s0->used_path && s0->clk_snap[3] > s0->clk_snap[2] && s0->clk_snap[1] > 0) {
-            r.kernel_us = (double)(s0->clk_snap[3] - s0->clk_snap[2]) / 100.0;   // s_memrealtime: 100 MHz
+        if (s0 && s0->used_path && s0->clk_snap[1] > 0)
             r.shader_mhz = (double)s0->clk_snap[0] / (double)s0->clk_snap[1] * 100.0;
-        }
+        // the kernel's end stamp lands just after the sequence number: read when the handle is next
+        // entered (trace_finalize)
+        f->tr_open = s0 && s0->used_path ? (int64_t)(f->tr_n % kCallRing) : -1;
         r.call = (double)f->tr_n;
         ++f->tr_n;
     }
@@ -4382,12 +4385,13 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
 int ggp_call_trace(const ggp_forest *f, int32_t cap, double *out, int32_t *n)
 {
     if (!f || cap < 0 || (cap > 0 && !out)) return GGP_EINVAL;
+    trace_finalize(const_cast<ggp_forest *>(f));
     const int64_t have = std::min<int64_t>(f->tr_n, kCallRing);
     const int32_t k = (int32_t)std::min<int64_t>(have, cap);
     for (int32_t i = 0; i < k; ++i) {   // the last k calls, oldest first
         const CallRec &r = f->tr_ring[(f->tr_n - k + i) % kCallRing];
-        const double v[7] = {r.enqueue_us, r.wait_us, r.result_us, r.kernel_us, r.shader_mhz, r.call, r.dispatch_us};
-        std::memcpy(out + 7 * (size_t)i, v, sizeof v);
+        const double v[6] = {r.enqueue_us, r.wait_us, r.result_us, r.kernel_us, r.shader_mhz, r.call};
+        std::memcpy(out + 6 * (size_t)i, v, sizeof v);
     }
     if (n) *n = k;
     return GGP_OK;

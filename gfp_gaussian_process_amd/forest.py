@@ -497,9 +497,9 @@ class Forest:
         return mhz.value, us.value
 
     def call_trace(self, last: int = 512) -> np.ndarray:
-        """the host split of the last `last` objective calls (ggp_call_trace), oldest first: [k, 7] =
-        (enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call index, dispatch_us)"""
-        out = np.zeros((max(1, last), 7))
+        """the host split of the last `last` objective calls (ggp_call_trace), oldest first: [k, 6] =
+        (enqueue_us, wait_us, result_us, kernel_us, shader_mhz, call index)"""
+        out = np.zeros((max(1, last), 6))
         n = ctypes.c_int32()
         self._check(self._lib.ggp_call_trace(self._h, int(last), out.ctypes.data_as(N.c_double_p), ctypes.byref(n)))
         return out[: n.value]

@@ -274,14 +274,13 @@ int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last 
  * DVFS clock of a real evaluation, for a benchmark line.  GGP_EINVAL if none ran on this handle. */
 int ggp_launch_clock(const ggp_forest *f, double *shader_mhz, double *window_us);
 /* The host split of the handle's last objective calls (ggp_total_loglik, or ggp_total_loglik_async +
- * ggp_loglik_result), for a benchmark line: out[7i..7i+6] for the last *n = min(calls, cap, 512)
+ * ggp_loglik_result), for a benchmark line: out[6i..6i+5] for the last *n = min(calls, cap, 512)
  * calls, oldest first = (enqueue_us: entry to the launches enqueued, wait_us: enqueued to the
  * completion seen through mapped memory, result_us: the host's sum and return, kernel_us: the path
  * launch's first block start to its publishing block's end on the device's 100 MHz counter (0 without
  * a path launch), shader_mhz: that launch's clock as ggp_launch_clock reports it, call: the call's
- * index on the handle, dispatch_us: enqueued to the path launch's start flag seen by the waiting host
- * (-1 if not seen)).  wait_us - dispatch_us - kernel_us is the completion's trip to the host.  Two
- * clock reads per call and one flag store per path launch; no other device work. */
+ * index on the handle).  wait_us - kernel_us is the launch's dispatch plus the completion's trip to
+ * the host.  Two clock reads per call; no device work beyond the path launch's clock counters. */
 int ggp_call_trace(const ggp_forest *f, int32_t cap, double *out, int32_t *n);
 int32_t ggp_comm_size(const ggp_forest *f);       /* ranks of the attached RCCL communicator as RCCL
                                                      counts them (ncclCommCount); 0 = not attached,

@@ -418,6 +418,29 @@ def _smoother_err(a, b):
     return float(em), float(ec)
 
 
+_NOISE_SEEDS = (12345, 777, 4242)
+_NOISE_CACHE = {}
+
+
+def _oracle_noise(hf, params, case):
+    """per output (forward, backward, combined): the ORACLE's own largest (mean, covariance) movement
+    under +-1 ulp random noise on every exp() over three seeds (cached per case)"""
+    if case not in _NOISE_CACHE:
+        from oracle import oracle as O
+        ref = O.OracleForest(hf.a).predict(params)
+        moves = [O.OracleForest(hf.a, exp_ulp_noise=sd).predict(params) for sd in _NOISE_SEEDS]
+        _NOISE_CACHE[case] = [(max(_smoother_err(mv[k], ref[k])[0] for mv in moves),
+                               max(_smoother_err(mv[k], ref[k])[1] for mv in moves)) for k in range(3)]
+    return _NOISE_CACHE[case]
+
+
+def example_pred_bound(hf, params, case, output):
+    """an example case's bound: pred_bound, or 3x the oracle's own +-1 ulp movement where larger"""
+    bm, bc = pred_bound(case, output)
+    nm, nc = _oracle_noise(hf, params, case)[("forward", "backward", "combined").index(output)]
+    return max(bm, 3 * nm), max(bc, 3 * nc)
+
+
 def _check_predict(hf, params, case, noise_seeds=()):
     """the device's -p rows against the oracle's: each output within its case's bound, or -- with
     noise_seeds -- within 3x the ORACLE's own movement under +-1 ulp random noise on every exp()
@@ -429,16 +452,11 @@ def _check_predict(hf, params, case, noise_seeds=()):
     from oracle import oracle as O
     got = g.Forest(hf).predict(params)
     ref = O.OracleForest(hf.a).predict(params)
-    moves = [O.OracleForest(hf.a, exp_ulp_noise=sd).predict(params) for sd in noise_seeds]
-    for k, (name, x, y) in enumerate(zip(("forward", "backward", "combined"), got, ref)):
+    for name, x, y in zip(("forward", "backward", "combined"), got, ref):
         assert np.all(np.isfinite(y)), name
         assert np.all(np.isfinite(x)), name
         em, ec = _smoother_err(x, y)
-        bm, bc = pred_bound(case, name)
-        if moves:
-            nm = max(_smoother_err(mv[k], y)[0] for mv in moves)
-            nc = max(_smoother_err(mv[k], y)[1] for mv in moves)
-            bm, bc = max(bm, 3 * nm), max(bc, 3 * nc)
+        bm, bc = example_pred_bound(hf, params, case, name) if noise_seeds else pred_bound(case, name)
         print(f"PRED_ERR {case} {name} mean {em:.3e} (bound {bm:.1e}) cov {ec:.3e} (bound {bc:.1e})")
         assert em < bm and ec < bc, (case, name, em, ec)
 
@@ -446,7 +464,7 @@ def _check_predict(hf, params, case, noise_seeds=()):
 @pytest.mark.parametrize("noise,div", [("scaled", "binomial"), ("const", "gauss")])
 def test_predict_example_vs_oracle(example_forests, noise, div):
     params = next(p for n, d, p in CONFIGS if (n, d) == (noise, div))
-    _check_predict(example_forests[(noise, div)], params, f"example/{noise}/{div}", noise_seeds=(12345, 777, 4242))
+    _check_predict(example_forests[(noise, div)], params, f"example/{noise}/{div}", noise_seeds=_NOISE_SEEDS)
 
 
 def test_predict_segments_vs_oracle():
@@ -554,7 +572,7 @@ def test_combine_fast_form_vs_exact(example_forests, noise, div, monkeypatch):
     em, ec = _smoother_err(got[2], exact[2])
     assert em < 1e-9 and ec < 1e-9, (em, ec)
     ref = O.OracleForest(hf.a).predict(params)[2]
-    bm, bc = pred_bound(f"example/{noise}/{div}", "combined")
+    bm, bc = example_pred_bound(hf, params, f"example/{noise}/{div}", "combined")
     for x in (got[2], exact[2]):
         em, ec = _smoother_err(x, ref)
         print(f"PRED_ERR combine_form mean {em:.3e} cov {ec:.3e}")

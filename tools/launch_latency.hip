@@ -129,12 +129,12 @@ int main()
     ggp_forest *f2 = nullptr;
     ggp_forest_create(&d2, &f2);
     const double c2 = median_us([&](int) { ggp_total_loglik(f2, P, &ll, &nc, &nr); }, 500);
-    std::vector<double> tr(7 * 500);
+    std::vector<double> tr(6 * 500);
     int32_t ntr = 0;
     ggp_call_trace(f2, 500, tr.data(), &ntr);
     auto med = [&](int k) {
         std::vector<double> x;
-        for (int i = 0; i < ntr; ++i) x.push_back(tr[7 * i + k]);
+        for (int i = 0; i < ntr; ++i) x.push_back(tr[6 * i + k]);
         std::sort(x.begin(), x.end());
         return x.empty() ? 0.0 : x[x.size() / 2];
     };
@@ -149,8 +149,8 @@ int main()
            enqueue_after_sync<8>(s, d), enqueue_after_sync<16>(s, d), enqueue_after_sync<24>(s, d),
            enqueue_after_sync<32>(s, d), enqueue_after_sync<40>(s, d), enqueue_after_sync<48>(s, d));
     printf("hipGetDevice %7.3f us, hipSetDevice (same device) %7.3f us, hipGetLastError %7.3f us\n", gd, sd, le);
-    printf("ggp_total_loglik C2 (1000 x 200)      %7.2f us: enqueue %.2f, wait %.2f (dispatch %.2f, kernel %.2f), result %.2f\n",
-           c2, med(0), med(1), med(6), med(3), med(2));
+    printf("ggp_total_loglik C2 (1000 x 200)      %7.2f us: enqueue %.2f, wait %.2f (kernel %.2f), result %.2f\n",
+           c2, med(0), med(1), med(3), med(2));
     ggp_forest_destroy(f2);
     ggp_host_forest_free(h2);
     ggp_forest_destroy(f);
