@@ -470,6 +470,28 @@ def main() -> int:
     for _ in range(args.warmup):
         obj.total_likelihood(P_EXAMPLE)
 
+    # ---- roofline of the dominant kernel, HIP events on the engine's stream: a profiled window of
+    # the same evaluations right after the warm-up, while the clock is the one the timed steps run at
+    # (a gap of tens of ms before it would drop the clock to ~2.2 GHz for milliseconds, DESIGN.md §6
+    # "The clock"); the events leave the handle's spin wait for a stream synchronisation, so the
+    # window is separate from the timed steps, which follow it after W more warm-up calls ----
+    fg.enable_profile()
+    per = {}                                   # kernel name -> [ms, rows, launches]
+    clocks = []
+    for _ in range(max(3, min(args.steps, 10))):
+        fg.total_likelihood(P_EXAMPLE)
+        ck = fg.launch_clock()
+        if ck:
+            clocks.append(ck[0])
+        for ms, rows, name in zip(*fg.launch_profile()):
+            acc = per.setdefault(name, [0.0, 0, 0])
+            acc[0] += ms
+            acc[1] += rows
+            acc[2] += 1
+    fg.disable_profile()
+    for _ in range(args.warmup):
+        obj.total_likelihood(P_EXAMPLE)
+
     # ---- timed region: exactly K steps (each step's wall time kept: the line's `steps_us`; the
     # collector paused so no collection lands inside a step) ----
     import gc
@@ -566,20 +588,8 @@ def main() -> int:
             eng["kind"] = "engine RCCL (ggp_comm_attach): partial, ncclAllGather, rank-order sum on the engine's stream"
             c4s["engine_rccl"] = eng
 
-    # ---- roofline of the dominant kernel, HIP events on the engine's stream ----
-    fg.enable_profile()
-    per = {}                                   # kernel name -> [ms, rows, launches]
-    clocks = []
-    for _ in range(max(3, min(args.steps, 10))):
-        fg.total_likelihood(P_EXAMPLE)
-        ck = fg.launch_clock()
-        if ck:
-            clocks.append(ck[0])
-        for ms, rows, name in zip(*fg.launch_profile()):
-            acc = per.setdefault(name, [0.0, 0, 0])
-            acc[0] += ms
-            acc[1] += rows
-            acc[2] += 1
+    # ---- roofline of the dominant kernel: HIP events on the engine's stream, recorded before the
+    # timed region (above) ----
     if c4s is not None:   # released only now: freeing a 2e7-row forest (host and device) idles the GPU
         # long enough for its clock to fall, so neither the headline's steps nor its profiled launches
         # may follow it (DESIGN.md §6 "The clock")

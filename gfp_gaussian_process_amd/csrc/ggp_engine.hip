@@ -4777,6 +4777,17 @@ int ggp_last_launch_profile(ggp_forest *ff, float *ms, int64_t *rows, int32_t *k
     DeviceGuard device_guard_;   // the caller's current device is restored on return
     if (!ff || !n || ff->shards.empty()) return GGP_EINVAL;
     Shard *f = ff->shards[0];   // the first shard's launches
+    if (cap < 0) {   // switch the events off again (the spin wait returns)
+        *n = 0;
+        if (!f->profile) return GGP_OK;
+        HIPCHK(hipSetDevice(f->device));
+        HIPCHK(hipStreamSynchronize(f->stream));
+        for (auto &e : f->ev) (void)hipEventDestroy(e);
+        f->ev.clear();
+        f->n_prof = 0;
+        f->profile = false;
+        return GGP_OK;
+    }
     if (!f->profile) {
         // enable for subsequent calls: one event pair per level
         HIPCHK(hipSetDevice(f->device));

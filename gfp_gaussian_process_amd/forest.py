@@ -681,6 +681,11 @@ class Forest:
         n = ctypes.c_int32()
         self._check(self._lib.ggp_last_launch_profile(self._h, None, None, None, 0, ctypes.byref(n)))
 
+    def disable_profile(self) -> None:
+        """switch the launch events off again (ggp_last_launch_profile with cap < 0)"""
+        n = ctypes.c_int32()
+        self._check(self._lib.ggp_last_launch_profile(self._h, None, None, None, -1, ctypes.byref(n)))
+
     def launch_profile(self):
         cap = 4096
         ms = (ctypes.c_float * cap)()
