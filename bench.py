@@ -478,7 +478,8 @@ def main() -> int:
     fg.enable_profile()
     per = {}                                   # kernel name -> [ms, rows, launches]
     clocks = []
-    for _ in range(max(3, min(args.steps, 10))):
+    n_prof = max(3, min(args.steps, 10))
+    for _ in range(n_prof):
         fg.total_likelihood(P_EXAMPLE)
         ck = fg.launch_clock()
         if ck:
@@ -941,6 +942,8 @@ def main() -> int:
             },
             "fp64": fp64,
             "total_log_likelihood": ll,
+            # the chained calls behind that total: W warm-up, the profiled window, W, then the K steps
+            "chained_calls": 2 * args.warmup + n_prof + args.steps,
             "steps_us": steps_us,
             "clock": None if clock_timed is None else {
                 "shader_mhz_last_timed_launch": clock_timed[0], "window_us": clock_timed[1],

@@ -58,6 +58,25 @@ struct DevForest {
 };
 
 constexpr int kNanNone = 0x7fffffff;
+constexpr int kRowStall = 0xffffff;   // a cell never has 2^24 - 1 rows (ggp_forest_create checks)
+
+// agent-coherent (every XCD) loads and stores: the hand-offs between workgroups of one launch
+GGP_DEV unsigned add_agent(unsigned *p) { return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+GGP_DEV void zero_agent(unsigned *p) { __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+GGP_DEV double ld_agent(const double *p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+GGP_DEV void st_agent(double *p, const double v)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+GGP_DEV T ld_agent_i(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+GGP_DEV void st_agent_i(T *p, const T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // lane-schedule kernels' register budget (tools/lane_wpe_ab.py builds a GGP_LANE_WPE=2 variant)
 #ifdef GGP_LANE_WPE
@@ -133,25 +152,48 @@ GGP_DEV bool cell_prologue(const DevForest &F, const double *p, const double *st
 // one generation depth.  `cpw` cells per 64-lane wave: < 64 spreads a small level over
 // more SIMDs (latency), 64 packs waves (throughput); results do not depend on it.
 // ------------------------------------------------------------------------------------------
-GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t *__restrict__ cells,
-                              const int n, const int cpw, double *__restrict__ state,
-                              double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan,
-                              const double *s_tab, const int lane)
+// one cell of the lane schedule (the cell's lane).  QUEUE (k_loglik_lane_queue): a parent in the
+// same launch is read with agent-coherent loads once its done flag is seen, a stalled wait makes
+// the cell a stall (no rows run), and a cell with daughters in the launch publishes its final
+// state (coherent stores, then its flag); the arithmetic is the same either way
+template <bool QUEUE>
+GGP_DEV void lane_cell_body(const DevForest &F, const double *p, const int c, double *__restrict__ state,
+                            double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const double *s_tab,
+                            const bool stall = false, const bool publish = false, unsigned *cell_done = nullptr,
+                            const unsigned epoch = 0)
 {
-    if (lane >= cpw) return;
-    const int i = blockIdx.x * cpw + lane;
-    if (i >= n) return;
-    const int c = cells[i];
     const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
     double m[4], C[16];
     const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
     double dt = 0.0;
-    bool pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+    bool pending;
+    if constexpr (QUEUE) {
+        const int par = F.parent[c];
+        if (par < 0) {
+            pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+        } else {   // the parent's final posterior, written by another workgroup of this launch
+            const double *ps = state + (size_t)20 * par;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = ld_agent(ps + k);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) C[k] = ld_agent(ps + 4 + k);
+            dt = F.time[r0] - F.time[F.row_off[par + 1] - 1];
+            pending = true;
+        }
+    } else {
+        pending = cell_prologue(F, p, state, c, r0, m, C, dt);
+    }
     bool divide = pending;
     double cl = 0.0;
     int nan_row = kNanNone;
     double t_cur = F.time[r0];
-    for (int64_t r = r0; r < r1; ++r) {
+    int64_t r_end = r1;
+    if (QUEUE && stall) {   // the parent never published: no row runs, the cell reports the stall
+        cl = __longlong_as_double(0x7ff8000000000000LL);
+        nan_row = kRowStall;
+        r_end = r0;
+    }
+    for (int64_t r = r0; r < r_end; ++r) {
         // this row's data and the next row's time, loaded before the propagation they would
         // otherwise wait behind (the same values)
         const double y_l = F.logl[r], y_f = F.fp[r];
@@ -178,12 +220,34 @@ GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t
         t_cur = t_next;
     }
     double *st = state + (size_t)20 * c;
+    if (QUEUE && publish) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st[k] = m[k];
+        for (int k = 0; k < 4; ++k) st_agent(st + k, m[k]);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+        for (int k = 0; k < 16; ++k) st_agent(st + 4 + k, C[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[k] = m[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) st[4 + k] = C[k];
+    }
     cell_ll[F.dfs_rank[c]] = cl;
     cell_nan[F.dfs_rank[c]] = nan_row;
+    if (QUEUE && publish) {
+        __builtin_amdgcn_s_waitcnt(0);   // the state at the coherence point, then the flag
+        __hip_atomic_store(cell_done + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+GGP_DEV void loglik_lane_cell(const DevForest &F, const double *p, const int32_t *__restrict__ cells,
+                              const int n, const int cpw, double *__restrict__ state,
+                              double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan,
+                              const double *s_tab, const int lane)
+{
+    if (lane >= cpw) return;
+    const int i = blockIdx.x * cpw + lane;
+    if (i >= n) return;
+    lane_cell_body<false>(F, p, cells[i], state, cell_ll, cell_nan, s_tab);
 }
 
 __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_loglik_level(DevForest F, ggp_params P,
@@ -216,6 +280,57 @@ __global__ __launch_bounds__(64) GGP_LANE_ATTR void k_loglik_level_batch(DevFore
     const int64_t pt = blockIdx.y;
     loglik_lane_cell(F, ptab + 11 * pt, cells, n, cpw, state + pt * n_cells * 20, cell_ll + pt * n_cells,
                      cell_nan + pt * n_cells, s_tab, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// LANE QUEUE: a run of consecutive lane-schedule levels in one persistent launch.  The levels'
+// cells are cut into chunks of up to 64 (one cell per lane, the level order), and one workgroup
+// per SIMD takes chunks from a counter until none is left.  A chunk of a later level of the run
+// waits, lane by lane, for its cells' parents' done flags; every chunk ahead of it in the queue
+// is held by a running workgroup, so the waits end.  Level-by-level launches leave the SIMDs
+// idle on the last round of each level: C4 (1e5 roots of 100 rows, then 2e5 daughters of 50)
+// takes 2 rounds of roots and 4 of daughters, 400 row-steps, where the queue starts daughters in
+// the roots' second round, 350.  The cell body is the lane schedule's (lane_cell_body): results
+// are bitwise the level launches'.
+// ------------------------------------------------------------------------------------------
+struct QChunk {
+    int32_t a, n;        // the chunk's cells: level_cells[a .. a + n)
+    int32_t wait;        // 1: the cells' parents are in the launch (their flags are waited for)
+    int32_t publish;     // 1: the cells' daughters are in the launch (flags published)
+};
+
+__global__ __launch_bounds__(64) GGP_LANE_ATTR void k_loglik_lane_queue(
+    DevForest F, ggp_params P, const int32_t *__restrict__ cells, const QChunk *__restrict__ chunks, int n_chunks,
+    unsigned *qctr, unsigned *cell_done, unsigned epoch, unsigned spin_max, double *__restrict__ state,
+    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan)
+{
+    __shared__ double s_tab[kDawsonTab];
+    const int lane = threadIdx.x;
+    load_dawson_table(s_tab, lane);
+    __syncthreads();
+    for (;;) {   // every workgroup ends when the counter passes n_chunks
+        unsigned k = 0;
+        if (lane == 0) k = add_agent(qctr);
+        k = (unsigned)__builtin_amdgcn_readfirstlane((int)k);
+        if (k >= (unsigned)n_chunks) break;
+        const QChunk q = chunks[k];
+        if (lane < q.n) {
+            const int c = cells[q.a + lane];
+            bool stall = false;
+            if (q.wait) {
+                const int par = F.parent[c];
+                unsigned spins = 0;
+                while (par >= 0 && ld_agent_i(cell_done + par) != epoch) {
+                    if (++spins > spin_max) {
+                        stall = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            lane_cell_body<true>(F, P.p, c, state, cell_ll, cell_nan, s_tab, stall, q.publish != 0, cell_done, epoch);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -860,22 +975,6 @@ struct ChainRed {
 };
 constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
 
-GGP_DEV unsigned add_agent(unsigned *p) { return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-GGP_DEV void zero_agent(unsigned *p) { __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-GGP_DEV double ld_agent(const double *p)
-{
-    return __longlong_as_double(
-        (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-GGP_DEV void st_agent(double *p, const double v)
-{
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T>
-GGP_DEV T ld_agent_i(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <class T>
-GGP_DEV void st_agent_i(T *p, const T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // what the reduction of path b needs, loaded at the launch's start and parked in LDS (red[0..63]:
 // lane k <= nb the DFS start of the block's tree k, k = nb its end; red[64..66]: the block j, its
@@ -1020,7 +1119,6 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
 // block.  A second daughter whose parent does not finish within spin_max polls ends as a stall
 // (NaN total, row kRowStall: GGP_ETIMEOUT on the host).
 // ------------------------------------------------------------------------------------------
-constexpr int kRowStall = 0xffffff;   // a cell never has 2^24 - 1 rows (ggp_forest_create checks)
 
 // k_loglik_wave's workgroups are one wave: the LDS executes a wave's DS instructions in issue
 // order, so a write is seen by every later read of the same wave without waiting for it (no
@@ -2672,6 +2770,18 @@ struct Shard {
     unsigned *d_cnt_blk = nullptr;
     ChainRed red{};                    // the path launch's in-launch reduction (a kernel argument)
     std::vector<int32_t> level_kind;   // GGP_KERNEL_* each level runs
+    // lane queue (k_loglik_lane_queue): runs of >= 2 consecutive lane-schedule levels, each one
+    // persistent launch over its chunks; the launch's chunk counter (zeroed before it)
+    struct QRun {
+        int la, lb;                    // levels la .. lb - 1
+        int64_t off, n, rows;          // chunks d_qchunks[off .. off + n), the run's rows
+    };
+    std::vector<QRun> qruns;
+    std::vector<int32_t> qrun_at;      // level -> its run (-1: none / not the run's first level)
+    QChunk *d_qchunks = nullptr;
+    unsigned *d_qctr = nullptr;
+    bool lane_queue = true;            // GGP_LANE_QUEUE=0: level-by-level lane launches
+    int queue_resident = 1024;         // k_loglik_lane_queue workgroups the device holds at once
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
     int64_t n_trees = 0, n_lblocks = 0;
     int red_threads = 64;
@@ -2886,6 +2996,20 @@ int launch_levels(Shard *f, const ggp_params &P)
         const int n = (int)(b - a);
         if (n <= 0) continue;
         HIPCHK(prof_begin());
+        if (f->lane_queue && f->qrun_at[L] >= 0) {   // levels la .. lb - 1 in one persistent launch
+            const Shard::QRun &R = f->qruns[(size_t)f->qrun_at[L]];
+            HIPCHK(hipMemsetAsync(f->d_qctr, 0, sizeof(unsigned), f->stream));
+            const int grid = (int)std::min<int64_t>(R.n, f->queue_resident);
+            hipLaunchKernelGGL(k_loglik_lane_queue, dim3(grid), dim3(64), 0, f->stream, f->F, P, f->d_level_cells,
+                               f->d_qchunks + R.off, (int)R.n, f->d_qctr, f->d_cell_done, f->epoch, f->spin_max,
+                               f->d_state, f->d_cell_ll, f->d_cell_nan);
+            HIPCHK(hipGetLastError());
+            f->kernel_used = GGP_KERNEL_LANE;
+            f->last_code = GGP_KERNEL_LANE << 8 | 2;
+            HIPCHK(prof_end(R.rows));
+            L = R.lb - 1;
+            continue;
+        }
         const int64_t n_simd = (int64_t)f->n_cu * 4;
         int kind = f->level_kind[L];
         if (kind == GGP_KERNEL_WAVE && risky) kind = n <= f->pair_max_cells ? GGP_KERNEL_PAIR : GGP_KERNEL_LANE;
@@ -3138,6 +3262,7 @@ void shard_destroy(Shard *f)
                     (void *)f->d_blk_sum, (void *)f->d_blk_nan, (void *)f->d_chain, (void *)f->d_cell_done,
                     (void *)f->d_path_cells, (void *)f->d_path_seq, (void *)f->d_path_blk,
                     (void *)f->d_blk_npaths, (void *)f->d_cnt_blk, (void *)f->d_pdesc,
+                    (void *)f->d_qchunks, (void *)f->d_qctr,
                     (void *)f->d_sm_ptab, (void *)f->d_sm_pstate, (void *)f->d_sm_comb})
         if (p) (void)hipFree(p);
     batch_free(f);
@@ -3247,6 +3372,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_JOINT_SLOT_MB")) f->joint_slot_bytes = (size_t)std::max(0, atoi(e)) << 20;
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
+    if (const char *e = getenv("GGP_LANE_QUEUE")) f->lane_queue = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL"); e && !ggp::kExact)
         f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
@@ -3489,6 +3615,38 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         check(dev_upload(&f->d_chain, ch.data(), nc));
         check(dev_upload<unsigned>(&f->d_cell_done, nullptr, nc));
         if (rc == GGP_OK && nc > 0 && hipMemset(f->d_cell_done, 0, (size_t)nc * sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
+        // lane queue runs: >= 2 consecutive levels the lane schedule takes, their cells in chunks of
+        // lane_cpw in level order; a chunk waits when its level is not the run's first and
+        // publishes when its level is not the run's last
+        f->qrun_at.assign(std::max(0, n_levels), -1);
+        if (f->lane_queue && f->n_paths == 0) {
+            std::vector<QChunk> qc;
+            const int cpw = lane_cpw(f);
+            for (int L = 0; L < n_levels;) {
+                int lb = L;
+                while (lb < n_levels && f->level_kind[lb] == GGP_KERNEL_LANE) ++lb;
+                if (lb - L >= 2) {
+                    Shard::QRun R{L, lb, (int64_t)qc.size(), 0, 0};
+                    for (int l = L; l < lb; ++l) {
+                        const int64_t a = f->level_start[l], b = f->level_start[l + 1];
+                        for (int64_t x = a; x < b; x += cpw)
+                            qc.push_back(QChunk{(int32_t)x, (int32_t)std::min<int64_t>(cpw, b - x), l > L ? 1 : 0,
+                                                l + 1 < lb ? 1 : 0});
+                    }
+                    R.n = (int64_t)qc.size() - R.off;
+                    f->qrun_at[L] = (int32_t)f->qruns.size();
+                    f->qruns.push_back(R);
+                }
+                L = std::max(lb, L + 1);
+            }
+            if (!qc.empty()) {
+                check(dev_upload(&f->d_qchunks, qc.data(), qc.size()));
+                check(dev_upload<unsigned>(&f->d_qctr, nullptr, 1));
+                int per_cu = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_lane_queue, 64, 0) == hipSuccess && per_cu > 0)
+                    f->queue_resident = per_cu * f->n_cu;
+            }
+        }
         if (rc != GGP_OK) {
             shard_destroy(f);
             return rc;
@@ -3501,6 +3659,8 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             int32_t c = level_cells[i];
             f->ev_rows[L] += d->row_offset[c + 1] - d->row_offset[c];
         }
+    for (auto &R : f->qruns)
+        for (int L = R.la; L < R.lb; ++L) R.rows += f->ev_rows[L];
     *out = f;
     return GGP_OK;
 }

@@ -149,6 +149,12 @@ GGP_DEV double exp_lane(const double x, bool &big)
 // process's libm).  x = k ln2/128 + r; exp(x) = 2^(k/128) (1 + tail) exp(r); tab = exp_table.inc
 // (LDS on the device: one 16-byte read per call).  |x| < 2^-54, |x| >= 512, inf and NaN take
 // glibc's special paths (exp_glibc_special).
+// Provenance and licence: the algorithm and the constants below are Szabolcs Nagy's exp from Arm's
+// optimized-routines (math/exp.c, math/exp_data.c; MIT OR Apache-2.0 WITH LLVM-exception), which
+// glibc ships as e_exp.c / e_exp_data.c (LGPL-2.1-or-later).  The code here is a restatement of
+// that published algorithm, not its source text; the 2^(k/128) table is computed by
+// tools/gen_exp_table.py (checked bitwise against this process's libm), and the eight constants
+// are the numeric values the bitwise result requires.
 constexpr double kGInvLn2N = 0x1.71547652b82fep0 * 128, kGShift = 0x1.8p52;
 constexpr double kGNegLn2hiN = -0x1.62e42fefa0000p-8, kGNegLn2loN = -0x1.cf79abc9e3b3ap-47;
 constexpr double kGC2 = 0x1.ffffffffffdbdp-2, kGC3 = 0x1.555555555543cp-3;

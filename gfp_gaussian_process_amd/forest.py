@@ -383,7 +383,7 @@ def kernel_name(code: int) -> str:
     """the HIP kernel symbol behind a launch-profile code (include/ggp.h)"""
     kind, lanes = code >> 8, code & 0xFF
     if kind == N.KERNELS["lane"]:
-        return "k_loglik_level"
+        return "k_loglik_lane_queue" if lanes == 2 else "k_loglik_level"
     if kind == N.KERNELS["wave"]:
         return "k_loglik_wave"
     if kind == N.KERNELS["pair"]:

@@ -237,7 +237,8 @@ int ggp_set_state(ggp_forest *f, const double *in);
 /* measurement hooks (bench.py): HIP-event timings of the launches of the last
  * ggp_total_loglik on the handle's stream.  ms[i], rows[i], kernel[i] for i < *n (cap
  * entries); kernel[i] = GGP_KERNEL_LANE << 8 | 1 or GGP_KERNEL_GROUP << 8 | G (lanes per
- * cell).  The first call only switches the events on (*n = 0); a call with cap < 0 switches them
+ * cell); GGP_KERNEL_LANE << 8 | 2 is one launch over a run of lane-schedule levels (the lane
+ * queue, rows = the run's rows).  The first call only switches the events on (*n = 0); a call with cap < 0 switches them
  * off again (*n = 0). */
 int ggp_last_launch_profile(ggp_forest *f, float *ms, int64_t *rows, int32_t *kernel, int32_t cap,
                             int32_t *n);

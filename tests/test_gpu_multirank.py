@@ -54,12 +54,15 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["config"]["rows_per_gpu"] == trees * rows
     # whole-job value: rows of both ranks over the max-over-ranks time of the K steps
     assert out["value"] == pytest.approx(2 * trees * rows / (out["ms_per_step"] * 1e-3), rel=1e-9)
-    # the gathered total after W + K chained calls: the rank-order sum of each rank's own chain
+    # the gathered total after the line's chained calls (W warm-up, the profiled window, W, the K
+    # steps): the rank-order sum of each rank's own chain
+    calls = out["chained_calls"]
+    assert calls >= 2 * warm + steps
     want = 0.0
     for rank in range(2):
         hf = g.HostForest.synthetic(trees, rows, seed=bench.SEED, first_tree=rank * trees)
         f = g.Forest(hf, device=0)
-        for _ in range(warm + steps):
+        for _ in range(calls):
             v = f.total_likelihood(bench.P_EXAMPLE)
         f.close()
         want = want + v
