@@ -1264,6 +1264,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 if (lane < W::kDtVals) lds[W::L_DTC + W::kDtVals * dt_victim + lane] = lds[dt_my_slot];
                 if (lane == 0) lds[W::L_DTK + dt_victim] = __longlong_as_double((long long)dbits);
                 dt_victim = (dt_victim + 1) & (W::kDtWays - 1);
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // (the derived values' table loads: none outlives the miss)
             }
             dt_cached = dbits;
         }
@@ -1372,7 +1373,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             scatter(m, C);
         }
         const bool divide = pending;
-        double t_cur = F.time[r0];
         prev_last = r1 - 1;
         GGP_PSTAMP(3);
         if (i == i_lo) GGP_TL(3);
@@ -1396,23 +1396,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         if (i != i_lo && !next_pre) load_chunk(r0);
         next_pre = false;
         wave_sync();
+        // the row time from LDS (no global load the step loop's waits would have to cover)
+        double t_cur = lds[W::L_ROWT];
         double cl = 0.0;
         int nan_row = kNanNone;
         int slot = 0;                    // row - chunk base
         const int nrows = (int)(r1 - r0);
-        int left = nrows;                // rows from the current one on
+        int left = nrows;                // rows from the chunk's first on (updated at each flush)
+        int slot_end = min(64, nrows);   // the chunk's rows: the step that fills them flushes
         bool live = !chain_broken;
         if (chain_broken) {
             cl = __longlong_as_double(0x7ff8000000000000LL);
             nan_row = kRowStall;
         }
-        // after a step: the ll ring is flushed every 64 rows (and at the cell's end), then the
-        // next chunk loaded.  false = stop (a NaN term; nan_row set)
-        auto end_step = [&]() -> bool {
-            ++slot;
-            --left;
+        // after the step whose row ends a chunk (slot == slot_end: 64 rows, or the cell's last): the
+        // ll ring is flushed, then the next chunk loaded (left, live: after this chunk).  false =
+        // stop (a NaN term; nan_row set)
+        auto flush = [&]() -> bool {
+            left -= slot;
             live = left > 0;
-            if (slot == 64 || !live) {
+            {
                 const int done = nrows - left;
                 const int64_t base = done - slot;
                 // the next chunk (this cell's, or the path's next cell's first) is loaded while the
@@ -1463,8 +1466,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     }
                     cl = acc;
                 }
+                // no global load outlives the flush, on either exit (s_waitcnt vmcnt(0)): the step
+                // loop then needs no vmcnt waits for the registers its loads wrote
+                __builtin_amdgcn_s_waitcnt(0x0F70);
                 if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) return false;
                 slot = 0;
+                slot_end = min(64, left);
                 if (nx) {
                     wave_sync();   // every lane has read this chunk's rows (lane 0's sum: the ll terms only)
                     lds[W::L_ROWL + lane] = na;
@@ -1475,8 +1482,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 next_pre = !live && c_nx >= 0;
                 GGP_TL_CNT(3, nx);
             }
-            GGP_STAMP(10);
-            wave_sync();   // the LDS slots are rewritten by the next step
             return true;
         };
         GGP_PSTAMP(4);
@@ -1515,43 +1520,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             if (pending) dt = t_next - t_cur;
             t_cur = t_next;
             GGP_STAMP_RESET();
-            if (!end_step()) live = false;
+            ++slot;
+            if (slot == slot_end && !flush()) live = false;
+            wave_sync();   // the LDS slots are rewritten by the next step
         }
         GGP_PSTAMP(5);
-        while (live) {   // steady steps: the state distributed over lanes 0-19
-            GGP_STAMP_STEP();
-            GGP_TL_CNT(0, true);
-            const double t_next = left > 1 ? lds[W::L_ROWT + slot + 1] : 0.0;
-            propagate(dt);
-            {
-                // every lane forms the innovation from the raw outputs (the values lanes 1, 4, 5, 9,
-                // 20, 24 finish: fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11), its loads issued
-                // with the finish's before any store
-                const double *o = lds + W::L_OUT;
-                const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
-                const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
-                lds[L.f_dst] = fv;
-                const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x, g_sc,
-                                                g_0, F.fp_auto);
-                if (lane == 0) {   // the ll term's inputs: the prior means (the flush forms m - y) and S
-                    lds[W::L_RX0 + slot] = o0;
-                    lds[W::L_RX1 + slot] = o1;
-                    lds[W::L_RS0 + slot] = v.S00;
-                    lds[W::L_RS1 + slot] = v.S01;
-                    lds[W::L_RS2 + slot] = v.S11;
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // (vmcnt(0): see the flush)
+        // steady steps, the state distributed over lanes 0-19: the chunk's rows [slot, slot_end) in
+        // a counted loop (one exit), then the flush; the row times from LDS in one read (ROWT[64]:
+        // the next chunk's first time; the next time is unused on the cell's last row)
+        while (live) {
+            for (;;) {
+                GGP_STAMP_STEP();
+                GGP_TL_CNT(0, true);
+                const double t_now = lds[W::L_ROWT + slot], t_next = lds[W::L_ROWT + slot + 1];
+                propagate(dt);
+                {
+                    // every lane forms the innovation from the raw outputs (the values lanes 1, 4, 5, 9,
+                    // 20, 24 finish: fma(-o0, o1, o5) = C01, fma(-o1, o1, o8) = C11), its loads issued
+                    // with the finish's before any store
+                    const double *o = lds + W::L_OUT;
+                    const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
+                    const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
+                    lds[L.f_dst] = fv;
+                    const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x,
+                                                  g_sc, g_0, F.fp_auto);
+                    if (lane == 0) {   // the ll term's inputs: the prior means (the flush forms m - y) and S
+                        lds[W::L_RX0 + slot] = o0;
+                        lds[W::L_RX1 + slot] = o1;
+                        lds[W::L_RS0 + slot] = v.S00;
+                        lds[W::L_RS1 + slot] = v.S01;
+                        lds[W::L_RS2 + slot] = v.S11;
+                    }
+                    GGP_STAMP(8);
+                    wave_sync();
+                    const W::UOps q = W::upost_load(L, lds);
+                    W::sched_fence();   // the operand reads issued before the update's arithmetic
+                    const double up = W::upost(q, fv, v);
+                    lds[L.u_post] = up;
+                    lds[L.u_v] = up - L.u_vshift;
                 }
-                GGP_STAMP(8);
-                wave_sync();
-                const W::UOps q = W::upost_load(L, lds);
-                W::sched_fence();   // the operand reads issued before the update's arithmetic
-                const double up = W::upost(q, fv, v);
-                lds[L.u_post] = up;
-                lds[L.u_v] = up - L.u_vshift;
+                GGP_STAMP(9);
+                dt = t_next - t_now;
+                if (++slot == slot_end) break;
+                GGP_STAMP(10);
+                wave_sync();   // the LDS slots are rewritten by the next step
             }
-            GGP_STAMP(9);
-            dt = t_next - t_cur;
-            t_cur = t_next;
-            if (!end_step()) break;
+            const bool stop = !flush() || !live;
+            GGP_STAMP(10);
+            wave_sync();
+            if (stop) break;
         }
         GGP_PSTAMP(6);
         GGP_TL(4);
