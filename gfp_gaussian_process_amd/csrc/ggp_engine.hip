@@ -1530,7 +1530,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         // a counted loop (one exit), then the flush; the row times from LDS in one read (ROWT[64]:
         // the next chunk's first time; the next time is unused on the cell's last row)
         while (live) {
-            for (;;) {
+            do {
+                wave_sync();   // the previous step's (or the flush's) LDS slots are complete
                 GGP_STAMP_STEP();
                 GGP_TL_CNT(0, true);
                 const double t_now = lds[W::L_ROWT + slot], t_next = lds[W::L_ROWT + slot + 1];
@@ -1545,7 +1546,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     lds[L.f_dst] = fv;
                     const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x,
                                                   g_sc, g_0, F.fp_auto);
-                    if (lane == 0) {   // the ll term's inputs: the prior means (the flush forms m - y) and S
+                    {   // the ll term's inputs: the prior means (the flush forms m - y) and S, the same
+                        // values from every lane to one address (no exec mask around the stores)
                         lds[W::L_RX0 + slot] = o0;
                         lds[W::L_RX1 + slot] = o1;
                         lds[W::L_RS0 + slot] = v.S00;
@@ -1562,10 +1564,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 }
                 GGP_STAMP(9);
                 dt = t_next - t_now;
-                if (++slot == slot_end) break;
                 GGP_STAMP(10);
-                wave_sync();   // the LDS slots are rewritten by the next step
-            }
+            } while (++slot != slot_end);
+            wave_sync();
             const bool stop = !flush() || !live;
             GGP_STAMP(10);
             wave_sync();
