@@ -1529,12 +1529,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         // steady steps, the state distributed over lanes 0-19: the chunk's rows [slot, slot_end) in
         // a counted loop (one exit), then the flush; the row times from LDS in one read (ROWT[64]:
         // the next chunk's first time; the next time is unused on the cell's last row)
+        // the row's slot as a byte offset in a vector register (sv = 8 slot): the slot-indexed LDS
+        // accesses of a step take it as their address, with the region in the offset field
+        auto at = [&](const int sv, const int region) -> double & {
+            return *reinterpret_cast<double *>(reinterpret_cast<char *>(lds + region) + sv);
+        };
         while (live) {
+            int sv;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(sv) : "s"(slot << 3));
             do {
                 wave_sync();   // the previous step's (or the flush's) LDS slots are complete
                 GGP_STAMP_STEP();
                 GGP_TL_CNT(0, true);
-                const double t_now = lds[W::L_ROWT + slot], t_next = lds[W::L_ROWT + slot + 1];
+                const double t_now = at(sv, W::L_ROWT), t_next = at(sv + 8, W::L_ROWT);
                 propagate(dt);
                 {
                     // every lane forms the innovation from the raw outputs (the values lanes 1, 4, 5, 9,
@@ -1542,17 +1549,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     // with the finish's before any store
                     const double *o = lds + W::L_OUT;
                     const double o0 = o[0], o1 = o[1], o4 = o[4], o5 = o[5], o8 = o[8];
-                    const double fv = W::finish(L, lds, slot);   // the prior's entries, -x0, -x1
+                    const double fv = W::finish_sv(L, lds, sv);   // the prior's entries, -x0, -x1
                     lds[L.f_dst] = fv;
                     const W::UInnov v = W::uinnov(o1, o4, __builtin_fma(-o0, o1, o5), __builtin_fma(-o1, o1, o8), var_x,
                                                   g_sc, g_0, F.fp_auto);
                     {   // the ll term's inputs: the prior means (the flush forms m - y) and S, the same
                         // values from every lane to one address (no exec mask around the stores)
-                        lds[W::L_RX0 + slot] = o0;
-                        lds[W::L_RX1 + slot] = o1;
-                        lds[W::L_RS0 + slot] = v.S00;
-                        lds[W::L_RS1 + slot] = v.S01;
-                        lds[W::L_RS2 + slot] = v.S11;
+                        at(sv, W::L_RX0) = o0;
+                        at(sv, W::L_RX1) = o1;
+                        at(sv, W::L_RS0) = v.S00;
+                        at(sv, W::L_RS1) = v.S01;
+                        at(sv, W::L_RS2) = v.S11;
                     }
                     GGP_STAMP(8);
                     wave_sync();
@@ -1565,6 +1572,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 GGP_STAMP(9);
                 dt = t_next - t_now;
                 GGP_STAMP(10);
+                sv += 8;
             } while (++slot != slot_end);
             wave_sync();
             const bool stop = !flush() || !live;

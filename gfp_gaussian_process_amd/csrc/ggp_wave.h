@@ -949,6 +949,12 @@ GGP_DEV double finish(const Lane &L, const double *lds, const int slot)
 {
     return __builtin_fma(-lds[L.f_na], lds[L.f_nb + mul24(slot, L.f_row)], lds[L.f_src]);   // f_row: 0 or 1
 }
+// the same with the row's slot as a byte offset held in a vector register (the step loop's sv)
+GGP_DEV double finish_sv(const Lane &L, const double *lds, const int sv)
+{
+    const double *row = reinterpret_cast<const double *>(reinterpret_cast<const char *>(lds + L.f_nb) + mul24(sv, L.f_row));
+    return __builtin_fma(-lds[L.f_na], *row, lds[L.f_src]);
+}
 
 struct UInnov {
     double S00, S01, S11, invdet;
