@@ -932,7 +932,12 @@ GGP_DEV double dpp_f64(const double v)
 // A wait that exceeds spin_max polls ends as a stall (GGP_ETIMEOUT), never as a hang or a model
 // NaN; ggp_total_loglik_chain then finishes the remaining points call by call from the last
 // completed point's state, and the -m lookahead evaluates a stalled node's call normally.
-// chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c}.
+// chain[c] = {parent to wait for or -1, 1 if a second daughter waits for c, the division's dt}.
+struct CellLink {
+    int32_t x, y;   // a second daughter's parent to wait for (or -1); 1: a second daughter waits for c
+    double dt;      // a daughter's division dt, time[its first row] - time[the parent's last row]
+                    // (the same subtraction the step would make: bitwise), 0 for a root
+};
 constexpr unsigned kChainSpinMax = 1u << 24;   // ~20 s of polling (GGP_CHAIN_SPIN_MAX)
 // rows of chained roots one chained launch may hold (~1 us per row: a few seconds, against the
 // ~20 s a wait may take before it counts as a stall)
@@ -957,6 +962,7 @@ struct PathDesc {
     int32_t i_lo, i_hi, c0, j;    // the path's cells [i_lo, i_hi) of path_cells, its first cell, its block
     int32_t npaths, nb, t0, pad;  // the block's path count, tree count and first tree
     int64_t r0, r1;               // the first cell's rows
+    CellLink l0;                  // the first cell's chain entry
 };
 
 struct ChainRed {
@@ -1133,7 +1139,7 @@ GGP_DEV void wave_sync()
 template <bool CHAIN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
-    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const int2 *__restrict__ chain, unsigned *cell_done,
+    double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const CellLink *__restrict__ chain, unsigned *cell_done,
     const unsigned epoch, const int32_t *__restrict__ seq, const ChainRed red, const int64_t call_seq,
     const unsigned spin_max, const double *__restrict__ ptab, const double *__restrict__ carry,
     const int32_t *__restrict__ pt_pred)
@@ -1225,7 +1231,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     int dt_victim = 0;
     const int dt_my_slot = W::dt_slot(lane < W::kDtVals ? lane : 0);
     GGP_STAMP_DECL;
-    int64_t prev_last = -1;
     // the cell's first state into POST (lanes' entries) and V (stage D's variables), from registers
     // holding the same values in every lane (once per cell)
     auto scatter = [&](const double *m, const double *C) {
@@ -1301,13 +1306,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         wave_sync();
     };
     bool next_pre = false;   // the previous cell's last flush loaded this cell's first chunk
+    // the cell, its chain entry and rows, loaded while the previous cell ran (the path's first
+    // cell: from its descriptor), so a cell starts without a chain of dependent loads
+    int c_cur = pd ? pd->c0 : cells[i_lo];
+    CellLink ch_cur = pd ? pd->l0 : chain[c_cur];
+    int64_t r0_cur = pd ? pd->r0 : F.row_off[c_cur], r1_cur = pd ? pd->r1 : F.row_off[c_cur + 1];
     for (int i = i_lo; i < i_hi; ++i) {
-        const int c = cells[i];
-        const int2 ch = chain[c];
+        const int c = c_cur;
+        const CellLink ch = ch_cur;
         bool chain_broken = false;
         // the path's next cell: its first chunk is loaded during this cell's last flush
         const int c_nx = i + 1 < i_hi ? cells[i + 1] : -1;
         const int64_t r0n = c_nx >= 0 ? F.row_off[c_nx] : 0, r1n = c_nx >= 0 ? F.row_off[c_nx + 1] : 0;
+        const CellLink ch_nx = c_nx >= 0 ? chain[c_nx] : CellLink{-1, 0, 0.0};
         // the cell to wait for: a second daughter's parent; in a chain also a root's own state at
         // the end of the previous point (its carried state)
         int wc = ch.x;
@@ -1336,7 +1347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                     chain_broken = true;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(2)   /* short: the poll's own load is most of an iteration */;
             }
         }
         // a root whose predecessor point's root stalled stalls too (its state would be that
@@ -1345,12 +1356,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             ld_agent_i(cell_nan + (wdone - cell_done) + F.dfs_rank[c]) == kRowStall)
             chain_broken = true;
         if (i == i_lo && wc >= 0) GGP_TL_SEEN(0);
-        const int64_t r0 = F.row_off[c], r1 = F.row_off[c + 1];
+        const int64_t r0 = r0_cur, r1 = r1_cur;
+        c_cur = c_nx;   // the next iteration's cell
+        ch_cur = ch_nx;
+        r0_cur = r0n;
+        r1_cur = r1n;
         double dt = 0.0;
         bool pending;
         if (i > i_lo) {   // the first daughter of the previous cell: its posterior is in POST / V
             pending = true;
-            dt = F.time[r0] - F.time[prev_last];
+            dt = ch.dt;
         } else if (ch.x >= 0) {   // a second daughter of a cell in another path: lane e takes entry e
             if (lane < 20) {
                 const double v = ld_agent(state + (size_t)20 * ch.x + lane);
@@ -1358,7 +1373,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 lds[L.u_v] = v - L.u_vshift;
             }
             pending = true;
-            dt = F.time[r0] - F.time[F.row_off[ch.x + 1] - 1];
+            dt = ch.dt;
         } else {
             double m[4], C[16];
             if (CHAIN && carried_prev) {   // a root: the previous point's final state of it (coherent loads)
@@ -1373,7 +1388,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             scatter(m, C);
         }
         const bool divide = pending;
-        prev_last = r1 - 1;
         GGP_PSTAMP(3);
         if (i == i_lo) GGP_TL(3);
         if (i == i_lo && ch.x >= 0) GGP_TL_SEEN(1);
@@ -2784,7 +2798,7 @@ struct Shard {
     int32_t *d_cell_nan = nullptr;
     // chained wave launches (k_loglik_wave): per cell {parent to wait for, has a waiting daughter},
     // done flags holding the epoch of the evaluation that finished the cell
-    int2 *d_chain = nullptr;
+    CellLink *d_chain = nullptr;
     unsigned *d_cell_done = nullptr;
     unsigned epoch = 0;
     int wave_resident = 2048;          // k_loglik_wave blocks the device holds at once
@@ -3551,7 +3565,9 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_loglik_wave<false>, 64, 0) == hipSuccess && per_cu > 0)
             f->wave_resident = per_cu * f->n_cu;
         if (const char *e = getenv("GGP_WAVE_PATHS_MAX")) f->wave_resident = atoi(e);
-        std::vector<int2> ch(nc, int2{-1, 0});
+        std::vector<CellLink> ch(nc, CellLink{-1, 0, 0.0});
+        for (int64_t c = 0; c < nc; ++c)   // the division dt of every daughter (the step's own subtraction)
+            if (d->parent[c] >= 0) ch[c].dt = d->time[d->row_offset[c]] - d->time[d->row_offset[d->parent[c] + 1] - 1];
         std::vector<int32_t> heads, pcells, pseq;
         auto next_of = [&](int32_t c) { return d->daughter1[c] >= 0 ? d->daughter1[c] : d->daughter2[c]; };
         if (all_wave) {
@@ -3615,6 +3631,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
                     P.pad = 0;
                     P.r0 = d->row_offset[P.c0];
                     P.r1 = d->row_offset[P.c0 + 1];
+                    P.l0 = ch[(size_t)P.c0];
                 }
                 check(dev_upload(&f->d_pdesc, pdv.data(), pdv.size()));
             }
