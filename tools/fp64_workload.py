@@ -19,6 +19,9 @@ P = [2.31e-03, 4.36e-02, 9.75e-08, 9.03e+01, 1.60e-02, 1.94e+01, 4.95e-04, 3.35e
 out = {}
 for name, trees, kernel in (("wave", 1000, "auto"), ("lane", 1024, "lane")):
     hf = g.HostForest.synthetic(trees, 200)
+    # the lane figure is one lane running whole updates: the level launches (k_loglik_level), not
+    # the lane queue, whose waiting chunks would add their polls to the counts
+    os.environ["GGP_LANE_QUEUE"] = "0" if name == "lane" else "1"
     f = g.Forest(hf, kernel=kernel)
     for _ in range(3):
         f.total_likelihood(P)
