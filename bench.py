@@ -490,7 +490,14 @@ def main() -> int:
             acc[1] += rows
             acc[2] += 1
     fg.disable_profile()
-    for _ in range(args.warmup):
+    # the profiled window synchronised on the stream, so the host thread slept between its calls;
+    # the same number of calls on every rank (each is a collective at N > 1), at least 300 of them
+    # (~50 ms of spin-waited calls), bring the host's enqueue back to its steady cost before the
+    # timed steps: with only W = 5 the timed steps' median enqueue was 5.9 us against 2.9 us
+    # (profiles/r6h_bench.json against profiles/r6g_bench.json), with 100 settling calls 4.1 us
+    # (profiles/r6i_bench_driver_cmd.txt)
+    n_settle = max(args.warmup, 300)
+    for _ in range(n_settle):
         obj.total_likelihood(P_EXAMPLE)
 
     # ---- timed region: exactly K steps (each step's wall time kept: the line's `steps_us`; the
@@ -942,8 +949,8 @@ def main() -> int:
             },
             "fp64": fp64,
             "total_log_likelihood": ll,
-            # the chained calls behind that total: W warm-up, the profiled window, W, then the K steps
-            "chained_calls": 2 * args.warmup + n_prof + args.steps,
+            # the chained calls behind that total: W warm-up, the profiled window, the settling calls, the K steps
+            "chained_calls": args.warmup + n_prof + n_settle + args.steps,
             "steps_us": steps_us,
             "clock": None if clock_timed is None else {
                 "shader_mhz_last_timed_launch": clock_timed[0], "window_us": clock_timed[1],
