@@ -54,8 +54,8 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["config"]["rows_per_gpu"] == trees * rows
     # whole-job value: rows of both ranks over the max-over-ranks time of the K steps
     assert out["value"] == pytest.approx(2 * trees * rows / (out["ms_per_step"] * 1e-3), rel=1e-9)
-    # the gathered total after the line's chained calls (W warm-up, the profiled window, W, the K
-    # steps): the rank-order sum of each rank's own chain
+    # the gathered total after the line's chained calls (W warm-up, the profiled window, the settling
+    # calls, the K steps): the rank-order sum of each rank's own chain
     calls = out["chained_calls"]
     assert calls >= 2 * warm + steps
     want = 0.0
