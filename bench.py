@@ -497,12 +497,6 @@ def main() -> int:
     # (profiles/r6h_bench.json against profiles/r6g_bench.json), with 100 settling calls 4.1 us
     # (profiles/r6i_bench_driver_cmd.txt)
     n_settle = max(args.warmup, 300)
-    # the calling thread on one CPU of the process's set from here through the timed steps (rank r:
-    # the r-th; no migration between cores mid-run), the full set restored after them
-    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") and \
-        os.environ.get("GGP_BENCH_PIN", "1") != "0" else []
-    if cpus:
-        os.sched_setaffinity(0, {cpus[local % len(cpus)]})
     for _ in range(n_settle):
         obj.total_likelihood(P_EXAMPLE)
 
@@ -520,8 +514,6 @@ def main() -> int:
     barrier()
     el = time.perf_counter() - t0
     gc.enable()
-    if cpus:
-        os.sched_setaffinity(0, set(cpus))
     clock_timed = fg.launch_clock()   # the last timed launch's shader clock (wave schedule only)
     steps_us = host_split(step_t, fg.call_trace(args.steps) if hasattr(fg, "call_trace") else None)
     if world > 1:
