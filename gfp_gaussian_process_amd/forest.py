@@ -428,8 +428,10 @@ class Forest:
         self.n_cells = host_forest.n_cells
         # the per-call argument objects, made once (an evaluation is ~0.3 ms: ~5 us of ctypes
         # object creation per call showed up in the C2 rate)
-        self._p = np.zeros(N.N_PARAMS)
-        self._p_ptr = self._p.ctypes.data_as(N.c_double_p)
+        # the call's parameters: a ctypes array (a slice assignment from a list costs half a
+        # numpy array's) and its pointer, made once
+        self._p = (ctypes.c_double * N.N_PARAMS)()
+        self._p_ptr = ctypes.cast(self._p, N.c_double_p)
         self._ll, self._nc, self._nr = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
         self._out_refs = (ctypes.byref(self._ll), ctypes.byref(self._nc), ctypes.byref(self._nr))
 
@@ -459,9 +461,7 @@ class Forest:
 
     def total_likelihood(self, params) -> float:
         try:
-            if len(params) != N.N_PARAMS:
-                raise ValueError
-            self._p[:] = params
+            self._p[:] = params   # (ctypes: ValueError unless exactly N_PARAMS values)
         except (TypeError, ValueError):
             raise ValueError("params must hold 11 values (Parameters.h:175 order)") from None
         self._usable()

@@ -1074,3 +1074,21 @@ def test_predict_many_segments_parameter_rows_from_global(monkeypatch):
         em, ec = _smoother_err(x, y)
         print(f"PRED_ERR 40 segments {name} mean {em:.3e} cov {ec:.3e}")
         assert em < PRED_TOL and ec < PRED_TOL, (name, em, ec)
+
+
+def test_total_likelihood_parameter_forms(example_forests):
+    """the 11 parameters as a list, a tuple or a numpy array give the same bits; any other count,
+    or a non-number, is a ValueError before anything runs (the carried state is untouched)"""
+    import gfp_gaussian_process_amd as g
+    hf = example_forests[("scaled", "binomial")]
+    P = CONFIGS[0][2]
+    vals = []
+    for form in (list(P), tuple(P), np.asarray(P)):
+        f = g.Forest(hf)
+        vals.append(f.total_likelihood(form))
+    assert vals[0] == vals[1] == vals[2]
+    f = g.Forest(hf)
+    for bad in (P[:10], list(P) + [1.0], [None] * 11, "abcdefghijk"):
+        with pytest.raises(ValueError):
+            f.total_likelihood(bad)
+    assert f.total_likelihood(P) == vals[0]   # the failed calls ran nothing: still the first call
