@@ -977,6 +977,7 @@ struct ArmHost {                  // mapped host memory: written by the host, re
     int64_t door;                 // k: call k's parameters are in place; -k: call k will not come
     double params[11];
     int64_t expired;              // k: the launch armed for call k expired before its door rang
+    uint64_t st[4];               // block 0 (100 MHz counter): entry, poll start, door seen, slots written
 };
 struct ArmDev {                   // device memory: block 0 -> the other blocks
     int64_t go;                   // k: parameters of call k below; -k: exit
@@ -1157,17 +1158,20 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
 // the evaluation has started, the block exits)
 GGP_DEV bool arm_wait(const ChainRed &R, const int64_t k, const int lane, ggp_params &P)
 {
-    // every poll is a relaxed load (no cache invalidation per poll), the acquire fence once it matched;
-    // block b polls slot b % kArmSlots: one flag polled by every block queued the polls on one memory
-    // channel, ~0.08 us per block before the last block saw it (2000 blocks: 170 us)
+    // every poll is a relaxed load (no cache invalidation); block b polls slot b % kArmSlots: one
+    // flag polled by every block queued the polls on one memory channel, ~0.08 us per block before
+    // the last block saw it (2000 blocks: 170 us)
     long long got = 0;
     if (blockIdx.x == 0) {
         if (lane == 0) {
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(&arm_host_of(R)->st[1], (uint64_t)t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             for (;;) {
                 const long long d = __hip_atomic_load(&arm_host_of(R)->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (d == k || d == -k) {
                     got = d;
+                    __hip_atomic_store(&arm_host_of(R)->st[2], (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kArmTicks) {
@@ -1180,20 +1184,27 @@ GGP_DEV bool arm_wait(const ChainRed &R, const int64_t k, const int lane, ggp_pa
         }
         got = ((long long)__builtin_amdgcn_readfirstlane((int)(got >> 32)) << 32) |
               (unsigned)__builtin_amdgcn_readfirstlane((int)(got & 0xffffffff));
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the parameters written before the door
-        // lane i fills slot i: the parameters (read by every lane from the door's page), then its go
+        // the parameters in one load (lane i < 11: parameter i), issued after the door's value came
+        // back: the host wrote them before the door, and the loads bypass every cache (one PCIe round
+        // trip instead of eleven serialised ones; no cache invalidation)
         ArmDev *slot = arm_dev_of(R, lane);
         if (got == k) {
+            unsigned long long v = 0;
+            if (lane < 11)
+                v = __hip_atomic_load(reinterpret_cast<unsigned long long *>(arm_host_of(R)->params + lane), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
             for (int i = 0; i < 11; ++i) {
-                const long long v = (long long)__hip_atomic_load(
-                    reinterpret_cast<unsigned long long *>(arm_host_of(R)->params + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                st_agent(slot->params + i, __longlong_as_double(v));
-                P.p[i] = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-                                              (unsigned)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffff)));
+                const long long u = ((long long)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+                                    (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i);
+                P.p[i] = __longlong_as_double(u);
+                st_agent(slot->params + i, P.p[i]);   // lane j fills slot j
             }
         }
         __hip_atomic_store(&slot->go, (int64_t)got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store(&arm_host_of(R)->st[3], (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         return got == k;
     }
     const ArmDev *slot = arm_dev_of(R, blockIdx.x % kArmSlots);
@@ -1215,14 +1226,16 @@ GGP_DEV bool arm_wait(const ChainRed &R, const int64_t k, const int lane, ggp_pa
     const long long g = ((long long)__builtin_amdgcn_readfirstlane((int)(got >> 32)) << 32) |
                         (unsigned)__builtin_amdgcn_readfirstlane((int)(got & 0xffffffff));
     if (g != k) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the slot's parameters written before its go
+    // the slot's parameters (written before its go, release) in one agent-coherent load issued after
+    // go's value came back (lane i < 11: parameter i), then wave-uniform registers
+    unsigned long long v = 0;
+    if (lane < 11)
+        v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(slot->params + lane), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int i = 0; i < 11; ++i) {   // agent-coherent loads, then wave-uniform registers
-        const long long v = (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(slot->params + i),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        P.p[i] = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-                                      (unsigned)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffff)));
-    }
+    for (int i = 0; i < 11; ++i)
+        P.p[i] = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+                                      (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i));
     return true;
 }
 
@@ -1315,6 +1328,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // an armed launch: that setup first, then the wait for its call's parameters, then the rest
     constexpr bool armed = !CHAIN && ARMED;
     if constexpr (armed) {
+        if (blockIdx.x == 0 && lane == 0)
+            __hip_atomic_store(&arm_host_of(red)->st[0], (uint64_t)clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         GGP_WAVE_SETUP_LDS();
         if (!arm_wait(red, call_seq, lane, P)) return;   // no evaluation ran: nothing is written
         clk_c0 = __builtin_amdgcn_s_memtime();            // the evaluation's window starts now
@@ -2949,7 +2964,9 @@ struct Shard {
     bool arm_call = false;             // the pending call went through the door
     ggp_params arm_params{};           // its parameters (a plain launch of them after an expiry)
     volatile ArmHost *h_arm = nullptr;
+    bool arm_debug = false;
     int64_t arm_calls = 0;        // calls that ran in an armed launch (ggp_arm)
+    double arm_dbg[5] = {0, 0, 0, 0, 0};   // GGP_ARM_DEBUG: summed block-0 stamp differences (us), calls
     int queue_resident = 1024;         // k_loglik_lane_queue workgroups the device holds at once
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
     int64_t n_trees = 0, n_lblocks = 0;
@@ -3352,7 +3369,18 @@ int shard_wait(Shard *s)
             for (int k = 0; k < 4; ++k) s->clk_snap[k] = s->h_clk[k];
     }
     s->seq_pending = false;
-    if (s->arm_call && seen) ++s->arm_calls;
+    if (s->arm_call && seen) {
+        ++s->arm_calls;
+        if (s->arm_debug) {   // entry -> poll, poll -> door, door -> slots, door -> the end (100 MHz)
+            const uint64_t e0 = s->h_arm->st[0], e1 = s->h_arm->st[1], e2 = s->h_arm->st[2], e3 = s->h_arm->st[3];
+            const uint64_t ee = s->h_clk[3];
+            s->arm_dbg[0] += (e1 - e0) / 100.0;
+            s->arm_dbg[1] += (e2 - e1) / 100.0;
+            s->arm_dbg[2] += (e3 - e2) / 100.0;
+            s->arm_dbg[3] += (ee - e2) / 100.0;
+            s->arm_dbg[4] += 1;
+        }
+    }
     s->arm_call = false;
     if (!seen || s->profile) {
         arm_quit(s);
@@ -3615,6 +3643,7 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_QUEUE")) f->lane_queue = atoi(e) != 0;
     if (const char *e = getenv("GGP_ARM")) f->arm = atoi(e) != 0;
+    if (const char *e = getenv("GGP_ARM_DEBUG")) f->arm_debug = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL"); e && !ggp::kExact)
         f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
@@ -4825,6 +4854,13 @@ int ggp_arm(ggp_forest *f, int32_t on, int64_t *armed_calls)
         arm_quit_all(f);
         for (Shard *s : f->shards) s->arm = on != 0;
     }
+    for (Shard *s : f->shards)
+        if (s->arm_debug && s->arm_dbg[4] > 0) {
+            const double n = s->arm_dbg[4];
+            fprintf(stderr, "ggp arm: %.0f calls, block 0 mean us: entry->poll %.2f poll->door %.2f door->slots %.2f door->end %.2f\n",
+                    n, s->arm_dbg[0] / n, s->arm_dbg[1] / n, s->arm_dbg[2] / n, s->arm_dbg[3] / n);
+            for (double &v : s->arm_dbg) v = 0;
+        }
     if (armed_calls) {
         int64_t n = 0;
         for (const Shard *s : f->shards) n += s->arm_calls;
