@@ -330,7 +330,6 @@ def main() -> int:
     ap.add_argument("--trees", type=int, default=1000, help="trees per GPU")
     ap.add_argument("--rows", type=int, default=200, help="rows per tree")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "group", "wave", "pair"])
-    ap.add_argument("--arm", type=int, default=0, help="armed objective calls at N = 1 (ggp_arm; 0 = plain launches)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle work (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--large-trees", type=int, default=12500,
@@ -498,18 +497,8 @@ def main() -> int:
     # (profiles/r6h_bench.json against profiles/r6g_bench.json), with 100 settling calls 4.1 us
     # (profiles/r6i_bench_driver_cmd.txt)
     n_settle = max(args.warmup, 300)
-    # armed calls (ggp_arm, N = 1 only: at N > 1 the call's exchange follows the evaluation): each
-    # call enqueues the next call's launch, which stages its tables and waits for the parameters, so
-    # the launch's enqueue, dispatch and setup overlap the previous call (DESIGN.md "Armed calls")
-    arm = world == 1 and bool(args.arm)
-    if arm:
-        fg.arm(True)
     for _ in range(n_settle):
         obj.total_likelihood(P_EXAMPLE)
-    if arm:
-        # the settling calls' waiting launch leaves (the barrier's device synchronisation would wait
-        # for it); the first timed call is a plain launch and arms the second
-        armed0 = fg.arm(True)
 
     # ---- timed region: exactly K steps (each step's wall time kept: the line's `steps_us`; the
     # collector paused so no collection lands inside a step) ----
@@ -522,8 +511,6 @@ def main() -> int:
     for k in range(args.steps):
         ll = obj.total_likelihood(P_EXAMPLE)
         step_t[k + 1] = time.perf_counter()
-    if arm:
-        armed_timed = fg.arm(False) - armed0   # the last call's waiting launch leaves (timed)
     barrier()
     el = time.perf_counter() - t0
     gc.enable()
@@ -965,8 +952,6 @@ def main() -> int:
             # the chained calls behind that total: W warm-up, the profiled window, the settling calls, the K steps
             "chained_calls": args.warmup + n_prof + n_settle + args.steps,
             "steps_us": steps_us,
-            # of the K timed calls, those run in an armed launch (the first is a plain launch)
-            "armed_calls": armed_timed if arm else None,
             "clock": None if clock_timed is None else {
                 "shader_mhz_last_timed_launch": clock_timed[0], "window_us": clock_timed[1],
                 "shader_mhz_profiled_launches": clocks,

@@ -93,7 +93,6 @@ ENGINE_SYMBOLS = {
     "ggp_comm_nan_rank": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_comm_size": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_launch_clock": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
-    "ggp_arm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "ggp_call_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, c_double_p, ctypes.POINTER(ctypes.c_int32)]),
     "ggp_comm_local_nan": (ctypes.c_int32, [ctypes.c_void_p]),
     "ggp_device_count": (ctypes.c_int, [c_int32_p]),

@@ -965,26 +965,6 @@ struct PathDesc {
     CellLink l0;                  // the first cell's chain entry
 };
 
-// An armed path launch (GGP_ARM=1, a single-shard path-launch handle): the next call's kernel is
-// enqueued behind the current one; it stages the call-independent tables (the Dawson/exp table,
-// the first chunk's rows, the reduction's tables) and then waits for its call's parameters, which
-// ggp_total_loglik_async writes into mapped host memory before ringing the door.  Block 0 watches
-// the door and hands the parameters to the other blocks through device memory.  Every wait is
-// bounded: without its call within kArmTicks the launch marks itself expired and exits (no
-// evaluation ran), and the host then runs that call as a plain launch; the host's -k makes it exit
-// at once (another entry point needs the stream).
-struct ArmHost {                  // mapped host memory: written by the host, read by block 0
-    int64_t door;                 // k: call k's parameters are in place; -k: call k will not come
-    double params[11];
-    int64_t expired;              // k: the launch armed for call k expired before its door rang
-    uint64_t st[4];               // block 0 (100 MHz counter): entry, poll start, door seen, slots written
-};
-struct ArmDev {                   // device memory: block 0 -> the other blocks
-    int64_t go;                   // k: parameters of call k below; -k: exit
-    double params[11];
-};
-constexpr unsigned long long kArmTicks = 5000000ull;   // 50 ms of the 100 MHz counter
-
 struct ChainRed {
     const PathDesc *pdesc;        // per path (nullptr: the tables below / the level launch's cells)
     const int32_t *path_blk;      // local block of each path
@@ -997,22 +977,8 @@ struct ChainRed {
     long long *host_nan;
     int n_lblocks;                // 0: no in-launch reduction
     unsigned long long *clk;      // mapped: block 0's shader-clock and 100 MHz ticks over its path, its
-                                  // start (100 MHz counter), the publishing block's end (ggp_call_trace);
-                                  // an ArmHost follows at clk + kArmHostOff (armed launches)
+                                  // start (100 MHz counter), the publishing block's end (ggp_call_trace)
 };
-// where an armed launch finds its door and its device slot without kernel arguments of their own
-// (the kernel's scalar registers are fully used: more arguments move spills into the step loop)
-constexpr int kArmHostOff = 8;    // u64 slots after clk (clk[0..3], then padding to 64 bytes)
-constexpr int kArmDevOff = 256;   // bytes after the in-launch reduction's done counter
-constexpr int kArmSlots = 64;     // ArmDev slots (one per lane of block 0), each on its own page
-constexpr int kArmSlotStride = 4352;   // bytes: 4 KiB + 256, so the slots fall on different channels
-constexpr int kArmHostSlots = 8 + (int)(sizeof(ArmHost) / 8) + 2;   // u64 slots from clk on
-GGP_DEV ArmHost *arm_host_of(const ChainRed &R) { return reinterpret_cast<ArmHost *>(R.clk + kArmHostOff); }
-GGP_DEV ArmDev *arm_dev_of(const ChainRed &R, int i)
-{
-    return reinterpret_cast<ArmDev *>(reinterpret_cast<char *>(R.done) + kArmDevOff + (size_t)i * kArmSlotStride);
-}
-constexpr size_t kDoneBytes = kArmDevOff + (size_t)kArmSlots * kArmSlotStride;   // the done allocation
 constexpr long long kChainNoNan = 0x7fffffffffffffffLL;
 
 
@@ -1153,92 +1119,6 @@ GGP_DEV void chain_reduce(const ChainRed &R, const RedPre &q, const int64_t seq,
     if (R.clk) __hip_atomic_store(R.clk + 3, t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// an armed launch's wait for its call (every lane of every block calls it): true with P holding call
-// k's parameters, false when call k will not come (the host's -k, or the launch expired: nothing of
-// the evaluation has started, the block exits)
-GGP_DEV bool arm_wait(const ChainRed &R, const int64_t k, const int lane, ggp_params &P)
-{
-    // every poll is a relaxed load (no cache invalidation); block b polls slot b % kArmSlots: one
-    // flag polled by every block queued the polls on one memory channel, ~0.08 us per block before
-    // the last block saw it (2000 blocks: 170 us)
-    long long got = 0;
-    if (blockIdx.x == 0) {
-        if (lane == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            __hip_atomic_store(&arm_host_of(R)->st[1], (uint64_t)t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            for (;;) {
-                const long long d = __hip_atomic_load(&arm_host_of(R)->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (d == k || d == -k) {
-                    got = d;
-                    __hip_atomic_store(&arm_host_of(R)->st[2], (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kArmTicks) {
-                    __hip_atomic_store(&arm_host_of(R)->expired, (int64_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    got = -k;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        got = ((long long)__builtin_amdgcn_readfirstlane((int)(got >> 32)) << 32) |
-              (unsigned)__builtin_amdgcn_readfirstlane((int)(got & 0xffffffff));
-        // the parameters in one load (lane i < 11: parameter i), issued after the door's value came
-        // back: the host wrote them before the door, and the loads bypass every cache (one PCIe round
-        // trip instead of eleven serialised ones; no cache invalidation)
-        ArmDev *slot = arm_dev_of(R, lane);
-        if (got == k) {
-            unsigned long long v = 0;
-            if (lane < 11)
-                v = __hip_atomic_load(reinterpret_cast<unsigned long long *>(arm_host_of(R)->params + lane), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-            for (int i = 0; i < 11; ++i) {
-                const long long u = ((long long)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
-                                    (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i);
-                P.p[i] = __longlong_as_double(u);
-                st_agent(slot->params + i, P.p[i]);   // lane j fills slot j
-            }
-        }
-        __hip_atomic_store(&slot->go, (int64_t)got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0)
-            __hip_atomic_store(&arm_host_of(R)->st[3], (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        return got == k;
-    }
-    const ArmDev *slot = arm_dev_of(R, blockIdx.x % kArmSlots);
-    if (lane == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
-            const long long g = __hip_atomic_load(&slot->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (g == k || g == -k) {
-                got = g;
-                break;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kArmTicks + kArmTicks / 2) {   // block 0 is gone
-                got = -k;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    const long long g = ((long long)__builtin_amdgcn_readfirstlane((int)(got >> 32)) << 32) |
-                        (unsigned)__builtin_amdgcn_readfirstlane((int)(got & 0xffffffff));
-    if (g != k) return false;
-    // the slot's parameters (written before its go, release) in one agent-coherent load issued after
-    // go's value came back (lane i < 11: parameter i), then wave-uniform registers
-    unsigned long long v = 0;
-    if (lane < 11)
-        v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(slot->params + lane), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int i = 0; i < 11; ++i)
-        P.p[i] = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
-                                      (unsigned)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i));
-    return true;
-}
-
 // ------------------------------------------------------------------------------------------
 // k_loglik_wave: the wave schedule.  Path launch: seq != nullptr, block b runs the path
 // cells[seq[b] .. seq[b+1]) and the sum is formed in-launch (red); level launch: one cell per
@@ -1256,7 +1136,7 @@ GGP_DEV void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool CHAIN, bool ARMED = false>
+template <bool CHAIN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_loglik_wave(
     DevForest F, ggp_params P, const int32_t *__restrict__ cells, int n, double *__restrict__ state,
     double *__restrict__ cell_ll, int32_t *__restrict__ cell_nan, const CellLink *__restrict__ chain, unsigned *cell_done,
@@ -1270,7 +1150,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int lane = threadIdx.x;
     // the launch's shader clock (ggp_launch_clock): block 0 reads the shader-clock counter and the
     // constant 100 MHz counter at its start and after its path (two scalar reads each)
-    unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     GGP_PSTAMP_DECL;
     GGP_PSTAMP(0);
     GGP_TL(0);
@@ -1313,33 +1193,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         cell_done += (size_t)n * pt;
     }
     const W::LaneC LC = W::unpack_lane(W::kLanePTab.l[lane]);   // this lane's row of the compile-time table (packed)
-    // the launch's call-independent setup into LDS: the table, the reduction's tables, the first
-    // chunk (a macro, not a lambda: a captured register array would be given a stack slot)
-#define GGP_WAVE_SETUP_LDS()                                                                        \
-    do {                                                                                            \
-        _Pragma("unroll") for (int j = 0; j < kTabR; ++j) if (lane + 64 * j < kTabN2)               \
-            reinterpret_cast<double2 *>(lds + W::L_TAB)[lane + 64 * j] = tab_v[j];                  \
-        if (red.n_lblocks > 0) red_park(rq0, lds + W::L_RED, lane);                                 \
-        lds[W::L_ROWL + lane] = pre_l; /* the first cell's chunk (its iteration loads no rows) */  \
-        lds[W::L_ROWF + lane] = pre_f;                                                              \
-        lds[W::L_ROWT + lane] = pre_t;                                                              \
-        if (lane == 0) lds[W::L_ROWT + 64] = pre_t64;                                               \
-    } while (0)
-    // an armed launch: that setup first, then the wait for its call's parameters, then the rest
-    constexpr bool armed = !CHAIN && ARMED;
-    if constexpr (armed) {
-        if (blockIdx.x == 0 && lane == 0)
-            __hip_atomic_store(&arm_host_of(red)->st[0], (uint64_t)clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        GGP_WAVE_SETUP_LDS();
-        if (!arm_wait(red, call_seq, lane, P)) return;   // no evaluation ran: nothing is written
-        clk_c0 = __builtin_amdgcn_s_memtime();            // the evaluation's window starts now
-        clk_r0 = __builtin_amdgcn_s_memrealtime();
-    }
     W::Lane L;
     {
         const ggp::OU ou = ggp::make_ou(p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
         const double kap = W::lane_kappa(lane, ou);
-        if constexpr (!armed) GGP_WAVE_SETUP_LDS();
+#pragma unroll
+        for (int j = 0; j < kTabR; ++j)
+            if (lane + 64 * j < kTabN2) reinterpret_cast<double2 *>(lds + W::L_TAB)[lane + 64 * j] = tab_v[j];
+        if (red.n_lblocks > 0) red_park(rq0, lds + W::L_RED, lane);
+        lds[W::L_ROWL + lane] = pre_l;   // the first cell's chunk (its loop iteration loads no rows)
+        lds[W::L_ROWF + lane] = pre_f;
+        lds[W::L_ROWT + lane] = pre_t;
+        if (lane == 0) lds[W::L_ROWT + 64] = pre_t64;
         GGP_PSTAMP(1);
         GGP_TL(1);
         lds[W::L_MONO + lane] = kap;   // the 33 kappas, one per lane (MONO is free here)
@@ -2957,16 +2822,6 @@ struct Shard {
     QChunk *d_qchunks = nullptr;
     unsigned *d_qctr = nullptr;
     bool lane_queue = true;            // GGP_LANE_QUEUE=0: level-by-level lane launches
-    // armed path launches (GGP_ARM=1; one shard, path launch): the next call's launch enqueued
-    // behind the current one, waiting at its door for the parameters (ArmHost in the mapped slots)
-    bool arm = false;
-    int64_t arm_k = 0;                 // the call the enqueued armed launch waits for (0: none)
-    bool arm_call = false;             // the pending call went through the door
-    ggp_params arm_params{};           // its parameters (a plain launch of them after an expiry)
-    volatile ArmHost *h_arm = nullptr;
-    bool arm_debug = false;
-    int64_t arm_calls = 0;        // calls that ran in an armed launch (ggp_arm)
-    double arm_dbg[5] = {0, 0, 0, 0, 0};   // GGP_ARM_DEBUG: summed block-0 stamp differences (us), calls
     int queue_resident = 1024;         // k_loglik_lane_queue workgroups the device holds at once
     // reduction (k_reduce_blocks): local trees in DFS order, the shard's blocks, global DFS ranks
     int64_t n_trees = 0, n_lblocks = 0;
@@ -3109,7 +2964,6 @@ struct ggp_forest {
     int64_t max_root_rows = 1;         // rows of the longest root cell (the chained launch's cap)
     int64_t chain_fallbacks = 0;       // chained calls finished call by call after a stall
 };
-
 
 namespace {
 
@@ -3287,57 +3141,6 @@ int shard_launch(Shard *s, const ggp_params &P)
     return GGP_OK;
 }
 
-// ---- armed path launches ------------------------------------------------------------------
-// the launch for the shard's next call (seq + 1, epoch + 1), enqueued behind whatever the stream
-// holds; its parameters come through the door (arm_wait)
-int arm_enqueue(Shard *s)
-{
-    ggp_params P0{};
-    hipLaunchKernelGGL((k_loglik_wave<false, true>), dim3((unsigned)s->n_paths), dim3(64), 0, s->stream, s->F, P0,
-                       s->d_path_cells, (int)s->n_cells, s->d_state, s->d_cell_ll, s->d_cell_nan, s->d_chain,
-                       s->d_cell_done, s->epoch + 1, s->d_path_seq, s->red, s->seq + 1, s->spin_max,
-                       (const double *)nullptr, (const double *)nullptr, (const int32_t *)nullptr);
-    if (hipGetLastError() != hipSuccess) {
-        s->arm_k = 0;
-        return GGP_EDEV;
-    }
-    s->arm_k = s->seq + 1;
-    return GGP_OK;
-}
-
-// the enqueued armed launch exits without evaluating (its door gets -k); the stream then drains
-void arm_quit(Shard *s)
-{
-    if (s->arm_k == 0) return;
-    s->h_arm->door = -s->arm_k;
-    s->arm_k = 0;
-}
-
-// every shard's armed launch leaves (an entry point other than the objective call needs the stream)
-void arm_quit_all(ggp_forest *f)
-{
-    if (!f) return;
-    for (Shard *s : f->shards) arm_quit(s);
-}
-
-// call k through the door of the armed launch waiting for it: the parameters, then the door
-void arm_ring(Shard *s, const ggp_params &P)
-{
-    for (int i = 0; i < 11; ++i) s->h_arm->params[i] = P.p[i];
-    std::atomic_thread_fence(std::memory_order_release);   // the parameters before the door
-    s->h_arm->door = s->arm_k;
-    s->arm_params = P;
-    s->arm_call = true;
-    s->arm_k = 0;
-    ++s->seq;     // launch_levels' bookkeeping for the path launch the armed kernel runs
-    ++s->epoch;
-    s->n_prof = 0;
-    s->used_path = true;
-    s->kernel_used = GGP_KERNEL_WAVE;
-    s->last_code = GGP_KERNEL_WAVE << 8 | 64;
-    s->seq_pending = true;
-}
-
 int shard_wait(Shard *s)
 {
     if (s->n_cells == 0) return GGP_OK;
@@ -3345,45 +3148,14 @@ int shard_wait(Shard *s)
     if (s->spin && s->seq_pending) {
         for (uint32_t it = 1;; ++it) {
             if (*s->h_seq == s->seq) { seen = true; break; }
-            if ((it & 1023) == 0) {
-                const bool drained = hipStreamQuery(s->stream) != hipErrorNotReady;
-                std::atomic_thread_fence(std::memory_order_acquire);   // the launch's stores, then their reads
-                if (s->arm_call && s->h_arm->expired == s->seq) {
-                    // the armed launch gave up before its door rang: the next call's armed launch
-                    // (behind it) leaves, this call runs as a plain launch (the next call is plain too,
-                    // and arms the one after it: a quit call number is never armed again)
-                    s->arm_call = false;
-                    arm_quit(s);
-                    --s->seq;
-                    --s->epoch;
-                    const int rc = shard_launch(s, s->arm_params);
-                    if (rc != GGP_OK) return rc;
-                    continue;
-                }
-                if (*s->h_seq == s->seq) { seen = true; break; }
-                if (drained) break;
-            }
+            if ((it & 1023) == 0 && hipStreamQuery(s->stream) != hipErrorNotReady) break;
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         if (seen && s->used_path && s->h_clk)   // the launch's counters, complete before its sequence number
             for (int k = 0; k < 4; ++k) s->clk_snap[k] = s->h_clk[k];
     }
     s->seq_pending = false;
-    if (s->arm_call && seen) {
-        ++s->arm_calls;
-        if (s->arm_debug) {   // entry -> poll, poll -> door, door -> slots, door -> the end (100 MHz)
-            const uint64_t e0 = s->h_arm->st[0], e1 = s->h_arm->st[1], e2 = s->h_arm->st[2], e3 = s->h_arm->st[3];
-            const uint64_t ee = s->h_clk[3];
-            s->arm_dbg[0] += (e1 - e0) / 100.0;
-            s->arm_dbg[1] += (e2 - e1) / 100.0;
-            s->arm_dbg[2] += (e3 - e2) / 100.0;
-            s->arm_dbg[3] += (ee - e2) / 100.0;
-            s->arm_dbg[4] += 1;
-        }
-    }
-    s->arm_call = false;
     if (!seen || s->profile) {
-        arm_quit(s);
         HIPCHK(hipSetDevice(s->device));
         HIPCHK(hipStreamSynchronize(s->stream));
     }
@@ -3642,8 +3414,6 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
     if (const char *e = getenv("GGP_PAIR_Q")) f->tune_pair_q = atoi(e) == 4 ? 4 : atoi(e) == 2 ? 2 : 0;
     if (const char *e = getenv("GGP_SMOOTHER_LANE")) f->smoother_lane = atoi(e) != 0;
     if (const char *e = getenv("GGP_LANE_QUEUE")) f->lane_queue = atoi(e) != 0;
-    if (const char *e = getenv("GGP_ARM")) f->arm = atoi(e) != 0;
-    if (const char *e = getenv("GGP_ARM_DEBUG")) f->arm_debug = atoi(e) != 0;
     if (const char *e = getenv("GGP_AUTO_SMALL"); e && !ggp::kExact)
         f->auto_small = std::string(e) == "group" ? GGP_KERNEL_GROUP : GGP_KERNEL_WAVE;
     f->row_off.assign(d->row_offset, d->row_offset + nc + 1);
@@ -3737,16 +3507,13 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
         check(dev_upload(&f->d_tree_dfs, tree_start.data(), tree_start.size()));
         check(dev_upload(&f->d_blk_t0, t0.data(), t0.size()));
         check(dev_upload(&f->d_blk_nt, blk_ntrees.data(), blk_ntrees.size()));
-        check(dev_upload<unsigned>(&f->d_done, nullptr, kDoneBytes / sizeof(unsigned)));   // the counter, then an armed launch's ArmDev slots
+        check(dev_upload<unsigned>(&f->d_done, nullptr, 1));
         check(dev_upload<double>(&f->d_blk_sum, nullptr, (size_t)std::max<int64_t>(1, f->n_lblocks)));
         check(dev_upload<int64_t>(&f->d_blk_nan, nullptr, (size_t)std::max<int64_t>(1, f->n_lblocks)));
-        if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, kDoneBytes) != hipSuccess) rc = GGP_EDEV;
-        static_assert(sizeof(ArmDev) <= 128 && kArmSlotStride % 128 == 0 && kArmDevOff >= 64 * sizeof(unsigned),
-                      "ArmDev slots after the counters, each in its own 128-byte line");
+        if (rc == GGP_OK && f->d_done && hipMemset(f->d_done, 0, sizeof(unsigned)) != hipSuccess) rc = GGP_EDEV;
     }
     if (rc == GGP_OK) {   // the result slots: pinned host memory the reduction writes over the bus
-        // + the launch clock's four counters and an armed launch's ArmHost (kArmHostSlots from clk)
-        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + kArmHostSlots;
+        const size_t slots = 2 * (size_t)f->n_lblocks + 1 + 4;   // + the launch clock's four counters
         void *h = nullptr, *m = nullptr;
         if (hipHostMalloc(&h, slots * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             rc = GGP_ENOMEM;
@@ -3763,9 +3530,6 @@ int shard_create(const ggp_forest_desc *d, DeviceCtx *dev, const std::vector<int
             f->h_clk = (volatile unsigned long long *)((char *)h + (2 * f->n_lblocks + 1) * sizeof(double));
             f->m_clk = (unsigned long long *)((char *)m + (2 * f->n_lblocks + 1) * sizeof(double));
             f->h_clk[0] = f->h_clk[1] = f->h_clk[2] = f->h_clk[3] = 0;
-            f->h_arm = reinterpret_cast<volatile ArmHost *>(const_cast<unsigned long long *>(f->h_clk) + kArmHostOff);
-            f->h_arm->door = 0;
-            f->h_arm->expired = 0;
         }
     }
     if (rc != GGP_OK) {
@@ -4298,7 +4062,6 @@ int ggp_comm_unique_id(const char *rccl_lib, unsigned char *id)
 int ggp_comm_attach(ggp_forest *f, const char *rccl_lib, int32_t nranks, int32_t rank, const unsigned char *id)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !id || nranks < 1 || rank < 0 || rank >= nranks) return GGP_EINVAL;
     if (f->comm) {
         g_last_err = "ggp_comm_attach: the handle is already attached";
@@ -4394,7 +4157,6 @@ int ggp_device_count(int32_t *n)
 void ggp_forest_destroy(ggp_forest *f)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f) return;
     if (Comm *c = f->comm) {
         if (!f->shards.empty()) {
@@ -4566,7 +4328,6 @@ int ggp_forest_shards(ggp_forest *f, int32_t *n, int32_t *device, int64_t *rows,
 int ggp_reset_state(ggp_forest *f)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -4580,7 +4341,6 @@ int ggp_reset_state(ggp_forest *f)
 int ggp_get_state(ggp_forest *f, double *out)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !out) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -4601,7 +4361,6 @@ int ggp_get_state(ggp_forest *f, double *out)
 int ggp_set_state(ggp_forest *f, const double *in)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !in) return GGP_EINVAL;
     for (Shard *s : f->shards) {
         if (!s->n_cells) continue;
@@ -4645,31 +4404,12 @@ int ggp_total_loglik_async(ggp_forest *f, const double *params)
     trace_finalize(f);   // before the next launch can overwrite the stamps
     ggp_params P;
     std::memcpy(P.p, params, sizeof P.p);
-    // an armed handle (GGP_ARM=1, one shard, a path launch, no events, no communicator): the call
-    // goes through the door of the launch enqueued behind the previous one
-    Shard *sa = f->shards.size() == 1 && !f->comm ? f->shards[0] : nullptr;
-    const bool use_arm = sa && sa->arm && sa->n_paths > 0 && !sa->profile && sa->spin && !wave_products_risky(sa, P.p);
-    if (!use_arm) {
-        arm_quit_all(f);
-    } else if (sa->arm_k != 0 && sa->arm_k != sa->seq + 1) {
-        arm_quit(sa);
-    }
-    if (use_arm && sa->arm_k != 0) {
-        arm_ring(sa, P);
-    } else {
-        for (Shard *s : f->shards) {   // every device enqueued before any is waited for
-            const int rc = shard_launch(s, P);
-            if (rc != GGP_OK) {
-                if (f->comm) comm_fail(f->comm);   // the peers would wait for this rank's all-gather
-                return rc;
-            }
+    for (Shard *s : f->shards) {   // every device enqueued before any is waited for
+        const int rc = shard_launch(s, P);
+        if (rc != GGP_OK) {
+            if (f->comm) comm_fail(f->comm);   // the peers would wait for this rank's all-gather
+            return rc;
         }
-    }
-    if (use_arm) {   // the next call's launch, enqueued while this one runs (not part of its enqueue)
-        f->tr_t1 = std::chrono::steady_clock::now();
-        (void)arm_enqueue(sa);
-        f->tr_pending = true;
-        return GGP_OK;
     }
     if (Comm *c = f->comm) {   // behind the evaluation: partial, all-gather, rank-order sum
         Shard *s = f->shards[0];
@@ -4846,29 +4586,6 @@ int ggp_loglik_result(ggp_forest *f, double *ll, int64_t *nan_cell, int64_t *nan
     return rc;
 }
 
-int ggp_arm(ggp_forest *f, int32_t on, int64_t *armed_calls)
-{
-    DeviceGuard device_guard_;   // the caller's current device is restored on return
-    if (!f) return GGP_EINVAL;
-    if (on >= 0) {
-        arm_quit_all(f);
-        for (Shard *s : f->shards) s->arm = on != 0;
-    }
-    for (Shard *s : f->shards)
-        if (s->arm_debug && s->arm_dbg[4] > 0) {
-            const double n = s->arm_dbg[4];
-            fprintf(stderr, "ggp arm: %.0f calls, block 0 mean us: entry->poll %.2f poll->door %.2f door->slots %.2f door->end %.2f\n",
-                    n, s->arm_dbg[0] / n, s->arm_dbg[1] / n, s->arm_dbg[2] / n, s->arm_dbg[3] / n);
-            for (double &v : s->arm_dbg) v = 0;
-        }
-    if (armed_calls) {
-        int64_t n = 0;
-        for (const Shard *s : f->shards) n += s->arm_calls;
-        *armed_calls = n;
-    }
-    return GGP_OK;
-}
-
 int ggp_call_trace(const ggp_forest *f, int32_t cap, double *out, int32_t *n)
 {
     if (!f || cap < 0 || (cap > 0 && !out)) return GGP_EINVAL;
@@ -4935,7 +4652,6 @@ static int64_t batch_reserve(ggp_forest *f, int32_t n_pts)
 int ggp_total_loglik_batch(ggp_forest *f, int32_t n_pts, const double *params, double *ll, int32_t *status)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || n_pts < 0 || (n_pts > 0 && (!params || !ll || !status))) {
         g_last_err = "ggp_total_loglik_batch: bad arguments";
         return GGP_EINVAL;
@@ -5125,7 +4841,6 @@ int ggp_total_loglik_chain(ggp_forest *f, int32_t n_pts, const double *params, d
                            int64_t *nan_cell, int64_t *nan_row)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || n_pts < 0 || !n_ok || (n_pts > 0 && (!params || !ll))) {
         g_last_err = "ggp_total_loglik_chain: bad arguments";
         return GGP_EINVAL;
@@ -5202,7 +4917,6 @@ int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, co
                           int32_t *status, int64_t *nan_cell, int64_t *nan_row)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || n_pts < 0 || (n_pts > 0 && (!params || !pred || !ll || !status))) {
         g_last_err = "ggp_total_loglik_tree: bad arguments";
         return GGP_EINVAL;
@@ -5248,7 +4962,6 @@ int ggp_total_loglik_tree(ggp_forest *f, int32_t n_pts, const double *params, co
 int ggp_keep_point_state(ggp_forest *f, int32_t point)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || point < 0 || point >= f->tree_pts) {
         g_last_err = "ggp_keep_point_state: no such point of the last ggp_total_loglik_tree call";
         return GGP_EINVAL;
@@ -5266,7 +4979,6 @@ int ggp_keep_point_state(ggp_forest *f, int32_t point)
 int ggp_last_launch_profile(ggp_forest *ff, float *ms, int64_t *rows, int32_t *kernel, int32_t cap, int32_t *n)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(ff);   // (an armed launch would hold the stream)
     if (!ff || !n || ff->shards.empty()) return GGP_EINVAL;
     Shard *f = ff->shards[0];   // the first shard's launches
     if (cap < 0) {   // switch the events off again (the spin wait returns)
@@ -5325,7 +5037,6 @@ int ggp_forest_info(ggp_forest *f, int64_t *n_levels, int64_t *max_level_cells, 
 int ggp_predict_profile(ggp_forest *f, float *ms_smooth, float *ms_combine)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f) return GGP_EINVAL;
     // per device: its shards run one after another; report the slowest device
     float best_a = 0, best_b = 0;
@@ -5357,7 +5068,6 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
                 double *out_comb)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !params || n_seg < 1) { g_last_err = "ggp_predict: null params or n_seg < 1"; return GGP_EINVAL; }
     if (f->n_cells == 0) return GGP_OK;
     // ---- workspaces ----
@@ -5470,7 +5180,6 @@ int ggp_predict(ggp_forest *f, const double *params, int32_t n_seg, double *out_
 int ggp_predict_rows(ggp_forest *f, int64_t r_lo, int64_t r_hi, double *out)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !out || r_lo < 0 || r_hi > f->n_rows || r_hi < r_lo) {
         g_last_err = "ggp_predict_rows: bad arguments";
         return GGP_EINVAL;
@@ -5499,7 +5208,6 @@ static int joints_impl(ggp_forest *f, const double *params, int32_t n_seg, doubl
                        int64_t cap, int64_t *out_idx, double *out_val, int64_t *n_out, int width)
 {
     DeviceGuard device_guard_;   // the caller's current device is restored on return
-    arm_quit_all(f);   // (an armed launch would hold the stream)
     if (!f || !params || n_seg < 1 || !n_out) { g_last_err = "ggp_joints: bad arguments"; return GGP_EINVAL; }
     if (r_lo < 0) r_lo = 0;
     if (r_hi > f->n_rows) r_hi = f->n_rows;

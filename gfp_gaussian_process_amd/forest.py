@@ -489,15 +489,6 @@ class Forest:
                                               int(rank), bytes(uid)))
         self._comm_rank = int(rank)
 
-    def arm(self, on: bool | None = True) -> int:
-        """armed objective calls (ggp_arm, include/ggp.h): each call enqueues the next call's launch,
-        which stages its tables and waits for the parameters; bitwise the plain calls.  Only while
-        this handle is the device's only user; arm(False) releases the device, arm(None) changes
-        nothing.  Returns the calls so far that ran in an armed launch"""
-        n = ctypes.c_int64()
-        self._check(self._lib.ggp_arm(self._h, -1 if on is None else int(bool(on)), ctypes.byref(n)))
-        return n.value
-
     def launch_clock(self):
         """(shader MHz, window us) of the last path launch's block 0 (ggp_launch_clock), or None"""
         mhz, us = ctypes.c_double(), ctypes.c_double()

@@ -275,19 +275,6 @@ int32_t ggp_comm_nan_rank(const ggp_forest *f);   /* first NaN rank of the last 
  * block 0 measured it over its path: s_memtime cycles per s_memrealtime tick (100 MHz) -- the
  * DVFS clock of a real evaluation, for a benchmark line.  GGP_EINVAL if none ran on this handle. */
 int ggp_launch_clock(const ggp_forest *f, double *shader_mhz, double *window_us);
-/* Armed objective calls (opt-in; GGP_ARM=1 at creation does the same): on a handle of one shard
- * whose forest takes the single path launch, each ggp_total_loglik_async enqueues the NEXT call's
- * launch behind its own.  That launch stages the call-independent tables and waits (up to 50 ms)
- * for its parameters, which the next call writes to mapped host memory before ringing its door,
- * so a call's launch, dispatch and table staging overlap the previous call.  Results are bitwise
- * the plain launches'.  An armed launch holds the device's compute units while it waits: any other
- * entry point on the handle, a call whose parameters need another schedule, a profiling window or
- * on = 0 makes it leave at once; other handles' work on the same device waits for it (50 ms at
- * most), so arm a handle only while it is the device's only user.  on < 0 leaves the setting;
- * armed_calls (nullable): the handle's calls so far that ran in an armed launch (an expired launch's
- * call ran as a plain one and is not counted). */
-int ggp_arm(ggp_forest *f, int32_t on, int64_t *armed_calls);
-
 /* The host split of the handle's last objective calls (ggp_total_loglik, or ggp_total_loglik_async +
  * ggp_loglik_result), for a benchmark line: out[6i..6i+5] for the last *n = min(calls, cap, 512)
  * calls, oldest first = (enqueue_us: entry to the launches enqueued, wait_us: enqueued to the
