@@ -1607,7 +1607,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             const double v = lds[W::L_POST + lane];
             if (publish)
                 st_agent(state + (size_t)20 * c + lane, v);
-            else
+            else if (i + 1 != i_hi)   // (the path's last cell: stored after the reduction's count)
                 state[(size_t)20 * c + lane] = v;
         }
         if (publish) {
@@ -1627,7 +1627,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         __hip_atomic_store(red.clk + 1, r1 - clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(red.clk + 2, clk_r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    // the path's last cell's state: nothing in this launch reads it unless it was published above
+    // (then this stores the same values again), so its store is issued after the reduction's count
+    // and its completion is no part of the wait in front of that count
+    const int c_last = cells[i_hi - 1];
+    const double v_last = lane < 20 ? lds[W::L_POST + lane] : 0.0;
     if (red.n_lblocks > 0) chain_reduce(red, red_unpark(lds + W::L_RED, lane), call_seq, lane, cell_ll, cell_nan, lds + W::L_RX0);
+    if (lane < 20) state[(size_t)20 * c_last + lane] = v_last;
     GGP_TL(6);
     GGP_TL_CNT_FLUSH();
 }
